@@ -1,0 +1,302 @@
+"""
+amvpt -- Python front end of the MI355X-native AMVPT (`mvpath`) integrator.
+
+A thin ctypes layer over the two in-tree native libraries:
+
+* ``lib/libamvpt_hip.so``  -- the drop-in C-ABI of the hot path (include/amvpt.h),
+  hand-written HIP kernels for gfx950;
+* ``lib/libamvpt_host.so`` -- the Mitsuba-style host framework (XML scene subset,
+  Properties, plugins, ``Integrator::render``) built on that C-ABI.
+
+The surface mirrors the reference's Python API for the path
+(``mi.load_file``, ``mi.load_string``, ``mi.render``, ``Bitmap.write``;
+reference: src/python/python/__init__.py / src/render/python).  There is no
+CPU fallback: rendering without a visible GPU raises ``RuntimeError``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(_HERE), "lib")
+HIP_LIB_PATH = os.path.join(LIB_DIR, "libamvpt_hip.so")
+HOST_LIB_PATH = os.path.join(LIB_DIR, "libamvpt_host.so")
+
+u32, i32, u64, f32, f64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_float, ctypes.c_double
+
+
+class ShapeDesc(ctypes.Structure):
+    _fields_ = [("type", u32), ("bsdf", i32), ("emitter", i32), ("flip_normals", u32),
+                ("to_world", f32 * 16), ("to_object", f32 * 16),
+                ("vertex_count", u32), ("face_count", u32),
+                ("positions", ctypes.POINTER(f32)), ("normals", ctypes.POINTER(f32)),
+                ("texcoords", ctypes.POINTER(f32)), ("faces", ctypes.POINTER(u32)),
+                ("center", f32 * 3), ("radius", f32)]
+
+
+class BsdfDesc(ctypes.Structure):
+    _fields_ = [("type", u32), ("nested", i32 * 2), ("reflectance", f32 * 3), ("distribution", u32),
+                ("sample_visible", u32), ("alpha_u", f32), ("alpha_v", f32), ("eta", f32 * 3),
+                ("k", f32 * 3), ("has_specular_reflectance", u32), ("specular_reflectance", f32 * 3)]
+
+
+class EmitterDesc(ctypes.Structure):
+    _fields_ = [("type", u32), ("shape", i32), ("radiance", f32 * 3), ("sampling_weight", f32)]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("shapes", ctypes.POINTER(ShapeDesc)), ("shape_count", u32),
+                ("bsdfs", ctypes.POINTER(BsdfDesc)), ("bsdf_count", u32),
+                ("emitters", ctypes.POINTER(EmitterDesc)), ("emitter_count", u32),
+                ("has_environment", u32)]
+
+
+class ViewDesc(ctypes.Structure):
+    _fields_ = [("type", u32), ("to_world", f32 * 16), ("to_world_inv", f32 * 16),
+                ("sample_to_camera", f32 * 16), ("camera_to_sample", f32 * 16),
+                ("near_clip", f32), ("far_clip", f32), ("normalization", f32),
+                ("resolution", f32 * 2), ("pp_offset", f32 * 2),
+                ("aperture_radius", f32), ("focus_distance", f32)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, u32) for n in (
+        "integrator", "max_depth", "rr_depth", "hide_emitters", "sa_reuse", "sa_mis", "fast_mis",
+        "debug", "adaptive", "spp_pass_lim", "reuse_count", "spp", "seed", "base_seed", "n_views",
+        "multisensor", "grid_x", "grid_y", "reverse_x", "reverse_y", "film_width", "film_height",
+        "film_alpha", "rfilter")] + [("rfilter_stddev", f32)]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [("lanes", u64), ("passes", u64), ("vertices", u64), ("reuse_lanes", u64),
+                ("visibility_rays", u64), ("view_splats", u64), ("adaptive_lanes", u64),
+                ("kernel_ms_primary", f64), ("kernel_ms_bounce", f64), ("kernel_ms_splat", f64),
+                ("total_ms", f64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+INTEGRATOR_MVPATH, INTEGRATOR_PATH = 0, 1
+_hip = None
+_host = None
+
+
+def hip_lib():
+    """Load libamvpt_hip.so (the C-ABI of the hot path); raises if it was not built."""
+    global _hip
+    if _hip is None:
+        if not os.path.exists(HIP_LIB_PATH):
+            raise RuntimeError("libamvpt_hip.so missing: run `make -C mitsuba3-amvpt_amd` "
+                               "(__graft_entry__.build()); the product path has no fallback")
+        L = ctypes.CDLL(HIP_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        L.amvpt_last_error.restype = ctypes.c_char_p
+        L.amvpt_abi_version.restype = u32
+        L.amvpt_film_channels.restype = u32
+        for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
+                   "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
+                   "amvpt_develop", "amvpt_set_chunk_lanes"):
+            getattr(L, fn).restype = ctypes.c_int
+        L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Counters)]
+        L.amvpt_render_records.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u32, u64,
+                                           u64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.amvpt_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.POINTER(ctypes.c_void_p)]
+        L.amvpt_scene_destroy.argtypes = [ctypes.c_void_p]
+        L.amvpt_scene_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+        L.amvpt_plan.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                 ctypes.POINTER(u32), ctypes.POINTER(u64)]
+        L.amvpt_develop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u32, u32, u32, ctypes.c_void_p]
+        L.amvpt_set_chunk_lanes.argtypes = [u64]
+        L.amvpt_set_device.argtypes = [ctypes.c_int]
+        L.amvpt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        _hip = L
+    return _hip
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        hip_lib()
+        if not os.path.exists(HOST_LIB_PATH):
+            raise RuntimeError("libamvpt_host.so missing: run `make -C mitsuba3-amvpt_amd`")
+        L = ctypes.CDLL(HOST_LIB_PATH)
+        L.amvpt_host_last_error.restype = ctypes.c_char_p
+        L.amvpt_host_load_file.restype = ctypes.c_void_p
+        L.amvpt_host_load_string.restype = ctypes.c_void_p
+        L.amvpt_host_load_file.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.amvpt_host_load_string.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.amvpt_host_scene_free.argtypes = [ctypes.c_void_p]
+        L.amvpt_host_sensor_count.argtypes = [ctypes.c_void_p]
+        L.amvpt_host_sensor_count.restype = u32
+        L.amvpt_host_film_info.argtypes = [ctypes.c_void_p, u32] + [ctypes.POINTER(u32)] * 4
+        L.amvpt_host_render.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.POINTER(Counters)]
+        L.amvpt_host_describe.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.POINTER(ctypes.POINTER(SceneDesc)),
+                                          ctypes.POINTER(ctypes.POINTER(ViewDesc)), ctypes.POINTER(Params)]
+        L.amvpt_host_integrator_string.argtypes = [ctypes.c_void_p]
+        L.amvpt_host_integrator_string.restype = ctypes.c_char_p
+        L.amvpt_host_write_exr.argtypes = [ctypes.c_char_p, ctypes.c_void_p, u32, u32, u32]
+        L.amvpt_host_read_exr.argtypes = [ctypes.c_char_p, ctypes.c_void_p, u32, u32, u32]
+        L.amvpt_host_parse_fov.argtypes = [f64, ctypes.c_char_p, ctypes.c_char_p, f64]
+        L.amvpt_host_parse_fov.restype = f64
+        L.amvpt_host_perspective_projection.argtypes = [ctypes.POINTER(ctypes.c_int)] * 3 + [f32, f32, f32,
+                                                                                              ctypes.POINTER(f32)]
+        _host = L
+    return _host
+
+
+def _defines(kw):
+    keys = [k.encode() for k in kw]
+    vals = [str(v).encode() for v in kw.values()]
+    K = (ctypes.c_char_p * max(1, len(keys)))(*keys)
+    V = (ctypes.c_char_p * max(1, len(vals)))(*vals)
+    return K, V, len(keys)
+
+
+def _check(rc, lib):
+    if rc != 0:
+        raise RuntimeError((lib.amvpt_host_last_error() if lib is _host else lib.amvpt_last_error()).decode())
+
+
+class Scene:
+    """A loaded scene (Scene + its sensors/integrator), as `mi.load_file` returns."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self._lib = host_lib()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.amvpt_host_scene_free(self._h)
+            self._h = None
+
+    def sensor_count(self):
+        return self._lib.amvpt_host_sensor_count(self._h)
+
+    def film_info(self, sensor=0):
+        w, h, c, s = u32(), u32(), u32(), u32()
+        _check(self._lib.amvpt_host_film_info(self._h, sensor, w, h, c, s), self._lib)
+        return w.value, h.value, c.value, s.value
+
+    def integrator_string(self):
+        return self._lib.amvpt_host_integrator_string(self._h).decode()
+
+    def describe(self, sensor=0, seed=0, spp=0):
+        """(SceneDesc*, ViewDesc*, Params) exactly as render() passes them to the C-ABI."""
+        sd = ctypes.POINTER(SceneDesc)()
+        vd = ctypes.POINTER(ViewDesc)()
+        p = Params()
+        _check(self._lib.amvpt_host_describe(self._h, sensor, seed, spp, ctypes.byref(sd), ctypes.byref(vd),
+                                             ctypes.byref(p)), self._lib)
+        return sd, vd, p
+
+
+def load_file(path, **defines):
+    L = host_lib()
+    K, V, n = _defines(defines)
+    h = L.amvpt_host_load_file(path.encode(), K, V, n)
+    if not h:
+        raise RuntimeError(L.amvpt_host_last_error().decode())
+    return Scene(h)
+
+
+def load_string(xml, **defines):
+    L = host_lib()
+    K, V, n = _defines(defines)
+    h = L.amvpt_host_load_string(xml.encode(), K, V, n)
+    if not h:
+        raise RuntimeError(L.amvpt_host_last_error().decode())
+    return Scene(h)
+
+
+def render(scene, sensor=0, seed=0, spp=0, raw=False, counters=None):
+    """Integrator::render(scene, sensor, seed, spp, develop=not raw) -> numpy (H, W, C)."""
+    w, h, c, _ = scene.film_info(sensor)
+    _, _, p = scene.describe(sensor, seed, spp)
+    ch = (5 if p.film_alpha else 4) if raw else c
+    out = np.zeros((h, w, ch), dtype=np.float32)
+    cnt = counters if counters is not None else Counters()
+    _check(scene._lib.amvpt_host_render(scene._h, sensor, seed, spp, 1 if raw else 0,
+                                        out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cnt)), scene._lib)
+    return out
+
+
+def plan(params):
+    L = hip_lib()
+    spp, spl, npass, lanes = u32(), u32(), u32(), u64()
+    _check(L.amvpt_plan(ctypes.byref(params), spp, spl, npass, lanes), L)
+    return spp.value, spl.value, npass.value, lanes.value
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    hip_lib().amvpt_device_count(ctypes.byref(n))
+    return n.value
+
+
+def write_exr(path, img):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    h, w, c = img.shape
+    L = host_lib()
+    _check(L.amvpt_host_write_exr(path.encode(), img.ctypes.data_as(ctypes.c_void_p), w, h, c), L)
+
+
+def read_exr(path, width, height, channels):
+    out = np.zeros((height, width, channels), dtype=np.float32)
+    L = host_lib()
+    _check(L.amvpt_host_read_exr(path.encode(), out.ctypes.data_as(ctypes.c_void_p), width, height, channels), L)
+    return out
+
+
+def parse_fov(fov=0.0, fov_axis=None, focal_length=None, aspect=1.0):
+    L = host_lib()
+    r = L.amvpt_host_parse_fov(float(fov), fov_axis.encode() if fov_axis else None,
+                               focal_length.encode() if focal_length else None, float(aspect))
+    if r < 0:
+        raise RuntimeError(L.amvpt_host_last_error().decode())
+    return r
+
+
+def perspective_projection(film_size, crop_size, crop_offset, fov_x, near_clip, far_clip):
+    L = host_lib()
+    I3 = ctypes.c_int * 2
+    m = (f32 * 16)()
+    L.amvpt_host_perspective_projection(I3(*film_size), I3(*crop_size), I3(*crop_offset), fov_x, near_clip,
+                                        far_clip, m)
+    return np.array(m[:], dtype=np.float32).reshape(4, 4)
+
+
+class DeviceScene:
+    """Direct handle on the C-ABI: amvpt_scene_create over host descriptors (bench / tests)."""
+
+    def __init__(self, scene_desc_ptr):
+        self._lib = hip_lib()
+        h = ctypes.c_void_p()
+        _check(self._lib.amvpt_scene_create(scene_desc_ptr, ctypes.byref(h)), self._lib)
+        self.h = h
+
+    def stats(self):
+        n, p = u32(), u32()
+        _check(self._lib.amvpt_scene_stats(self.h, n, p), self._lib)
+        return n.value, p.value
+
+    def render(self, views_ptr, params, film_ptr, lane_begin=0, lane_end=2 ** 64 - 1, stream=None,
+               counters=None):
+        cnt = counters if counters is not None else Counters()
+        _check(self._lib.amvpt_render(self.h, views_ptr, ctypes.byref(params), lane_begin, lane_end,
+                                      ctypes.c_void_p(film_ptr), ctypes.c_void_p(stream), ctypes.byref(cnt)),
+               self._lib)
+        return cnt
+
+    def render_records(self, views_ptr, params, film_ptr, records_ptr, pass_index=0, lane_begin=0,
+                       lane_end=2 ** 64 - 1, stream=None):
+        _check(self._lib.amvpt_render_records(self.h, views_ptr, ctypes.byref(params), pass_index, lane_begin,
+                                              lane_end, ctypes.c_void_p(film_ptr), ctypes.c_void_p(records_ptr),
+                                              ctypes.c_void_p(stream)), self._lib)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._lib.amvpt_scene_destroy(self.h)
+            self.h = None

@@ -1,0 +1,480 @@
+/*
+ * amvpt_capi.cpp -- C-ABI of libamvpt_hip.so (include/amvpt.h).
+ *
+ * Scene upload replaces the reference's Scene constructor + Embree BVH build
+ * (src/render/scene.cpp:30-96, src/render/scene_embree.inl:114-116): the host
+ * builds a binned-SAH binary BVH over rectangles, triangles and spheres, lays
+ * out the primitives in BVH order and uploads the small read-only tables once.
+ * The product path has no CPU fallback: without a GPU every render entry
+ * point returns AMVPT_ERR_NO_DEVICE.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace amvpt {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+amvpt_status hip_fail(const char *what, int err) {
+    g_err = std::string(what) + ": " + hipGetErrorString((hipError_t) err);
+    return err == (int) hipErrorOutOfMemory ? AMVPT_ERR_OOM : AMVPT_ERR_HIP;
+}
+
+/* ---- host arithmetic for per-shape constants (same sequences as the kernels) ---- */
+static inline float hdot(const float *a, const float *b) { return std::fmaf(a[2], b[2], std::fmaf(a[1], b[1], a[0] * b[0])); }
+static inline void hvec(const float *m, const float *v, float *o) { /* Transform4f * Vector3f */
+    for (int i = 0; i < 3; ++i) o[i] = std::fmaf(m[i * 4 + 2], v[2], std::fmaf(m[i * 4 + 1], v[1], m[i * 4 + 0] * v[0]));
+}
+static inline void hpoint(const float *m, const float *p, float *o) { /* transform_affine(Point3f) */
+    for (int i = 0; i < 3; ++i)
+        o[i] = std::fmaf(m[i * 4 + 2], p[2], std::fmaf(m[i * 4 + 1], p[1], std::fmaf(m[i * 4 + 0], p[0], m[i * 4 + 3])));
+}
+static inline void hcross(const float *a, const float *b, float *o) {
+    o[0] = std::fmaf(a[1], b[2], -(a[2] * b[1]));
+    o[1] = std::fmaf(a[2], b[0], -(a[0] * b[2]));
+    o[2] = std::fmaf(a[0], b[1], -(a[1] * b[0]));
+}
+
+/* ---------------------------------------------------------------- */
+/* Binned SAH BVH                                                    */
+/* ---------------------------------------------------------------- */
+
+struct Box {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const float *p) { for (int i = 0; i < 3; ++i) { lo[i] = std::min(lo[i], p[i]); hi[i] = std::max(hi[i], p[i]); } }
+    void grow(const Box &b) { grow(b.lo); grow(b.hi); }
+    float area() const {
+        float d[3];
+        for (int i = 0; i < 3; ++i) d[i] = std::max(hi[i] - lo[i], 0.f);
+        return 2.f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+    bool empty() const { return lo[0] > hi[0]; }
+};
+
+struct BuildPrim { Box box; float c[3]; uint32_t idx; };
+
+struct Builder {
+    std::vector<BuildPrim> &prims;
+    std::vector<DNode> nodes;
+    explicit Builder(std::vector<BuildPrim> &p) : prims(p) {}
+
+    static void pad(Box &b) {
+        float m = 0.f;
+        for (int i = 0; i < 3; ++i) m = std::max(m, std::max(std::fabs(b.lo[i]), std::fabs(b.hi[i])));
+        float e = 1e-4f * (1.f + m);
+        for (int i = 0; i < 3; ++i) { b.lo[i] -= e; b.hi[i] += e; }
+    }
+    void set(uint32_t ni, const Box &b) {
+        Box pb = b;
+        pad(pb);
+        for (int i = 0; i < 3; ++i) { nodes[ni].lo[i] = pb.lo[i]; nodes[ni].hi[i] = pb.hi[i]; }
+    }
+    void build(uint32_t ni, uint32_t begin, uint32_t end, int depth) {
+        Box b, cb;
+        for (uint32_t i = begin; i < end; ++i) { b.grow(prims[i].box); cb.grow(prims[i].c); }
+        set(ni, b);
+        uint32_t n = end - begin;
+        if (n <= 2 || depth >= 40) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
+        const int NB = 16;
+        float best_cost = INFINITY;
+        int best_axis = -1, best_split = -1;
+        for (int ax = 0; ax < 3; ++ax) {
+            float ext = cb.hi[ax] - cb.lo[ax];
+            if (!(ext > 0.f)) continue;
+            Box bins[NB];
+            uint32_t cnt[NB] = {0};
+            for (uint32_t i = begin; i < end; ++i) {
+                int k = std::min(NB - 1, (int) (NB * (prims[i].c[ax] - cb.lo[ax]) / ext));
+                bins[k].grow(prims[i].box);
+                cnt[k]++;
+            }
+            Box lb[NB], rb[NB];
+            uint32_t lc[NB], rc[NB];
+            Box acc;
+            uint32_t ac = 0;
+            for (int k = 0; k < NB; ++k) { if (cnt[k]) acc.grow(bins[k]); ac += cnt[k]; lb[k] = acc; lc[k] = ac; }
+            acc = Box();
+            ac = 0;
+            for (int k = NB - 1; k >= 0; --k) { if (cnt[k]) acc.grow(bins[k]); ac += cnt[k]; rb[k] = acc; rc[k] = ac; }
+            for (int k = 0; k < NB - 1; ++k) {
+                if (!lc[k] || !rc[k + 1]) continue;
+                float cost = lb[k].area() * lc[k] + rb[k + 1].area() * rc[k + 1];
+                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = k; }
+            }
+        }
+        float leaf_cost = b.area() * n;
+        if (best_axis < 0 || (n <= 4 && best_cost >= leaf_cost)) {
+            if (best_axis < 0) {
+                /* degenerate centroids: median split on the index */
+                if (n <= 4) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
+                uint32_t mid = begin + n / 2;
+                uint32_t l = (uint32_t) nodes.size();
+                nodes.resize(nodes.size() + 2);
+                nodes[ni].left_or_first = l; nodes[ni].count = 0;
+                build(l, begin, mid, depth + 1);
+                build(l + 1, mid, end, depth + 1);
+                return;
+            }
+            nodes[ni].left_or_first = begin; nodes[ni].count = n;
+            return;
+        }
+        float ext = cb.hi[best_axis] - cb.lo[best_axis];
+        auto it = std::partition(prims.begin() + begin, prims.begin() + end, [&](const BuildPrim &p) {
+            int k = std::min(NB - 1, (int) (NB * (p.c[best_axis] - cb.lo[best_axis]) / ext));
+            return k <= best_split;
+        });
+        uint32_t mid = (uint32_t) (it - prims.begin());
+        if (mid == begin || mid == end) mid = begin + n / 2;
+        uint32_t l = (uint32_t) nodes.size();
+        nodes.resize(nodes.size() + 2);
+        nodes[ni].left_or_first = l; nodes[ni].count = 0;
+        build(l, begin, mid, depth + 1);
+        build(l + 1, mid, end, depth + 1);
+    }
+};
+
+static bool device_ok() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+static uint32_t leaf_flags(const amvpt_bsdf_desc &d) {
+    if (d.type == AMVPT_BSDF_DIFFUSE) return 0x2u | 0x8000u;
+    uint32_t f = 0x8u | 0x8000u;
+    if (d.alpha_u != d.alpha_v) f |= 0x1000u;
+    return f;
+}
+
+} // namespace amvpt
+
+using namespace amvpt;
+
+extern "C" {
+
+const char *amvpt_last_error(void) { return g_err.c_str(); }
+uint32_t amvpt_abi_version(void) { return AMVPT_ABI_VERSION; }
+
+amvpt_status amvpt_device_count(int *count) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (count) *count = n;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_set_device(int device) {
+    if (!device_ok()) { set_error("no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", (int) e);
+    return AMVPT_OK;
+}
+
+uint32_t amvpt_film_channels(const amvpt_params *p) { return p && p->film_alpha ? 5u : 4u; }
+
+amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes) {
+    if (chunk_lanes) g_chunk_lanes = std::max<uint64_t>(256, chunk_lanes);
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_plan(const amvpt_params *P, uint32_t *spp, uint32_t *spp_pp, uint32_t *n_passes,
+                        uint64_t *lanes) {
+    if (!P) { set_error("amvpt_plan: null params"); return AMVPT_ERR_INVALID; }
+    uint32_t s = P->spp ? P->spp : 1, spl;
+    uint32_t np;
+    if (P->integrator == AMVPT_INTEGRATOR_MVPATH) {
+        spl = P->spp_pass_lim ? std::min(P->spp_pass_lim, s) : s;
+        np = s / spl;
+        s = np * spl;
+    } else {
+        spl = s;
+        np = 1;
+    }
+    uint64_t wf = (uint64_t) P->film_width * P->film_height * spl;
+    if (wf > 0xffffffffull) {
+        spl /= (uint32_t) ((wf + 0xffffffffull - 1) / 0xffffffffull);
+        np = s / spl;
+        wf = (uint64_t) P->film_width * P->film_height * spl;
+    }
+    if (spp) *spp = s;
+    if (spp_pp) *spp_pp = spl;
+    if (n_passes) *n_passes = np;
+    if (lanes) *lanes = wf;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
+    if (!d || !out) { set_error("amvpt_scene_create: null argument"); return AMVPT_ERR_INVALID; }
+    *out = nullptr;
+    if (!device_ok()) { set_error("amvpt_scene_create: no HIP device visible (the product path has no CPU fallback)"); return AMVPT_ERR_NO_DEVICE; }
+    if (d->has_environment) { set_error("environment emitters are outside the implemented path"); return AMVPT_ERR_UNSUPPORTED; }
+    /* validate */
+    for (uint32_t i = 0; i < d->bsdf_count; ++i) {
+        const amvpt_bsdf_desc &b = d->bsdfs[i];
+        if (b.type == AMVPT_BSDF_ROUGHCONDUCTOR &&
+            (b.distribution != AMVPT_MICROFACET_GGX || (!b.sample_visible && b.alpha_u != b.alpha_v))) {
+            set_error("roughconductor: only the GGX distribution (isotropic, or with visible-normal sampling) is implemented");
+            return AMVPT_ERR_UNSUPPORTED;
+        }
+        if (b.type == AMVPT_BSDF_TWOSIDED) {
+            for (int k = 0; k < 2; ++k) {
+                int32_t nb = b.nested[k];
+                if (nb < 0 || (uint32_t) nb >= d->bsdf_count || d->bsdfs[nb].type == AMVPT_BSDF_TWOSIDED) {
+                    set_error("twosided: invalid nested BSDF");
+                    return AMVPT_ERR_INVALID;
+                }
+            }
+        } else if (b.type > AMVPT_BSDF_TWOSIDED) {
+            set_error("unknown BSDF type");
+            return AMVPT_ERR_INVALID;
+        }
+    }
+    for (uint32_t i = 0; i < d->emitter_count; ++i) {
+        const amvpt_emitter_desc &e = d->emitters[i];
+        if (e.shape < 0 || (uint32_t) e.shape >= d->shape_count) { set_error("emitter without a valid shape"); return AMVPT_ERR_INVALID; }
+        if (d->shapes[e.shape].type == AMVPT_SHAPE_MESH) { set_error("area emitters on meshes are not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+        if (e.sampling_weight != 1.f) { set_error("non-uniform emitter sampling weights are not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+    }
+
+    std::vector<DShape> shapes(d->shape_count);
+    std::vector<float> vpos, vnrm, vuv;
+    std::vector<uint32_t> faces;
+    std::vector<BuildPrim> bprims;
+    std::vector<DPrim> scene_prims; /* scene order */
+    for (uint32_t i = 0; i < d->shape_count; ++i) {
+        const amvpt_shape_desc &s = d->shapes[i];
+        DShape &o = shapes[i];
+        std::memset(&o, 0, sizeof(o));
+        o.type = s.type;
+        o.flip = s.flip_normals;
+        o.bsdf = s.bsdf;
+        o.emitter = s.emitter;
+        std::memcpy(o.to_world, s.to_world, 12 * sizeof(float));
+        std::memcpy(o.to_object, s.to_object, 12 * sizeof(float));
+        if (s.bsdf < 0 || (uint32_t) s.bsdf >= d->bsdf_count) { set_error("shape without a valid BSDF"); return AMVPT_ERR_INVALID; }
+        if (s.type == AMVPT_SHAPE_RECTANGLE) {
+            /* Rectangle::update (rectangle.cpp:112-123) */
+            const float ex[3] = {2.f, 0.f, 0.f}, ey[3] = {0.f, 2.f, 0.f};
+            hvec(s.to_world, ex, o.frame_s);
+            hvec(s.to_world, ey, o.frame_t);
+            /* normal through inverse_transpose = transpose(to_object) */
+            float nn[3];
+            for (int r = 0; r < 3; ++r)
+                nn[r] = std::fmaf(s.to_object[2 * 4 + r], 1.f, std::fmaf(s.to_object[1 * 4 + r], 0.f, s.to_object[0 * 4 + r] * 0.f));
+            float inv = 1.f / std::sqrt(hdot(nn, nn));
+            for (int r = 0; r < 3; ++r) o.frame_n[r] = nn[r] * inv;
+            float cr[3];
+            hcross(o.frame_s, o.frame_t, cr);
+            o.inv_area = 1.f / std::sqrt(hdot(cr, cr));
+            DPrim p{};
+            std::memcpy(p.a, s.to_object + 0, 16);
+            std::memcpy(p.b, s.to_object + 4, 16);
+            std::memcpy(p.c, s.to_object + 8, 16);
+            p.type = PRIM_RECT; p.shape = i; p.face = 0;
+            BuildPrim bp;
+            const float corners[4][3] = {{-1, -1, 0}, {-1, 1, 0}, {1, -1, 0}, {1, 1, 0}};
+            for (auto &c : corners) { float w[3]; hpoint(s.to_world, c, w); bp.box.grow(w); }
+            p.pad = (uint32_t) scene_prims.size();
+            scene_prims.push_back(p);
+            bp.idx = p.pad;
+            for (int k = 0; k < 3; ++k) bp.c[k] = 0.5f * (bp.box.lo[k] + bp.box.hi[k]);
+            bprims.push_back(bp);
+        } else if (s.type == AMVPT_SHAPE_MESH) {
+            if (!s.positions || !s.faces) { set_error("mesh without positions/faces"); return AMVPT_ERR_INVALID; }
+            o.vbase = (uint32_t) (vpos.size() / 3);
+            o.fbase = (uint32_t) (faces.size() / 3);
+            o.has_normals = s.normals != nullptr;
+            o.has_uv = s.texcoords != nullptr;
+            vpos.insert(vpos.end(), s.positions, s.positions + 3 * (size_t) s.vertex_count);
+            if (s.normals) {
+                vnrm.resize(vpos.size() - 3 * (size_t) s.vertex_count, 0.f);
+                vnrm.insert(vnrm.end(), s.normals, s.normals + 3 * (size_t) s.vertex_count);
+            }
+            if (s.texcoords) {
+                vuv.resize(2 * (vpos.size() / 3 - s.vertex_count), 0.f);
+                vuv.insert(vuv.end(), s.texcoords, s.texcoords + 2 * (size_t) s.vertex_count);
+            }
+            faces.insert(faces.end(), s.faces, s.faces + 3 * (size_t) s.face_count);
+            for (uint32_t f = 0; f < s.face_count; ++f) {
+                DPrim p{};
+                const float *P0 = s.positions + 3 * s.faces[3 * f], *P1 = s.positions + 3 * s.faces[3 * f + 1],
+                            *P2 = s.positions + 3 * s.faces[3 * f + 2];
+                for (int k = 0; k < 3; ++k) { p.a[k] = P0[k]; p.b[k] = P1[k]; p.c[k] = P2[k]; }
+                p.type = PRIM_TRI; p.shape = i; p.face = f;
+                p.pad = (uint32_t) scene_prims.size();
+                BuildPrim bp;
+                bp.box.grow(P0); bp.box.grow(P1); bp.box.grow(P2);
+                bp.idx = p.pad;
+                for (int k = 0; k < 3; ++k) bp.c[k] = 0.5f * (bp.box.lo[k] + bp.box.hi[k]);
+                scene_prims.push_back(p);
+                bprims.push_back(bp);
+            }
+        } else if (s.type == AMVPT_SHAPE_SPHERE) {
+            std::memcpy(o.center, s.center, 12);
+            o.radius = s.radius;
+            o.inv_area = 1.f / ((4.f * 3.14159265358979323846f) * (s.radius * s.radius));
+            DPrim p{};
+            p.a[0] = s.center[0]; p.a[1] = s.center[1]; p.a[2] = s.center[2]; p.a[3] = s.radius;
+            p.type = PRIM_SPHERE; p.shape = i; p.face = 0;
+            p.pad = (uint32_t) scene_prims.size();
+            BuildPrim bp;
+            for (int k = 0; k < 3; ++k) { bp.box.lo[k] = s.center[k] - s.radius; bp.box.hi[k] = s.center[k] + s.radius; }
+            bp.idx = p.pad;
+            for (int k = 0; k < 3; ++k) bp.c[k] = s.center[k];
+            scene_prims.push_back(p);
+            bprims.push_back(bp);
+        } else {
+            set_error("unknown shape type");
+            return AMVPT_ERR_INVALID;
+        }
+    }
+    if (!vnrm.empty()) vnrm.resize(vpos.size(), 0.f);
+    if (!vuv.empty()) vuv.resize(2 * (vpos.size() / 3), 0.f);
+
+    std::vector<DNode> nodes;
+    std::vector<DPrim> prims;
+    if (bprims.empty()) {
+        DNode root{};
+        root.lo[0] = root.lo[1] = root.lo[2] = 1.f;
+        root.hi[0] = root.hi[1] = root.hi[2] = -1.f;
+        root.left_or_first = 0;
+        root.count = 0;
+        /* an empty inner node whose children are never reached: make it an empty leaf */
+        nodes.push_back(root);
+        nodes[0].count = 0;
+        DNode c{};
+        c.lo[0] = c.lo[1] = c.lo[2] = 1.f; c.hi[0] = c.hi[1] = c.hi[2] = -1.f;
+        nodes[0].left_or_first = 1;
+        nodes.push_back(c); nodes.push_back(c);
+        nodes[1].count = 0; nodes[2].count = 0;
+        nodes[1].left_or_first = 1; nodes[2].left_or_first = 1; /* never visited: empty boxes */
+    } else {
+        Builder b(bprims);
+        b.nodes.resize(1);
+        b.build(0, 0, (uint32_t) bprims.size(), 0);
+        nodes = std::move(b.nodes);
+        prims.resize(bprims.size());
+        for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
+    }
+    if (prims.empty()) prims.resize(1); /* keep a valid pointer */
+
+    std::vector<DBsdf> bsdfs(d->bsdf_count);
+    for (uint32_t i = 0; i < d->bsdf_count; ++i) {
+        const amvpt_bsdf_desc &s = d->bsdfs[i];
+        DBsdf &o = bsdfs[i];
+        std::memset(&o, 0, sizeof(o));
+        o.type = s.type;
+        o.distribution = s.distribution;
+        o.sample_visible = s.sample_visible;
+        o.has_spec = s.has_specular_reflectance;
+        o.nested0 = s.nested[0];
+        o.nested1 = s.nested[1];
+        std::memcpy(o.refl, s.reflectance, 12);
+        o.alpha_u = s.alpha_u; o.alpha_v = s.alpha_v;
+        std::memcpy(o.eta, s.eta, 12);
+        std::memcpy(o.k, s.k, 12);
+        std::memcpy(o.spec, s.specular_reflectance, 12);
+        if (s.type == AMVPT_BSDF_TWOSIDED) {
+            uint32_t f0 = leaf_flags(d->bsdfs[s.nested[0]]), f1 = leaf_flags(d->bsdfs[s.nested[1]]);
+            o.flags = ((f0 & ~0x10000u) | 0x8000u) | ((f1 & ~0x8000u) | 0x10000u);
+        } else {
+            o.flags = leaf_flags(s);
+        }
+    }
+    std::vector<DEmitter> emitters(std::max<uint32_t>(1, d->emitter_count));
+    for (uint32_t i = 0; i < d->emitter_count; ++i) {
+        emitters[i].shape = d->emitters[i].shape;
+        std::memcpy(emitters[i].radiance, d->emitters[i].radiance, 12);
+    }
+    if (vpos.empty()) vpos.resize(3, 0.f);
+    if (vnrm.empty()) vnrm.resize(3, 0.f);
+    if (vuv.empty()) vuv.resize(2, 0.f);
+    if (faces.empty()) faces.resize(3, 0);
+
+    amvpt_scene *sc = new amvpt_scene();
+    (void) hipGetDevice(&sc->device);
+    auto upload = [&](const void *src, size_t bytes, void **dst) -> amvpt_status {
+        hipError_t e = hipMalloc(dst, bytes);
+        if (e != hipSuccess) return hip_fail("hipMalloc(scene)", (int) e);
+        sc->allocations.push_back(*dst);
+        e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", (int) e);
+        return AMVPT_OK;
+    };
+    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces;
+    amvpt_status st;
+#define UP(vec, ptr)                                                                      \
+    if ((st = upload(vec.data(), vec.size() * sizeof(vec[0]), &ptr)) != AMVPT_OK) {       \
+        amvpt_scene_destroy(sc);                                                          \
+        return st;                                                                        \
+    }
+    UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
+    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces)
+#undef UP
+    DScene &D = sc->dev;
+    D.nodes = (const DNode *) p_nodes;
+    D.prims = (const DPrim *) p_prims;
+    D.shapes = (const DShape *) p_shapes;
+    D.bsdfs = (const DBsdf *) p_bsdfs;
+    D.emitters = (const DEmitter *) p_emit;
+    D.vpos = (const float *) p_vpos;
+    D.vnrm = (const float *) p_vnrm;
+    D.vuv = (const float *) p_vuv;
+    D.faces = (const uint32_t *) p_faces;
+    D.n_nodes = (uint32_t) nodes.size();
+    D.n_prims = (uint32_t) prims.size();
+    D.n_shapes = d->shape_count;
+    D.n_emitters = d->emitter_count;
+    D.emitter_pmf = d->emitter_count ? 1.f / (float) d->emitter_count : 0.f;
+    D.lds_bytes = (uint32_t) (nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim));
+    sc->n_nodes = D.n_nodes;
+    sc->n_prims = (uint32_t) bprims.size();
+    std::vector<DScene> one(1, D);
+    if ((st = upload(one.data(), sizeof(DScene), &sc->dev_scene_struct)) != AMVPT_OK) {
+        amvpt_scene_destroy(sc);
+        return st;
+    }
+    *out = sc;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_scene_destroy(amvpt_scene *scene) {
+    if (!scene) return AMVPT_OK;
+    for (void *p : scene->allocations) (void) hipFree(p);
+    delete scene;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_scene_stats(const amvpt_scene *scene, uint32_t *n_nodes, uint32_t *n_prims) {
+    if (!scene) { set_error("null scene"); return AMVPT_ERR_INVALID; }
+    if (n_nodes) *n_nodes = scene->n_nodes;
+    if (n_prims) *n_prims = scene->n_prims;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_render(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                          uint64_t lane_begin, uint64_t lane_end, float *film_device, void *stream,
+                          amvpt_counters *counters) {
+    if (!device_ok()) { set_error("amvpt_render: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    return render_impl(scene, views, params, lane_begin, lane_end, film_device, stream, counters, nullptr, 0);
+}
+
+amvpt_status amvpt_render_records(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                                  uint32_t pass, uint64_t lane_begin, uint64_t lane_end, float *film_device,
+                                  float *records_device, void *stream) {
+    if (!device_ok()) { set_error("amvpt_render_records: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    return render_impl(scene, views, params, lane_begin, lane_end, film_device, stream, nullptr, records_device, pass);
+}
+
+amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t width, uint32_t height,
+                           uint32_t film_alpha, void *stream) {
+    if (!device_ok()) { set_error("amvpt_develop: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    return develop_impl(film_device, out_device, width, height, film_alpha, stream);
+}
+
+} // extern "C"

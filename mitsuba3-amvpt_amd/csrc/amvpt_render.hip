@@ -1,0 +1,1189 @@
+/*
+ * amvpt_render.hip -- the MI355X wavefront pipeline of the `mvpath` integrator.
+ *
+ * One frame = n_passes passes (mvpath.cpp:36-41,222-246); one pass = L lanes
+ * (lane -> pixel = lane >> log2(spp_per_pass), mvpath.cpp:173-190), processed
+ * in chunks of at most g_chunk_lanes lanes.  Per chunk:
+ *
+ *   k_mv_primary<G>  render_multisample + sample_multi up to the suffix
+ *                    (jitter, sample_ray_idx, primary hit, emitter sample +
+ *                    shadow ray, camera_selection with G-1 visibility rays,
+ *                    mis_weights, direct light, mixture pdf)   mvpath_multi.h:8-322
+ *                    -> view records (SoA) + compacted suffix queue
+ *   k_raygen_single  render_sample: jitter + sample_ray -> queue (G = 1 / `path`)
+ *   k_bounce (xN)    one iteration of the shared-suffix / sample_single loop per
+ *                    live path; ballot + mbcnt compaction into the next queue
+ *                    mvpath_multi.h:563-686, mvpath_single.h:130-275
+ *   k_splat_*        indirect accumulation + ImageBlock::put into the film
+ *                    (float atomics)          mvpath_multi.h:343-368,61-76; imageblock.cpp:174-559
+ *
+ * All queues and records are SoA float4 streams in HBM (16 B per lane per
+ * stream: one dwordx4 load/store per lane, 1 KiB per wave instruction).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "dbsdf.h"
+#include "internal.h"
+
+namespace amvpt {
+
+uint64_t g_chunk_lanes = 1ull << 23;
+
+/* ------------------------------------------------------------------ */
+/* Parameters                                                         */
+/* ------------------------------------------------------------------ */
+
+struct KParams {
+    uint32_t W, H, C;
+    uint32_t spp_pp, log_spp, pow2;
+    uint32_t max_depth, rr_depth;
+    uint32_t sa_mis, fast_mis, debug, n_adapt;
+    uint32_t G;
+    uint32_t multisensor, n_views, gx, gy, rev_x, rev_y, sres_x, sres_y;
+    uint32_t box, coalesce_single, path_box_pos, is_mvpath;
+    uint32_t seed_value;
+    float inv_w, inv_h;
+    float adapt_w;
+    FilterCoeffs filt;
+    uint64_t chunk_begin;
+    uint32_t chunk_n;
+    uint32_t record;      /* write per-lane splat records */
+};
+
+/* SoA streams of one chunk */
+struct Bufs {
+    float4 *q_in[6];
+    float4 *q_out[6];
+    uint32_t *cnt_in, *cnt_out;
+    float4 *lane_out;     /* (indirect / result rgb, valid_ray) */
+    float4 *lane_rec;     /* (pdfW, flags) */
+    float4 *view_rec;     /* [3][G][n]: (pos, weight, flags), (result), (bsdf_val) */
+    float *film;
+    float *records;       /* optional [n][G][8] */
+    unsigned long long *stats; /* [0] vertices [1] reuse lanes [2] visibility rays [3] splats */
+};
+
+/* ------------------------------------------------------------------ */
+/* Scene staging                                                      */
+/* ------------------------------------------------------------------ */
+
+constexpr uint32_t kLdsSceneBytes = 48 * 1024;
+
+AD SceneRef stage_scene(const DScene &S, char *lds) {
+    SceneRef sc;
+    sc.g = &S;
+    if (S.lds_bytes <= kLdsSceneBytes) {
+        const uint32_t nn = S.n_nodes * (uint32_t) sizeof(DNode) / 16, np = S.n_prims * (uint32_t) sizeof(DPrim) / 16;
+        float4 *dst = (float4 *) lds;
+        const float4 *sn = (const float4 *) S.nodes, *spr = (const float4 *) S.prims;
+        for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) dst[i] = sn[i];
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) dst[nn + i] = spr[i];
+        __syncthreads();
+        sc.nodes = (const DNode *) lds;
+        sc.prims = (const DPrim *) (lds + (size_t) nn * 16);
+    } else {
+        sc.nodes = S.nodes;
+        sc.prims = S.prims;
+    }
+    return sc;
+}
+
+AD SI intersect(const SceneRef &sc, const Ray &r) { return compute_si(sc, r, trace_closest(sc, r)); }
+
+/* ------------------------------------------------------------------ */
+/* Emitters at scene level                                            */
+/* ------------------------------------------------------------------ */
+
+AD int32_t si_emitter(const SceneRef &sc, const SI &si) {
+    return si.valid() ? sc.g->shapes[si.shape].emitter : -1;
+}
+
+AD C3 emitter_eval(const SceneRef &sc, int32_t e, const SI &si, bool active) {
+    if (e < 0 || !active) return c3(0.f);
+    if (!(si.wi.z > 0.f)) return c3(0.f);
+    return c3(sc.g->emitters[e].radiance);
+}
+
+AD void sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, float u2, bool active, DSamp &ds,
+                                 C3 &spec) {
+    ds = ds_zero();
+    spec = c3(0.f);
+    uint32_t n = sc.g->n_emitters;
+    if (n == 0) return;
+    uint32_t index = 0;
+    float weight = 1.f;
+    if (n >= 2) {
+        float scaled = u1 * (float) n;
+        index = min((uint32_t) scaled, n - 1u);
+        weight = (float) n;
+        u1 = scaled - (float) index;
+    }
+    if (!active) return;
+    const DEmitter &em = sc.g->emitters[index];
+    const DShape &s = sc.g->shapes[em.shape];
+    ds = shape_sample_direction(s, ref.p, u1, u2);
+    bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
+    spec = a ? c3(em.radiance) / ds.pdf : c3(0.f);
+    ds.emitter = (int32_t) index;
+    ds.pdf *= sc.g->emitter_pmf;
+    spec = spec * weight;
+    if (ds.pdf != 0.f) {
+        Ray r = spawn_ray_to(ref.p, ref.n, ds.p);
+        if (trace_any(sc, r)) { spec = c3(0.f); ds.pdf = 0.f; }
+    }
+}
+
+AD float pdf_emitter_direction(const SceneRef &sc, f3 refp, const DSamp &ds, bool active) {
+    if (ds.emitter < 0 || !active) return 0.f;
+    const DEmitter &em = sc.g->emitters[ds.emitter];
+    const DShape &s = sc.g->shapes[em.shape];
+    bool a = dot(ds.d, ds.n) < 0.f;
+    float v = shape_pdf_direction(s, refp, ds);
+    return (a ? v : 0.f) * sc.g->emitter_pmf;
+}
+
+AD float mis_weight(float a, float b) {
+    a *= a; b *= b;
+    float w = a / (a + b);
+    return finite_(w) ? w : 0.f;
+}
+
+/* ------------------------------------------------------------------ */
+/* Sensors                                                            */
+/* ------------------------------------------------------------------ */
+
+AD Ray persp_sample_ray(const DView &v, float x, float y) {
+    f3 near_p = xf_point(v.sample_to_camera, mk(x + v.pp[0], y + v.pp[1], 0.f));
+    f3 d = normalize(near_p);
+    Ray r;
+    r.o = mk(v.to_world[3], v.to_world[7], v.to_world[11]);
+    r.d = xf_vector(v.to_world, d);
+    float inv_z = rcp(d.z);
+    float near_t = v.near_clip * inv_z, far_t = v.far_clip * inv_z;
+    r.o = r.o + r.d * near_t;
+    r.maxt = far_t - near_t;
+    return r;
+}
+
+/* GridSensor::sample_ray_idx (grid.cpp:269-297) */
+AD Ray sample_ray_idx(const KParams &P, const DView *V, float ax, float ay, uint32_t &index) {
+    if (!P.multisensor) { index = 0; return persp_sample_ray(V[0], ax, ay); }
+    float fx = ax * (float) P.gx, fy = ay * (float) P.gy;
+    uint32_t ux = (uint32_t) fx, uy = (uint32_t) fy;
+    uint32_t ix = ux, iy = uy;
+    if (P.rev_x) ix = (P.gx - 1) - ix;
+    if (P.rev_y) iy = (P.gy - 1) - iy;
+    index = ix + P.gx * iy;
+    index = min(index, P.n_views - 1);
+    return persp_sample_ray(V[index], fx - (float) ux, fy - (float) uy);
+}
+
+struct Surf { f3 p, d; float uvx, uvy, pdf, Jp; bool face, valid; };
+
+/* PerspectiveCamera::sample_surface under a masked vcall (perspective.cpp:327-385) */
+AD Surf persp_sample_surface(const DView &v, const SI &it, bool active) {
+    Surf r;
+    r.p = mk(0.f, 0.f, 0.f); r.d = mk(0.f, 0.f, 0.f);
+    r.uvx = r.uvy = r.pdf = r.Jp = 0.f;
+    r.face = false; r.valid = false;
+    if (!active) return r;
+    f3 ref_p = xf_point_affine(v.to_world_inv, it.p);
+    bool a = ref_p.z >= v.near_clip && ref_p.z <= v.far_clip;
+    f3 screen = xf_point(v.camera_to_sample, ref_p);
+    float ux = screen.x - v.pp[0], uy = screen.y - v.pp[1];
+    a = a && ux >= 0.f && ux <= 1.f && uy >= 0.f && uy <= 1.f;
+    r.uvx = ux * v.res[0];
+    r.uvy = uy * v.res[1];
+    float dist = norm(ref_p), inv_dist = rcp(dist);
+    float ctf = ref_p.z;
+    a = a && ctf > 0.f;
+    float ictf = rcp(ctf), ictf3 = ictf * ictf * ictf;
+    r.pdf = v.normalization * ictf3;
+    r.p = xf_point_affine(v.to_world, mk(0.f, 0.f, 0.f));
+    r.d = (r.p - it.p) * inv_dist;
+    float cts = dot(r.d, it.n);
+    r.face = cts > 0.f;
+    cts = fabs_(cts);
+    r.Jp = (cts * inv_dist * inv_dist) * r.pdf;
+    r.valid = a;
+    return r;
+}
+
+/* ------------------------------------------------------------------ */
+/* Film                                                               */
+/* ------------------------------------------------------------------ */
+
+AD void film_add(float *p, float v) { atomicAdd(p, v); }
+
+/* ImageBlock::put (imageblock.cpp:174-559), both accumulation methods. */
+AD void film_put(const KParams &P, float *film, float px, float py, const float *vals, bool coalesce) {
+    const uint32_t W = P.W, H = P.H, C = P.C;
+    if (P.box) {
+        int ix = (int) floorf(px), iy = (int) floorf(py);
+        uint32_t ux = (uint32_t) ix, uy = (uint32_t) iy;
+        if (!(ux < W && uy < H)) return;
+        float *ptr = film + ((size_t) uy * W + ux) * C;
+        for (uint32_t k = 0; k < C; ++k) film_add(ptr + k, vals[k]);
+        return;
+    }
+    const float radius = P.filt.radius;
+    if (!coalesce) {
+        float pfx = px + (0.f - 0.5f), pfy = py + (0.f - 0.5f);
+        int p0x = max((int) ceilf(pfx - radius), 0), p0y = max((int) ceilf(pfy - radius), 0);
+        int p1x = min((int) floorf(pfx + radius), (int) W - 1), p1y = min((int) floorf(pfy + radius), (int) H - 1);
+        uint32_t u0x = (uint32_t) p0x, u0y = (uint32_t) p0y, u1x = (uint32_t) p1x, u1y = (uint32_t) p1y;
+        const uint32_t count = (uint32_t) ceilf(2.f * radius);
+        if (!(u0x <= u1x && u0y <= u1y)) return;
+        float rx = (float) u0x - pfx, ry = (float) u0y - pfy;
+        for (uint32_t ys = 0; ys < count; ++ys) {
+            float wy = gaussian_eval(P.filt, ry + (float) ys);
+            if (!(u0y + ys <= u1y)) continue;
+            for (uint32_t xs = 0; xs < count; ++xs) {
+                float wx = gaussian_eval(P.filt, rx + (float) xs);
+                float w = wx * wy;
+                if (!(u0x + xs <= u1x)) continue;
+                float *ptr = film + ((size_t) (u0y + ys) * W + (u0x + xs)) * C;
+                for (uint32_t k = 0; k < C; ++k) film_add(ptr + k, vals[k] * w);
+            }
+        }
+        return;
+    }
+    const uint32_t n = (uint32_t) ceilf(radius - .5f), count = 2 * n + 1;
+    int pix = (int) floorf(px) - (int) n, piy = (int) floorf(py) - (int) n;
+    uint32_t x = (uint32_t) pix, y = (uint32_t) piy;
+    float rx = ((float) pix + .5f) - px, ry = ((float) piy + .5f) - py;
+    for (uint32_t ys = 0; ys < count; ++ys) {
+        float wy = gaussian_eval(P.filt, ry + (float) ys);
+        if (!(y + ys < H)) continue;
+        for (uint32_t xs = 0; xs < count; ++xs) {
+            float wx = gaussian_eval(P.filt, rx + (float) xs);
+            float w = wx * wy;
+            if (!(x + xs < W)) continue;
+            float *ptr = film + ((size_t) (y + ys) * W + (x + xs)) * C;
+            for (uint32_t k = 0; k < C; ++k) film_add(ptr + k, vals[k] * w);
+        }
+    }
+}
+
+AD void pack_vals(const KParams &P, C3 v, float alpha, float weight, float *vals) {
+    vals[0] = v.r; vals[1] = v.g; vals[2] = v.b;
+    if (P.C == 4) { vals[3] = weight; vals[4] = 0.f; }
+    else { vals[3] = alpha; vals[4] = weight; }
+}
+
+/* ------------------------------------------------------------------ */
+/* Queue                                                              */
+/* ------------------------------------------------------------------ */
+
+/* Sum over the wave, result valid in every lane. */
+AD unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (unsigned long long) __shfl_xor((long long) v, o);
+    return v;
+}
+AD void stat_add(unsigned long long *ctr, unsigned long long v) {
+    v = wave_sum(v);
+    if (__lane_id() == 0 && v) atomicAdd(ctr, v);
+}
+
+/* Wave-aggregated slot allocation: one atomic per wave (ballot + mbcnt). */
+AD uint32_t queue_slot(bool want, uint32_t *counter) {
+    uint64_t mask = __ballot(want);
+    uint32_t lane = __lane_id();
+    uint32_t cnt = (uint32_t) __popcll(mask);
+    uint32_t leader = mask ? (uint32_t) (__ffsll((unsigned long long) mask) - 1) : 0u;
+    uint32_t base = 0;
+    if (cnt && lane == leader) base = atomicAdd(counter, cnt);
+    base = (uint32_t) __shfl((int) base, (int) leader);
+    uint32_t rank = (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
+    return base + rank;
+}
+
+struct PathState {
+    Ray ray;
+    C3 thr, res;
+    float eta, prev_pdf;
+    uint32_t depth;
+    bool prev_delta, valid_ray;
+    f3 prev_p;
+    uint32_t idx;         /* chunk-local lane index */
+    uint64_t rng_state;
+    uint32_t rng_seq;     /* v1 of TEA -> inc = 2*v1+1 */
+};
+
+AD void store_state(float4 *const *q, uint32_t slot, const PathState &s) {
+    uint32_t bits = (s.depth & 0x3fffffffu) | (s.prev_delta ? 0x40000000u : 0u) | (s.valid_ray ? 0x80000000u : 0u);
+    q[0][slot] = make_float4(s.ray.o.x, s.ray.o.y, s.ray.o.z, s.ray.d.x);
+    q[1][slot] = make_float4(s.ray.d.y, s.ray.d.z, s.thr.r, s.thr.g);
+    q[2][slot] = make_float4(s.thr.b, s.eta, s.prev_pdf, bitsf(bits));
+    q[3][slot] = make_float4(s.prev_p.x, s.prev_p.y, s.prev_p.z, bitsf(s.idx));
+    q[4][slot] = make_float4(s.res.r, s.res.g, s.res.b, bitsf(s.rng_seq));
+    q[5][slot] = make_float4(bitsf((uint32_t) s.rng_state), bitsf((uint32_t) (s.rng_state >> 32)), 0.f, 0.f);
+}
+
+AD PathState load_state(float4 *const *q, uint32_t slot) {
+    PathState s;
+    float4 a = q[0][slot], b = q[1][slot], c = q[2][slot], d = q[3][slot], e = q[4][slot], f = q[5][slot];
+    s.ray.o = mk(a.x, a.y, a.z);
+    s.ray.d = mk(a.w, b.x, b.y);
+    s.ray.maxt = kLargest;
+    s.thr = C3{b.z, b.w, c.x};
+    s.eta = c.y;
+    s.prev_pdf = c.z;
+    uint32_t bits = fbits(c.w);
+    s.depth = bits & 0x3fffffffu;
+    s.prev_delta = (bits & 0x40000000u) != 0;
+    s.valid_ray = (bits & 0x80000000u) != 0;
+    s.prev_p = mk(d.x, d.y, d.z);
+    s.idx = fbits(d.w);
+    s.res = C3{e.x, e.y, e.z};
+    s.rng_seq = fbits(e.w);
+    s.rng_state = (uint64_t) fbits(f.x) | ((uint64_t) fbits(f.y) << 32);
+    return s;
+}
+
+/* ------------------------------------------------------------------ */
+/* k_raygen_single: render_sample prologue (mvpath_single.h:50-76)     */
+/* ------------------------------------------------------------------ */
+
+AD void lane_pixel(const KParams &P, uint32_t lane, int &px, int &py) {
+    uint32_t pix = P.pow2 ? (lane >> P.log_spp) : (lane / P.spp_pp);
+    uint32_t y = pix / P.W;
+    py = (int) y;
+    px = (int) (pix - P.W * y);
+}
+
+__global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V, Bufs B) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = i < P.chunk_n;
+    PathState s;
+    if (ok) {
+        uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        int px, py;
+        lane_pixel(P, lane, px, py);
+        uint32_t v0, v1;
+        tea4(P.seed_value, lane, v0, v1);
+        Pcg rng;
+        rng.seed(v0, v1);
+        float jx = rng.next_1d(), jy = rng.next_1d();
+        float sx = (float) px + jx, sy = (float) py + jy;
+        uint32_t index;
+        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index);
+        s.thr = c3(1.f); s.res = c3(0.f);
+        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
+        s.prev_p = mk(0.f, 0.f, 0.f);
+        s.idx = i;
+        s.rng_state = rng.state;
+        s.rng_seq = v1;
+        if (P.max_depth == 0) {
+            B.lane_out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ok = false;
+        }
+    }
+    uint32_t slot = queue_slot(ok, B.cnt_out);
+    if (ok) store_state(B.q_out, slot, s);
+}
+
+/* ------------------------------------------------------------------ */
+/* k_bounce: one loop iteration (mvpath_multi.h:563-686 == mvpath_single.h:130-275) */
+/* ------------------------------------------------------------------ */
+
+__global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const DScene S = *Sp;
+    SceneRef sc = stage_scene(S, lds);
+    const uint32_t count = *B.cnt_in;
+    unsigned long long verts = 0;
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < count; i0 += gridDim.x * blockDim.x) {
+        uint32_t i = i0 + threadIdx.x;
+        bool ok = i < count;
+        PathState s;
+        bool keep = false;
+        if (ok) {
+            s = load_state(B.q_in, i);
+            Pcg rng;
+            rng.state = s.rng_state;
+            rng.inc = (((uint64_t) s.rng_seq) << 1) | 1u;
+            ++verts;
+            SI si = intersect(sc, s.ray);
+            int32_t em = si_emitter(sc, si);
+            {
+                DSamp ds = ds_zero();
+                ds.p = si.p; ds.n = si.sh.n;
+                f3 rel = si.p - s.prev_p;
+                ds.dist = norm(rel);
+                ds.d = si.valid() ? rel / ds.dist : -si.wi;
+                ds.emitter = em;
+                float em_pdf = pdf_emitter_direction(sc, s.prev_p, ds, !s.prev_delta);
+                float mis_bsdf = mis_weight(s.prev_pdf, em_pdf);
+                s.res = cfma(s.thr, emitter_eval(sc, em, si, s.prev_pdf > 0.f) * mis_bsdf, s.res);
+            }
+            bool active_next = (s.depth + 1 < P.max_depth) && si.valid();
+            int32_t b = si.valid() ? S.shapes[si.shape].bsdf : -1;
+            bool active_em = active_next && (bsdf_flags(S.bsdfs, b) & BF_Smooth);
+            float e1 = rng.next_1d(), e2 = rng.next_1d();
+            DSamp ds;
+            C3 em_w;
+            sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
+            active_em = active_em && ds.pdf != 0.f;
+            f3 wo = si.sh.to_local(ds.d);
+            float s1 = rng.next_1d();
+            float s2a = rng.next_1d(), s2b = rng.next_1d();
+            (void) s1;
+            C3 bval;
+            float bpdf;
+            bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
+            BSample bs;
+            C3 bw;
+            bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
+            {
+                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
+                if (active_em) s.res = cfma(s.thr, bval * em_w * mis_em, s.res);
+            }
+            s.ray = spawn_ray(si.p, si.n, si.sh.to_world(bs.wo));
+            s.thr = s.thr * bw;
+            s.eta *= bs.eta;
+            s.prev_p = si.p;
+            s.prev_pdf = bs.pdf;
+            s.prev_delta = (bs.type & BF_Delta) != 0;
+            if (si.valid()) s.depth += 1;
+            float tmax = cmax(s.thr);
+            float rr_prob = vmin(tmax * sqr(s.eta), .95f);
+            bool rractive = s.depth >= P.rr_depth;
+            bool rr_continue = rng.next_1d() < rr_prob;
+            s.valid_ray = s.valid_ray || (si.valid() && !(bs.type & BF_Null));
+            if (rractive) s.thr = s.thr * rcp(rr_prob);
+            keep = active_next && (!rractive || rr_continue) && (tmax != 0.f);
+            s.rng_state = rng.state;
+            if (!keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
+        }
+        uint32_t slot = queue_slot(keep, B.cnt_out);
+        if (keep) store_state(B.q_out, slot, s);
+    }
+    if (B.stats) stat_add(&B.stats[0], verts);
+}
+
+/* ------------------------------------------------------------------ */
+/* k_splat_single: ImageBlock::put of render_sample                    */
+/* ------------------------------------------------------------------ */
+
+__global__ void __launch_bounds__(256) k_splat_single(KParams P, Bufs B) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.chunk_n) return;
+    uint32_t lane = (uint32_t) (P.chunk_begin + i);
+    int px, py;
+    lane_pixel(P, lane, px, py);
+    Pcg rng = lane_rng(P.seed_value, lane);
+    float jx = rng.next_1d(), jy = rng.next_1d();
+    float sx = (float) px + jx, sy = (float) py + jy;
+    float4 lo = B.lane_out[i];
+    bool valid = lo.w != 0.f;
+    C3 spec = valid ? C3{lo.x, lo.y, lo.z} : c3(0.f);
+    float alpha = valid ? 1.f : 0.f;
+    float vals[5];
+    pack_vals(P, spec, alpha, 1.f, vals);
+    float putx = P.path_box_pos ? (float) px : sx, puty = P.path_box_pos ? (float) py : sy;
+    film_put(P, B.film, putx, puty, vals, P.coalesce_single != 0);
+    if (P.record) {
+        float *r = B.records + (size_t) i * 8;
+        r[0] = sx; r[1] = sy; r[2] = spec.r; r[3] = spec.g; r[4] = spec.b; r[5] = alpha; r[6] = 1.f; r[7] = 1.f;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* k_mv_primary<G>: sample_multi up to the shared suffix               */
+/* ------------------------------------------------------------------ */
+
+enum : uint32_t { VF_VALID = 1u, VF_INDIRECT = 2u };
+enum : uint32_t { LF_VALIDRAY = 1u, LF_ADAPT = 2u, LF_PHIT = 4u, LF_MIS = 8u };
+
+struct SD {        /* SampleData (mvpath.h:150-167) without the derived fields */
+    C3 result, bsdf_val;
+    f3 wi;
+    float px, py, weight, pdfM, pdf, pdf_lk, Jp, iJp;
+    uint32_t idx;
+    bool indirect, valid;
+};
+
+struct BD { int32_t bsdf; float alpha, sqr_a, rsqrt_a; bool diffuse, reuse; };
+
+AD float tv_pdf(const DBsdf *T, f3 wo_l, f3 wi_k, float p_k, const BD &bd, bool active) {
+    active = active && p_k > 0.f;
+    float p_l = bsdf_pdf(T, bd.bsdf, CTX_GLOSSY, wi_k, wo_l, active);
+    active = active && p_l > 0.f;
+    float p_max = vmax(p_l, p_k), p_min = vmin(p_l, p_k);
+    float q = p_min * rcp(p_max);
+    float p = fmadd(q - 1.f, bd.rsqrt_a, 1.f);
+    p = sqr(vmax(p, 0.f));
+    p = lerp_(p, q, bd.alpha);
+    return active ? p : 0.f;
+}
+AD float tv_pdf_fast(f3 wo_l, f3 wi_k, float p_k, const BD &bd, bool active) {
+    float p_l = sqr(normalize(wi_k + wo_l).z);
+    float N = fmadd(bd.sqr_a, vmax(p_k, p_l), 1.f), D = fmadd(bd.sqr_a, vmin(p_k, p_l), 1.f);
+    float q = sqr(N * rcp(D));
+    float p = fmadd(q - 1.f, bd.rsqrt_a, 1.f);
+    p = sqr(vmax(p, 0.f));
+    p = lerp_(p, q, bd.alpha);
+    return active ? p : 0.f;
+}
+AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
+
+template <int G>
+__global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const DScene S = *Sp;
+    SceneRef sc = stage_scene(S, lds);
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = i < P.chunk_n;
+    PathState ps;
+    bool push = false;
+    unsigned long long st_reuse = 0, st_vis = 0;
+    if (ok) {
+        const uint32_t n = P.chunk_n;
+        uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        int px, py;
+        lane_pixel(P, lane, px, py);
+        uint32_t v0, v1;
+        tea4(P.seed_value, lane, v0, v1);
+        Pcg rng;
+        rng.seed(v0, v1);
+        float jx = rng.next_1d(), jy = rng.next_1d();
+        float sx = (float) px + jx, sy = (float) py + jy;
+        uint32_t p_idx;
+        Ray pray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), p_idx);
+        SD sd[G];
+        uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            sd[k].result = c3(0.f); sd[k].bsdf_val = c3(0.f); sd[k].wi = mk(0.f, 0.f, 0.f);
+            sd[k].px = sd[k].py = sd[k].weight = sd[k].pdfM = sd[k].pdf = sd[k].pdf_lk = sd[k].Jp = sd[k].iJp = 0.f;
+            uint32_t id = p_idx + (uint32_t) k;
+            sd[k].idx = id < max_idx ? id : id - (uint32_t) G;
+            sd[k].indirect = false; sd[k].valid = false;
+        }
+        sd[0].px = sx; sd[0].py = sy;
+
+        /* ---- sample_multi (mvpath_multi.h:130-369) ---- */
+        bool valid_ray = false, adapt_mask = false;
+        float pdfW = 1.f;
+        bool should_mis = P.sa_mis != 0;
+        if (P.max_depth != 0) {
+            SI si = intersect(sc, pray);
+            bool p_hit = si.valid();
+            int32_t em = si_emitter(sc, si);
+            bool direct_em = em >= 0;
+            if (direct_em) sd[0].result = emitter_eval(sc, em, si, true);
+            int32_t b = p_hit ? S.shapes[si.shape].bsdf : -1;
+            bool bsdf_smooth = (bsdf_flags(S.bsdfs, b) & BF_Smooth) != 0;
+            bool active_em = p_hit && bsdf_smooth;
+            float e1 = rng.next_1d(), e2 = rng.next_1d();
+            DSamp ds;
+            C3 em_w;
+            sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
+            active_em = active_em && ds.pdf != 0.f;
+            f3 wo = si.sh.to_local(ds.d);
+            float rand_1 = rng.next_1d();
+            float r2a = rng.next_1d(), r2b = rng.next_1d();
+            (void) rand_1;
+            C3 bsdf_val;
+            float direct_pdf;
+            bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bsdf_val, direct_pdf);
+            BSample bsmp;
+            C3 bsdf_weight;
+            bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, r2a, r2b, true, bsmp, bsdf_weight);
+            bool flag_delta = (bsmp.type & BF_Delta) != 0, flag_null = (bsmp.type & BF_Null) != 0;
+            bool flag_diff = (bsmp.type & BF_Diffuse) != 0;
+            bool delta = flag_delta || flag_null, p_not_delta = !delta && p_hit;
+            bool reuse = !direct_em && p_not_delta && bsdf_smooth;
+            st_reuse += reuse ? 1 : 0;
+            bool p_face = si.wi.z > 0.f;
+            if (should_mis) {
+                BD bd;
+                bd.bsdf = b;
+                bd.alpha = bsdf_roughness(S.bsdfs, b, si.wi);
+                bd.sqr_a = fmsub(bd.alpha, bd.alpha, 1.f);
+                bd.rsqrt_a = rsqrt_(bd.alpha);
+                bd.diffuse = flag_diff;
+                bd.reuse = reuse;
+                sd[0].bsdf_val = bsdf_val;
+                /* ---- camera_selection (mvpath_multi.h:371-464) ---- */
+                {
+                    Surf p0 = persp_sample_surface(V[sd[0].idx], si, p_hit);
+                    sd[0].pdf = p0.pdf;
+                    sd[0].pdf_lk = p0.pdf;
+                    sd[0].Jp = p0.Jp;
+                    sd[0].iJp = p_hit ? rcp(p0.Jp) : 0.f;
+                    sd[0].wi = si.wi;
+                    sd[0].valid = p_hit;
+                    sd[0].indirect = p_hit;
+                    f3 wo_r0 = reflect_l(si.wi);
+                    sd[0].pdfM = P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
+                                            : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit);
+                    if (bd.diffuse) sd[0].pdfM = 1.f;
+                    float n_direct = 1.f, n_indir = 2.f;
+#pragma unroll
+                    for (int k = 1; k < G; ++k) {
+                        Surf r = persp_sample_surface(V[sd[k].idx], si, bd.reuse);
+                        bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
+                        if (valid) {
+                            ++st_vis;
+                            Ray vr = spawn_ray_to(si.p, si.n, r.p);
+                            valid = !trace_any(sc, vr);
+                        }
+                        f3 wik = si.sh.to_local(r.d);
+                        sd[k].wi = wik;
+                        f3 wor = reflect_l(wik);
+                        sd[k].pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
+                                                : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
+                        float pdf_Mat = P.fast_mis ? tv_pdf_fast(wo_r0, wik, sd[k].pdfM, bd, valid)
+                                                   : tv_pdf(S.bsdfs, wo_r0, wik, sd[k].pdfM, bd, valid);
+                        if (bd.diffuse) pdf_Mat = 1.f;
+                        float J = r.Jp * sd[0].iJp;
+                        float pdf_J = J > 1.f ? rcp(J) : J;
+                        float pdf_Sel = pdf_Mat * pdf_J;
+                        valid = valid && (rng.next_1d() < pdf_Sel);
+                        sd[k].Jp = r.Jp;
+                        sd[k].iJp = valid ? rcp(r.Jp) : 0.f;
+                        sd[k].px = r.uvx;
+                        sd[k].py = r.uvy;
+                        sd[k].pdf = valid ? r.pdf : 0.f;
+                        sd[k].pdf_lk = valid ? sd[0].pdf * J * pdf_Sel : 0.f;
+                        sd[k].valid = valid;
+                        bool indirect = valid, direct = valid;
+                        bool replace = n_indir * rng.next_1d() < 1.f;
+                        C3 bvk;
+                        float bpk;
+                        BSample bsk;
+                        C3 bwk;
+                        bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
+                        bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
+                        direct = direct && bpk > 0.f;
+                        sd[k].bsdf_val = bvk;
+                        direct_pdf += direct ? bpk : 0.f;
+                        n_direct += (float) direct;
+                        indirect = indirect && bsk.type == bsmp.type;
+                        if (indirect && replace) bsmp.wo = bsk.wo;
+                        n_indir += (float) indirect;
+                        sd[k].indirect = indirect;
+                    }
+                    direct_pdf /= n_direct;
+                }
+                /* ---- mis_weights (mvpath_multi.h:466-523) ---- */
+#pragma unroll
+                for (int k = 0; k < G; ++k) {
+                    float pdfSum = sd[k].pdf_lk;
+                    if (k > 0) pdfSum += sd[k].pdf;
+                    bool cond = k > 0 ? sd[k].valid : bd.reuse;
+                    float add;
+                    if (cond && !bd.diffuse) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int j = 1; j < G; ++j) {
+                            if (j == k) continue;
+                            float pdf_J = vmin(sqr(sd[j].Jp * sd[k].iJp), 1.f);
+                            f3 worj = reflect_l(sd[j].wi);
+                            float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, sd[k].wi, sd[k].pdfM, bd, sd[j].valid)
+                                                       : tv_pdf(S.bsdfs, worj, sd[k].wi, sd[k].pdfM, bd, sd[j].valid);
+                            acc = fmadd(sd[j].pdf, pdf_J * pdf_Mat, acc);
+                        }
+                        add = acc;
+                    } else {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int j = 1; j < G; ++j) {
+                            if (j == k) continue;
+                            float pdf_J = vmin(sqr(sd[j].Jp * sd[k].iJp), 1.f);
+                            acc = fmadd(sd[j].pdf, pdf_J, acc);
+                        }
+                        add = cond ? acc : 0.f;
+                    }
+                    pdfSum += add;
+                    sd[k].weight = sd[k].pdf_lk / pdfSum;
+                }
+            } else {
+                sd[0].valid = p_hit;
+#pragma unroll
+                for (int k = 1; k < G; ++k) {
+                    Surf r = persp_sample_surface(V[sd[k].idx], si, reuse);
+                    bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
+                    if (valid) {
+                        ++st_vis;
+                        Ray vr = spawn_ray_to(si.p, si.n, r.p);
+                        valid = !trace_any(sc, vr);
+                    }
+                    sd[k].px = r.uvx;
+                    sd[k].py = r.uvy;
+                    sd[k].valid = valid;
+                }
+            }
+            /* ---- emitter sampling contribution ---- */
+            {
+                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
+                C3 emis_mis = em_w * mis_em;
+                if (should_mis) {
+#pragma unroll
+                    for (int k = 0; k < G; ++k)
+                        if (active_em && sd[k].valid) sd[k].result = cfma(sd[k].bsdf_val, emis_mis, sd[k].result);
+                } else {
+                    if (active_em) sd[0].result = cfma(bsdf_val, emis_mis, sd[0].result);
+                }
+            }
+            /* ---- BSDF sampling / multi-view mixture pdf ---- */
+            Ray pd_ray = spawn_ray(si.p, si.n, si.sh.to_world(bsmp.wo));
+            if (should_mis) {
+                float n_indir = 0.f, pdf = 0.f;
+#pragma unroll
+                for (int k = 0; k < G; ++k) {
+                    bool valid = sd[k].indirect;
+                    C3 bv;
+                    float bp;
+                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, sd[k].wi, bsmp.wo, valid, bv, bp);
+                    if (k == 0) {
+                        bv = p_not_delta ? bv : bsdf_weight;
+                        bp = p_not_delta ? bp : bsmp.pdf;
+                        valid = valid && (bp > 0.f || delta);
+                    }
+                    bool pvalid = bp > 0.f;
+                    valid = valid && ((k == 0) ? (pvalid || delta) : pvalid);
+                    bp = valid ? bp : 0.f;
+                    sd[k].bsdf_val = valid ? bv : c3(0.f);
+                    pdf += bp;
+                    n_indir += (float) valid;
+                    sd[k].indirect = sd[k].indirect && valid;
+                }
+                bsmp.pdf = p_not_delta ? pdf / n_indir : bsmp.pdf;
+                adapt_mask = p_hit && !flag_null && (n_indir <= 1.f);
+            }
+            C3 thr = should_mis ? c3(1.f) : bsdf_weight;
+            valid_ray = valid_ray || (p_hit && !flag_null);
+            bool pd_active = p_hit;
+            if (!should_mis) pd_active = pd_active && (cmax(thr) != 0.f);
+            if (P.max_depth <= 1) pd_active = false;
+            pdfW = p_not_delta ? rcp(bsmp.pdf) : 1.f;
+            if (pd_active) {
+                ps.ray = pd_ray;
+                ps.thr = thr;
+                ps.res = c3(0.f);
+                ps.eta = bsmp.eta;
+                ps.prev_pdf = bsmp.pdf;
+                ps.depth = p_hit ? 1u : 0u;
+                ps.prev_delta = flag_delta;
+                ps.valid_ray = false;
+                ps.prev_p = si.p;
+                ps.idx = i;
+                ps.rng_state = rng.state;
+                ps.rng_seq = v1;
+                push = true;
+            }
+            (void) rand_1;
+            /* p_sample.weight/valid finalisation happens after the suffix */
+            if (!should_mis) {
+#pragma unroll
+                for (int k = 0; k < G; ++k) sd[k].weight = 1.f;
+            }
+            sd[0].weight = p_hit ? sd[0].weight : 1.f;
+            sd[0].valid = true;
+        }
+        if (!push) B.lane_out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) | (should_mis ? LF_MIS : 0u);
+        B.lane_rec[i] = make_float4(pdfW, bitsf(lflags), 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            float px_k = sd[k].px, py_k = sd[k].py;
+            if (k > 0) {
+                uint32_t y = sd[k].idx / P.gx, x = sd[k].idx - y * P.gx;
+                if (P.rev_x) x = (P.gx - 1) - x;
+                if (P.rev_y) y = (P.gy - 1) - y;
+                px_k += (float) (x * P.sres_x);
+                py_k += (float) (y * P.sres_y);
+            }
+            uint32_t vf = (sd[k].valid ? VF_VALID : 0u) | (sd[k].indirect ? VF_INDIRECT : 0u);
+            size_t o = (size_t) k * n + i;
+            B.view_rec[o] = make_float4(px_k, py_k, sd[k].weight, bitsf(vf));
+            B.view_rec[(size_t) G * n + o] = make_float4(sd[k].result.r, sd[k].result.g, sd[k].result.b, 0.f);
+            B.view_rec[(size_t) 2 * G * n + o] = make_float4(sd[k].bsdf_val.r, sd[k].bsdf_val.g, sd[k].bsdf_val.b, 0.f);
+        }
+    }
+    uint32_t slot = queue_slot(push, B.cnt_out);
+    if (push) store_state(B.q_out, slot, ps);
+    if (B.stats) {
+        stat_add(&B.stats[1], st_reuse);
+        stat_add(&B.stats[2], st_vis);
+        stat_add(&B.stats[0], (ok && P.max_depth != 0) ? 1ull : 0ull);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* k_splat_multi<G>: indirect accumulation + splats (mvpath_multi.h:343-368,44-76) */
+/* ------------------------------------------------------------------ */
+
+template <int G>
+__global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.chunk_n) return;
+    const uint32_t n = P.chunk_n;
+    float4 lr = B.lane_rec[i], lo = B.lane_out[i];
+    uint32_t lflags = fbits(lr.y);
+    float pdfW = lr.x;
+    bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
+    bool mis = (lflags & LF_MIS) != 0;
+    bool adapt_mask = (lflags & LF_ADAPT) != 0;
+    C3 indirect = C3{lo.x, lo.y, lo.z};
+    float alpha = valid_ray ? 1.f : 0.f;
+    C3 res0 = c3(0.f);
+    if (!mis) {
+        float4 r0 = B.view_rec[(size_t) G * n + i];
+        res0 = C3{r0.x, r0.y, r0.z} + indirect;
+    }
+    unsigned long long splats = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        size_t o = (size_t) k * n + i;
+        float4 a = B.view_rec[o];
+        uint32_t vf = fbits(a.w);
+        bool valid = (vf & VF_VALID) != 0;
+        float weight = a.z;
+        C3 result;
+        if (mis) {
+            float4 r = B.view_rec[(size_t) G * n + o], bvv = B.view_rec[(size_t) 2 * G * n + o];
+            result = C3{r.x, r.y, r.z};
+            if (vf & VF_INDIRECT) result = cfma(C3{bvv.x, bvv.y, bvv.z} * pdfW, indirect, result);
+        } else {
+            result = res0;
+        }
+        if (k == 0 && P.n_adapt && adapt_mask) weight = weight * P.adapt_w;
+        C3 v = {weight * result.r, weight * result.g, weight * result.b};
+        if (P.debug) {
+            if (k == 0) {
+                float vals[5];
+                pack_vals(P, c3(adapt_mask ? 1.f : 0.f), alpha, 1.f, vals);
+                film_put(P, B.film, a.x, a.y, vals, true);
+            }
+            continue;
+        }
+        if (valid) {
+            float vals[5];
+            pack_vals(P, v, alpha, weight, vals);
+            film_put(P, B.film, a.x, a.y, vals, k == 0);
+            ++splats;
+        }
+        if (P.record) {
+            float *rr = B.records + ((size_t) i * G + k) * 8;
+            rr[0] = a.x; rr[1] = a.y; rr[2] = v.r; rr[3] = v.g; rr[4] = v.b; rr[5] = alpha; rr[6] = weight;
+            rr[7] = valid ? 1.f : 0.f;
+        }
+    }
+    if (B.stats && splats) atomicAdd(&B.stats[3], splats);
+}
+
+/* develop: rgb / W (hdrfilm.cpp:400) */
+__global__ void k_develop(const float *film, float *out, uint32_t npx, uint32_t alpha) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    uint32_t C = alpha ? 5u : 4u, T = alpha ? 4u : 3u;
+    const float *src = film + (size_t) p * C;
+    float w = src[C - 1];
+    float d = w == 0.f ? 1.f : w;
+    for (uint32_t c = 0; c < T; ++c) out[(size_t) p * T + c] = src[c] / d;
+}
+
+/* ------------------------------------------------------------------ */
+/* Host orchestration                                                 */
+/* ------------------------------------------------------------------ */
+
+static void plan(const amvpt_params &P, uint32_t &spp, uint32_t &spp_pp, uint32_t &n_passes, uint64_t &L) {
+    uint32_t s = P.spp ? P.spp : 1;
+    uint64_t px = (uint64_t) P.film_width * P.film_height;
+    if (P.integrator == AMVPT_INTEGRATOR_MVPATH) {
+        spp_pp = P.spp_pass_lim ? std::min(P.spp_pass_lim, s) : s;
+        n_passes = s / spp_pp;
+        s = n_passes * spp_pp;
+    } else {
+        spp_pp = s;
+        n_passes = 1;
+    }
+    uint64_t wf = px * spp_pp;
+    if (wf > 0xffffffffull) {
+        spp_pp /= (uint32_t) ((wf + 0xffffffffull - 1) / 0xffffffffull);
+        n_passes = s / spp_pp;
+        wf = px * spp_pp;
+    }
+    spp = s;
+    L = wf;
+}
+
+static uint32_t group_size(const amvpt_params &P) {
+    uint32_t N = P.n_views, G = std::min(P.reuse_count, N);
+    if (G == 0 || N % G) {
+        G = 0;
+        for (uint32_t p = 8; p < N; p++) if (N % p == 0) { G = p; break; }
+        if (!G) {
+            for (uint32_t p = 8; p > 1; p--) if (N % p == 0) { G = p; break; }
+            G = G ? G : N;
+        }
+        G = G ? G : N;
+    }
+    return G;
+}
+
+static void gaussian_coeffs(float stddev, FilterCoeffs &f) {
+    static const double cd[10] = {9.992604880e-1, -4.977025247e-1, 1.222248550e-1, -1.932406282e-2,
+                                  2.136713061e-3, -1.679873860e-4, 9.202145248e-6, -3.329417433e-7,
+                                  7.128382794e-9, -6.821193280e-11};
+    f.radius = 4.f * stddev;
+    double scale = 1;
+    for (int i = 0; i < 10; ++i) {
+        f.c[i] = (float) (cd[i] * scale);
+        scale /= ((double) stddev * (double) stddev);
+    }
+    /* coeff[0] -= estrin(radius^2, coeff): same Estrin levels as the device */
+    float x = f.radius * f.radius;
+    const float *c = f.c;
+    float r0 = std::fmaf(x, c[1], c[0]), r1 = std::fmaf(x, c[3], c[2]), r2 = std::fmaf(x, c[5], c[4]),
+          r3 = std::fmaf(x, c[7], c[6]), r4 = std::fmaf(x, c[9], c[8]);
+    float x2 = x * x;
+    float q0 = std::fmaf(x2, r1, r0), q1 = std::fmaf(x2, r3, r2), q2 = r4;
+    float x4 = x2 * x2;
+    float w0 = std::fmaf(x4, q1, q0), w1 = q2;
+    float x8 = x4 * x4;
+    f.c[0] -= std::fmaf(x8, w1, w0);
+}
+
+#define HIPCHK(x)                                                    \
+    do {                                                             \
+        hipError_t e_ = (x);                                         \
+        if (e_ != hipSuccess) return hip_fail(#x, (int) e_);         \
+    } while (0)
+
+struct Arena {
+    void *base = nullptr;
+    size_t bytes = 0;
+    int device = -1;
+};
+static Arena g_arena;
+
+template <int G>
+static void launch_primary(dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *S, const DView *V,
+                           const Bufs &B) {
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G>), grid, dim3(256), lds, st, P, S, V, B);
+}
+template <int G>
+static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G>), grid, dim3(256), 0, st, P, B);
+}
+
+typedef void (*primary_fn)(dim3, size_t, hipStream_t, const KParams &, const DScene *, const DView *, const Bufs &);
+typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
+static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
+                                      launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>};
+static const splat_fn kSplat[] = {nullptr, nullptr, launch_splat<2>, launch_splat<3>, launch_splat<4>,
+                                  launch_splat<5>, launch_splat<6>, launch_splat<7>, launch_splat<8>};
+constexpr uint32_t kMaxG = 8;
+
+amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                         uint64_t lane_begin, uint64_t lane_end, float *film, void *stream,
+                         amvpt_counters *counters, float *records, uint32_t record_pass) {
+    if (!scene || !views || !params || !film) { set_error("amvpt_render: null argument"); return AMVPT_ERR_INVALID; }
+    const amvpt_params &Pp = *params;
+    hipStream_t st = (hipStream_t) stream;
+    uint32_t spp, spp_pp, n_passes;
+    uint64_t L;
+    plan(Pp, spp, spp_pp, n_passes, L);
+    const bool is_mv = Pp.integrator == AMVPT_INTEGRATOR_MVPATH;
+    const bool reuse = is_mv && Pp.sa_reuse && Pp.n_views > 1 && Pp.reuse_count != 1;
+    const uint32_t G = reuse ? group_size(Pp) : 1;
+    if (G > kMaxG) { set_error("amvpt_render: group size > 8 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+    const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
+    if (n_adapt) { set_error("amvpt_render: adaptive > 0 not implemented in this build"); return AMVPT_ERR_UNSUPPORTED; }
+    if (!is_mv && n_passes > 1) { set_error("path: more than 2^32 lanes per frame"); return AMVPT_ERR_UNSUPPORTED; }
+    if (Pp.multisensor && (Pp.grid_x == 0 || Pp.grid_y == 0 || Pp.film_width % Pp.grid_x || Pp.film_height % Pp.grid_y)) {
+        set_error("Film size must be divisible by grid dimensions !");
+        return AMVPT_ERR_INVALID;
+    }
+    for (uint32_t v = 0; v < Pp.n_views; ++v)
+        if (views[v].type != AMVPT_CAMERA_PERSPECTIVE) {
+            set_error("amvpt_render: thinlens sub-sensors not implemented in this build");
+            return AMVPT_ERR_UNSUPPORTED;
+        }
+    if (lane_end > L) lane_end = L;
+    if (lane_begin >= lane_end) {
+        if (counters) *counters = amvpt_counters{};
+        return AMVPT_OK;
+    }
+
+    KParams P{};
+    P.W = Pp.film_width; P.H = Pp.film_height; P.C = Pp.film_alpha ? 5 : 4;
+    P.spp_pp = spp_pp;
+    uint32_t log_spp = 0;
+    while ((1u << log_spp) < spp_pp) ++log_spp;
+    P.log_spp = log_spp;
+    P.pow2 = (1u << log_spp) == spp_pp;
+    P.max_depth = Pp.max_depth; P.rr_depth = Pp.rr_depth;
+    P.sa_mis = Pp.sa_mis; P.fast_mis = Pp.fast_mis; P.debug = Pp.debug; P.n_adapt = n_adapt;
+    P.G = G;
+    P.multisensor = Pp.multisensor; P.n_views = Pp.n_views;
+    P.gx = Pp.grid_x ? Pp.grid_x : 1; P.gy = Pp.grid_y ? Pp.grid_y : 1;
+    P.rev_x = Pp.reverse_x; P.rev_y = Pp.reverse_y;
+    P.sres_x = P.W / P.gx; P.sres_y = P.H / P.gy;
+    P.box = Pp.rfilter == AMVPT_RFILTER_BOX;
+    P.coalesce_single = spp_pp >= 4;
+    P.path_box_pos = (!is_mv && P.box) ? 1 : 0;
+    P.is_mvpath = is_mv;
+    P.inv_w = 1.f / (float) P.W;
+    P.inv_h = 1.f / (float) P.H;
+    P.adapt_w = 1.f / (float) (n_adapt + 1);
+    if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
+
+    /* views to device (tiny) */
+    std::vector<DView> hv(Pp.n_views);
+    for (uint32_t v = 0; v < Pp.n_views; ++v) {
+        const amvpt_view_desc &d = views[v];
+        DView &o = hv[v];
+        std::memcpy(o.to_world, d.to_world, 12 * sizeof(float));
+        std::memcpy(o.to_world_inv, d.to_world_inv, 12 * sizeof(float));
+        std::memcpy(o.sample_to_camera, d.sample_to_camera, 16 * sizeof(float));
+        std::memcpy(o.camera_to_sample, d.camera_to_sample, 16 * sizeof(float));
+        o.near_clip = d.near_clip; o.far_clip = d.far_clip; o.normalization = d.normalization; o.pad0 = 0.f;
+        o.res[0] = d.resolution[0]; o.res[1] = d.resolution[1];
+        o.pp[0] = d.pp_offset[0]; o.pp[1] = d.pp_offset[1];
+    }
+
+    /* lane arena: queues (2 x 6 x 16 B) + lane_out/lane_rec (32 B) + view records (48 B x G) */
+    const uint64_t span = lane_end - lane_begin;
+    const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
+    const size_t per_lane = 12 * 16 + 32 + (size_t) 48 * G + (records ? 0 : 0);
+    const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
+    const size_t need = views_bytes + 256 + 64 + per_lane * chunk + 4096;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (g_arena.bytes < need || g_arena.device != dev) {
+        if (g_arena.base) (void) hipFree(g_arena.base);
+        g_arena.base = nullptr;
+        g_arena.bytes = 0;
+        if (hipMalloc(&g_arena.base, need) != hipSuccess) {
+            set_error("amvpt_render: device allocation of the lane arena failed");
+            return AMVPT_ERR_OOM;
+        }
+        g_arena.bytes = need;
+        g_arena.device = dev;
+    }
+    char *base = (char *) g_arena.base;
+    DView *dviews = (DView *) base;
+    unsigned long long *dstats = (unsigned long long *) (base + views_bytes);
+    uint32_t *dcnt = (uint32_t *) (base + views_bytes + 64);
+    char *p = base + views_bytes + 256 + 64;
+    auto carve = [&](size_t bytes) { char *r = p; p += (bytes + 255) & ~(size_t) 255; return r; };
+    HIPCHK(hipMemcpyAsync(dviews, hv.data(), hv.size() * sizeof(DView), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(dstats, 0, 64, st));
+
+    Bufs B{};
+    float4 *qa[6], *qb[6];
+    for (int k = 0; k < 6; ++k) qa[k] = (float4 *) carve(16 * chunk);
+    for (int k = 0; k < 6; ++k) qb[k] = (float4 *) carve(16 * chunk);
+    B.lane_out = (float4 *) carve(16 * chunk);
+    B.lane_rec = (float4 *) carve(16 * chunk);
+    B.view_rec = (float4 *) carve((size_t) 48 * G * chunk);
+    B.film = film;
+    B.records = records;
+    B.stats = dstats;
+
+    const DScene *dS = (const DScene *) scene->dev_scene_struct;
+    const size_t lds = scene->dev.lds_bytes <= kLdsSceneBytes ? scene->dev.lds_bytes : 0;
+    hipEvent_t ev[4];
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;
+    auto t0 = std::chrono::steady_clock::now();
+    const uint32_t max_bounces = P.max_depth == 0xffffffffu ? 0xffffffffu : P.max_depth + 1;
+
+    for (uint32_t pass = 0; pass < n_passes; ++pass) {
+        P.seed_value = Pp.base_seed + (is_mv ? (spp_pp * pass + Pp.seed) : Pp.seed);
+        P.record = (records && pass == record_pass) ? 1u : 0u;
+        for (uint64_t c0 = lane_begin; c0 < lane_end; c0 += chunk) {
+            const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, lane_end - c0);
+            P.chunk_begin = c0;
+            P.chunk_n = cn;
+            B.records = P.record ? records + (size_t) (c0 - lane_begin) * G * 8 : records;
+            const dim3 grid((cn + 255) / 256);
+            /* counters: [0] = queue A, [1] = queue B */
+            HIPCHK(hipMemsetAsync(dcnt, 0, 2 * sizeof(uint32_t), st));
+            for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
+            B.cnt_out = dcnt; B.cnt_in = dcnt + 1;
+            HIPCHK(hipEventRecord(ev[0], st));
+            if (G == 1) {
+                hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
+            } else {
+                kPrimary[G](grid, lds, st, P, dS, dviews, B);
+            }
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(ev[1], st));
+            /* suffix bounces: ping-pong A <-> B */
+            const uint32_t bgrid = std::min<uint32_t>((cn + 255) / 256, 256 * 16);
+            bool a_is_in = true;
+            for (uint32_t bnc = 0; bnc < max_bounces; ++bnc) {
+                for (int k = 0; k < 6; ++k) {
+                    B.q_in[k] = a_is_in ? qa[k] : qb[k];
+                    B.q_out[k] = a_is_in ? qb[k] : qa[k];
+                }
+                B.cnt_in = a_is_in ? dcnt : dcnt + 1;
+                B.cnt_out = a_is_in ? dcnt + 1 : dcnt;
+                HIPCHK(hipMemsetAsync(B.cnt_out, 0, sizeof(uint32_t), st));
+                hipLaunchKernelGGL(k_bounce, dim3(bgrid), dim3(256), lds, st, P, dS, B);
+                HIPCHK(hipGetLastError());
+                a_is_in = !a_is_in;
+                if (bnc >= 15 && (bnc & 7) == 7) { /* unbounded depth: poll the live count */
+                    uint32_t live = 0;
+                    HIPCHK(hipMemcpyAsync(&live, B.cnt_out, 4, hipMemcpyDeviceToHost, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    if (live == 0) break;
+                }
+            }
+            HIPCHK(hipEventRecord(ev[2], st));
+            if (G == 1) hipLaunchKernelGGL(k_splat_single, grid, dim3(256), 0, st, P, B);
+            else kSplat[G](grid, st, P, B);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(ev[3], st));
+            if (counters) {
+                HIPCHK(hipEventSynchronize(ev[3]));
+                float a = 0, b = 0, c = 0;
+                HIPCHK(hipEventElapsedTime(&a, ev[0], ev[1]));
+                HIPCHK(hipEventElapsedTime(&b, ev[1], ev[2]));
+                HIPCHK(hipEventElapsedTime(&c, ev[2], ev[3]));
+                ms_primary += a; ms_bounce += b; ms_splat += c;
+            }
+        }
+    }
+    if (counters) {
+        unsigned long long hs[8] = {0};
+        HIPCHK(hipMemcpyAsync(hs, dstats, 64, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        amvpt_counters &c = *counters;
+        c = amvpt_counters{};
+        c.lanes = span * n_passes;
+        c.passes = n_passes;
+        c.vertices = hs[0];
+        c.reuse_lanes = hs[1];
+        c.visibility_rays = hs[2];
+        c.view_splats = hs[3];
+        c.kernel_ms_primary = ms_primary;
+        c.kernel_ms_bounce = ms_bounce;
+        c.kernel_ms_splat = ms_splat;
+        c.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (auto &e : ev) (void) hipEventDestroy(e);
+    return AMVPT_OK;
+}
+
+amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream) {
+    uint32_t npx = w * h;
+    hipLaunchKernelGGL(k_develop, dim3((npx + 255) / 256), dim3(256), 0, (hipStream_t) stream, film, out, npx, alpha);
+    HIPCHK(hipGetLastError());
+    return AMVPT_OK;
+}
+
+} // namespace amvpt

@@ -1,0 +1,315 @@
+/*
+ * dgeom.h -- ray/primitive intersection, BVH traversal and surface
+ * interactions on gfx950.
+ *
+ * Closest hit = minimum (t, BVH primitive index); BVH boxes are built with a
+ * relative outward pad so that the box test never culls a primitive whose hit
+ * distance is <= the current best.  The hit record is therefore the same as a
+ * brute-force scan and independent of traversal order.
+ *
+ * Reference (file:line): Rectangle ray_intersect_preliminary / SI
+ * src/shapes/rectangle.cpp:447-563; Mesh SI src/render/mesh.cpp:1393-1560 and
+ * moeller_trumbore include/mitsuba/render/mesh.h:467-488; Sphere
+ * src/shapes/sphere.cpp:460-718; finalize/initialize_sh_frame
+ * include/mitsuba/render/interaction.h:278-288,497-517; spawn_ray*
+ * interaction.h:140-169.
+ */
+#pragma once
+#include "dmath.h"
+#include "dscene.h"
+
+namespace amvpt {
+
+struct Ray { f3 o, d; float maxt; };
+AD f3 ray_at(const Ray &r, float t) { return fma3(r.d, t, r.o); }
+
+/* Scene tables as seen by a kernel; nodes/prims may point into LDS. */
+struct SceneRef {
+    const DNode *nodes;
+    const DPrim *prims;
+    const DScene *g;
+};
+
+struct Hit { float t, u, v; int32_t prim; };
+
+AD bool rect_hit(const DPrim &p, const Ray &r, float &t, float &lx, float &ly) {
+    /* to_object.transform_affine(ray) then plane z=0 (rectangle.cpp:447-467) */
+    f3 o = {fmadd(p.a[2], r.o.z, fmadd(p.a[1], r.o.y, fmadd(p.a[0], r.o.x, p.a[3]))),
+            fmadd(p.b[2], r.o.z, fmadd(p.b[1], r.o.y, fmadd(p.b[0], r.o.x, p.b[3]))),
+            fmadd(p.c[2], r.o.z, fmadd(p.c[1], r.o.y, fmadd(p.c[0], r.o.x, p.c[3])))};
+    f3 d = {fmadd(p.a[2], r.d.z, fmadd(p.a[1], r.d.y, p.a[0] * r.d.x)),
+            fmadd(p.b[2], r.d.z, fmadd(p.b[1], r.d.y, p.b[0] * r.d.x)),
+            fmadd(p.c[2], r.d.z, fmadd(p.c[1], r.d.y, p.c[0] * r.d.x))};
+    t = -o.z / d.z;
+    f3 local = fma3(d, t, o);
+    lx = local.x; ly = local.y;
+    return t >= 0.f && t <= r.maxt && fabs_(local.x) <= 1.f && fabs_(local.y) <= 1.f;
+}
+
+AD bool tri_hit(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
+    f3 p0 = ld3(p.a), p1 = ld3(p.b), p2 = ld3(p.c);
+    f3 e1 = p1 - p0, e2 = p2 - p0;
+    f3 pvec = cross(r.d, e2);
+    float inv_det = rcp(dot(e1, pvec));
+    f3 tvec = r.o - p0;
+    u = dot(tvec, pvec) * inv_det;
+    bool active = u >= 0.f && u <= 1.f;
+    f3 qvec = cross(tvec, e1);
+    v = dot(r.d, qvec) * inv_det;
+    active = active && v >= 0.f && u + v <= 1.f;
+    t = dot(e2, qvec) * inv_det;
+    return active && t >= 0.f && t <= r.maxt;
+}
+
+/* float64 sphere test, as the llvm variants compute it (sphere.cpp:460-518) */
+AD bool sphere_hit(const DPrim &p, const Ray &ray, float &t_out) {
+    double cx = p.a[0], cy = p.a[1], cz = p.a[2], r = p.a[3];
+    double ox = ray.o.x, oy = ray.o.y, oz = ray.o.z, dx = ray.d.x, dy = ray.d.y, dz = ray.d.z;
+    double maxt = ray.maxt;
+    double lx = ox - cx, ly = oy - cy, lz = oz - cz;
+    double dn = __builtin_sqrt(__builtin_fma(dz, dz, __builtin_fma(dy, dy, dx * dx)));
+    double plane_t = __builtin_fma(-lz, dz, __builtin_fma(-ly, dy, -lx * dx)) / dn;
+    bool no_hit = plane_t == 0.0 && (ray.o.x != p.a[0] && ray.o.y != p.a[1] && ray.o.z != p.a[2]);
+    f3 pp = ray_at(ray, (float) plane_t);
+    double ppx = (double) pp.x - cx, ppy = (double) pp.y - cy, ppz = (double) pp.z - cz;
+    no_hit = no_hit && (__builtin_sqrt(__builtin_fma(ppz, ppz, __builtin_fma(ppy, ppy, ppx * ppx))) > r);
+    double A = __builtin_fma(dz, dz, __builtin_fma(dy, dy, dx * dx));
+    double B = 2.0 * __builtin_fma(ppz, dz, __builtin_fma(ppy, dy, ppx * dx));
+    double C = __builtin_fma(ppz, ppz, __builtin_fma(ppy, ppy, ppx * ppx)) - r * r;
+    bool linear = A == 0.0, valid_linear = linear && B != 0.0;
+    double x0 = -C / B, x1 = x0;
+    double discrim = __builtin_fma(B, B, -(4.0 * A * C));
+    bool valid_quad = !linear && discrim >= 0.0;
+    {
+        double sq = __builtin_sqrt(discrim);
+        double temp = -0.5 * (B + __builtin_copysign(sq, B));
+        double x0p = temp / A, x1p = C / temp;
+        /* std::min / std::max semantics, as in the oracle */
+        double x0m = x1p < x0p ? x1p : x0p, x1m = x0p < x1p ? x1p : x0p;
+        x0 = linear ? x0 : x0m;
+        x1 = linear ? x0 : x1m;
+    }
+    bool found = valid_linear || valid_quad;
+    double near_t = x0 + plane_t, far_t = x1 + plane_t;
+    bool out_bounds = !(near_t <= maxt && far_t >= 0.0);
+    bool in_bounds = near_t < 0.0 && far_t > maxt;
+    bool active = found && !no_hit && !out_bounds && !in_bounds;
+    t_out = active ? (near_t < 0.0 ? (float) far_t : (float) near_t) : kInf;
+    return active;
+}
+
+AD bool prim_hit(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
+    if (p.type == PRIM_RECT) return rect_hit(p, r, t, u, v);
+    if (p.type == PRIM_TRI) return tri_hit(p, r, t, u, v);
+    u = v = 0.f;
+    return sphere_hit(p, r, t);
+}
+
+/* Slab test with inclusive bounds; boxes carry a relative pad from the builder. */
+AD bool box_hit(const DNode &n, f3 o, f3 inv_d, float tmax, float &tnear) {
+    float tx0 = (n.lo[0] - o.x) * inv_d.x, tx1 = (n.hi[0] - o.x) * inv_d.x;
+    float ty0 = (n.lo[1] - o.y) * inv_d.y, ty1 = (n.hi[1] - o.y) * inv_d.y;
+    float tz0 = (n.lo[2] - o.z) * inv_d.z, tz1 = (n.hi[2] - o.z) * inv_d.z;
+    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+    float tm = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tnear = tmin;
+    return tmin <= tm;
+}
+
+constexpr int kStack = 48;
+
+/* Closest hit over the BVH (ties broken toward the lower primitive index). */
+/* 1/d with zero components replaced by +-1e-30 so that (bound - o) * inv never is 0*inf */
+AD f3 safe_inv(f3 d) {
+    return {1.f / (d.x != 0.f ? d.x : mulsign(1e-30f, d.x)), 1.f / (d.y != 0.f ? d.y : mulsign(1e-30f, d.y)),
+            1.f / (d.z != 0.f ? d.z : mulsign(1e-30f, d.z))};
+}
+
+AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
+    Hit best{kInf, 0.f, 0.f, -1};
+    uint32_t best_orig = 0xffffffffu;
+    f3 inv_d = safe_inv(ray.d);
+    uint32_t stack[kStack];
+    int sp = 0;
+    uint32_t node = 0;
+    float tmax_box = ray.maxt;
+    while (true) {
+        const DNode n = sc.nodes[node];
+        if (n.count) {
+            for (uint32_t i = 0; i < n.count; ++i) {
+                uint32_t pi = n.left_or_first + i;
+                const DPrim p = sc.prims[pi];
+                float t, u, v;
+                if (prim_hit(p, ray, t, u, v)) {
+                    /* ties resolve toward the lower scene-order primitive index (p.pad) */
+                    if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                        best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                        best_orig = p.pad;
+                        tmax_box = t;
+                    }
+                }
+            }
+        } else {
+            uint32_t l = n.left_or_first, r = l + 1;
+            float tl, tr;
+            bool hl = box_hit(sc.nodes[l], ray.o, inv_d, tmax_box, tl);
+            bool hr = box_hit(sc.nodes[r], ray.o, inv_d, tmax_box, tr);
+            if (hl && hr) {
+                uint32_t first = tl <= tr ? l : r, second = tl <= tr ? r : l;
+                if (sp < kStack) stack[sp++] = second;
+                node = first;
+                continue;
+            }
+            if (hl) { node = l; continue; }
+            if (hr) { node = r; continue; }
+        }
+        if (sp == 0) break;
+        node = stack[--sp];
+        /* prune with the current best */
+    }
+    return best;
+}
+
+/* Any hit in [0, maxt] (Scene::ray_test). */
+AD bool trace_any(const SceneRef &sc, const Ray &ray) {
+    f3 inv_d = safe_inv(ray.d);
+    uint32_t stack[kStack];
+    int sp = 0;
+    uint32_t node = 0;
+    while (true) {
+        const DNode n = sc.nodes[node];
+        if (n.count) {
+            for (uint32_t i = 0; i < n.count; ++i) {
+                const DPrim p = sc.prims[n.left_or_first + i];
+                float t, u, v;
+                if (prim_hit(p, ray, t, u, v)) return true;
+            }
+        } else {
+            uint32_t l = n.left_or_first, r = l + 1;
+            float tl, tr;
+            bool hl = box_hit(sc.nodes[l], ray.o, inv_d, ray.maxt, tl);
+            bool hr = box_hit(sc.nodes[r], ray.o, inv_d, ray.maxt, tr);
+            if (hl && hr) {
+                if (sp < kStack) stack[sp++] = r;
+                node = l;
+                continue;
+            }
+            if (hl) { node = l; continue; }
+            if (hr) { node = r; continue; }
+        }
+        if (sp == 0) break;
+        node = stack[--sp];
+    }
+    return false;
+}
+
+/* SurfaceInteraction3f restricted to what the path reads. */
+struct SI {
+    float t;
+    f3 p, n;
+    Frame3 sh;
+    f3 wi;
+    int32_t shape;
+    AD bool valid() const { return t != kInf; }
+};
+
+AD SI compute_si(const SceneRef &sc, const Ray &ray, const Hit &h) {
+    SI si;
+    si.shape = -1;
+    if (h.prim < 0) {
+        si.t = kInf;
+        si.p = mk(0.f, 0.f, 0.f);
+        si.n = mk(0.f, 0.f, 0.f);
+        si.sh = Frame3{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f)};
+        si.wi = -ray.d;
+        return si;
+    }
+    const DPrim pr = sc.prims[h.prim];
+    const DShape &s = sc.g->shapes[pr.shape];
+    si.shape = (int32_t) pr.shape;
+    si.t = h.t;
+    f3 dp_du;
+    if (pr.type == PRIM_RECT) {
+        f3 p = ray_at(ray, h.t);
+        f3 tr = mk(s.to_world[3], s.to_world[7], s.to_world[11]);
+        f3 fn = ld3(s.frame_n);
+        float dist = dot(tr - p, fn);
+        si.p = p + dist * fn;
+        si.n = fn;
+        si.sh.n = fn;
+        dp_du = ld3(s.frame_s);
+    } else if (pr.type == PRIM_TRI) {
+        const uint32_t *fi = sc.g->faces + 3 * (size_t) (s.fbase + pr.face);
+        uint32_t i0 = s.vbase + fi[0], i1 = s.vbase + fi[1], i2 = s.vbase + fi[2];
+        f3 p0 = ld3(sc.g->vpos + 3 * (size_t) i0), p1 = ld3(sc.g->vpos + 3 * (size_t) i1),
+           p2 = ld3(sc.g->vpos + 3 * (size_t) i2);
+        float b1 = h.u, b2 = h.v, b0 = 1.f - b1 - b2;
+        si.p = fma3(p0, b0, fma3(p1, b1, p2 * b2));
+        si.n = normalize(cross(p1 - p0, p2 - p0));
+        f3 dpdv;
+        coord_sys(si.n, dp_du, dpdv);
+        if (s.has_uv) {
+            const float *uv = sc.g->vuv;
+            float u0x = uv[2 * i0], u0y = uv[2 * i0 + 1], u1x = uv[2 * i1], u1y = uv[2 * i1 + 1],
+                  u2x = uv[2 * i2], u2y = uv[2 * i2 + 1];
+            float d0x = u1x - u0x, d0y = u1y - u0y, d1x = u2x - u0x, d1y = u2y - u0y;
+            float det = fmsub(d0x, d1y, d0y * d1x), inv_det = rcp(det);
+            if (det != 0.f) {
+                f3 dp0 = p1 - p0, dp1 = p2 - p0;
+                dp_du = mk(fmsub(d1y, dp0.x, d0y * dp1.x) * inv_det, fmsub(d1y, dp0.y, d0y * dp1.y) * inv_det,
+                           fmsub(d1y, dp0.z, d0y * dp1.z) * inv_det);
+            }
+        }
+        if (s.has_normals) {
+            f3 n0 = ld3(sc.g->vnrm + 3 * (size_t) i0), n1 = ld3(sc.g->vnrm + 3 * (size_t) i1),
+               n2 = ld3(sc.g->vnrm + 3 * (size_t) i2);
+            f3 n = fma3(n2, b2, fma3(n1, b1, n0 * b0));
+            float il = rsqrt_(sqnorm(n));
+            si.sh.n = n * il;
+        } else {
+            si.sh.n = si.n;
+        }
+        if (s.flip) { si.n = -si.n; si.sh.n = -si.sh.n; }
+    } else {
+        f3 c = ld3(s.center);
+        si.sh.n = normalize(ray_at(ray, h.t) - c);
+        si.p = fma3(si.sh.n, s.radius, c);
+        const float *to = s.to_object;
+        f3 local = {fmadd(to[2], si.p.z, fmadd(to[1], si.p.y, fmadd(to[0], si.p.x, to[3]))),
+                    fmadd(to[6], si.p.z, fmadd(to[5], si.p.y, fmadd(to[4], si.p.x, to[7]))),
+                    fmadd(to[10], si.p.z, fmadd(to[9], si.p.y, fmadd(to[8], si.p.x, to[11])))};
+        dp_du = mk(-local.y, local.x, 0.f);
+        const float *tw = s.to_world;
+        dp_du = mk(fmadd(tw[2], dp_du.z, fmadd(tw[1], dp_du.y, tw[0] * dp_du.x)),
+                   fmadd(tw[6], dp_du.z, fmadd(tw[5], dp_du.y, tw[4] * dp_du.x)),
+                   fmadd(tw[10], dp_du.z, fmadd(tw[9], dp_du.y, tw[8] * dp_du.x))) * (2.f * kPi);
+        if (s.flip) si.sh.n = -si.sh.n;
+        si.n = si.sh.n;
+    }
+    /* initialize_sh_frame */
+    si.sh.s = normalize(fma3(si.sh.n, -dot(si.sh.n, dp_du), dp_du));
+    if (dp_du.x == 0.f && dp_du.y == 0.f && dp_du.z == 0.f) {
+        f3 s0, t0;
+        coord_sys(si.sh.n, s0, t0);
+        si.sh.s = s0;
+    }
+    si.sh.t = cross(si.sh.n, si.sh.s);
+    si.wi = si.sh.to_local(-ray.d);
+    return si;
+}
+
+AD f3 offset_p(f3 p, f3 n, f3 d) {
+    float mag = (1.f + hmax3(mk(fabs_(p.x), fabs_(p.y), fabs_(p.z)))) * kRayEps;
+    mag = mulsign(mag, dot(n, d));
+    return fma3(n, mag, p);
+}
+AD Ray spawn_ray(f3 p, f3 n, f3 d) { return Ray{offset_p(p, n, d), d, kLargest}; }
+AD Ray spawn_ray_to(f3 p, f3 n, f3 t) {
+    f3 o = offset_p(p, n, t - p);
+    f3 d = t - o;
+    float dist = norm(d);
+    d = d / dist;
+    return Ray{o, d, dist * (1.f - kShadowEps)};
+}
+
+} // namespace amvpt

@@ -1,0 +1,88 @@
+/*
+ * dscene.h -- device-resident scene layout of the AMVPT hot path (HBM).
+ *
+ * Everything the per-lane kernels read about the scene lives in a handful of
+ * small, read-only tables that fit the Infinity Cache / L2 (Cornell box: ~6 KB)
+ * and are staged into LDS at kernel start when they fit (kLdsSceneBytes):
+ *   nodes[]   binary BVH, 32 B per node                (replaces Embree, scene_embree.inl)
+ *   prims[]   BVH-ordered primitives, 64 B each        (rectangle / triangle / sphere)
+ *   shapes[]  per-shape transforms, frames, mesh bases (rectangle.cpp, mesh.cpp, sphere.cpp)
+ *   bsdfs[]   flattened BSDF parameters                (diffuse / roughconductor / twosided)
+ *   emitters[] area lights                             (area.cpp)
+ *   views[]   per-sub-sensor projective transforms     (grid.cpp + perspective.cpp)
+ *   mesh vertex / normal / texcoord / face streams     (mesh.cpp)
+ */
+#pragma once
+#include <stdint.h>
+
+namespace amvpt {
+
+enum : uint32_t { PRIM_RECT = 0, PRIM_TRI = 1, PRIM_SPHERE = 2 };
+
+struct alignas(16) DNode {
+    float lo[3];
+    uint32_t left_or_first;  /* inner: index of left child (right = left + 1); leaf: first prim */
+    float hi[3];
+    uint32_t count;          /* 0: inner node; >0: leaf with `count` prims */
+};
+
+struct alignas(16) DPrim {
+    /* rect: rows 0..2 of to_object; tri: p0, p1, p2 (xyz); sphere: a = (center, radius) */
+    float a[4], b[4], c[4];
+    uint32_t type, shape, face;
+    uint32_t pad;            /* scene-order primitive index: closest-hit tie-break */
+};
+
+struct DShape {
+    uint32_t type, flip;
+    int32_t bsdf, emitter;
+    float to_world[12];     /* rows 0..2 of the 4x4 */
+    float to_object[12];
+    float frame_s[3], frame_t[3], frame_n[3]; /* rectangle m_frame */
+    float inv_area;
+    uint32_t vbase, fbase, has_normals, has_uv;
+    float center[3], radius;
+};
+
+struct DBsdf {
+    uint32_t type, distribution, sample_visible, has_spec;
+    int32_t nested0, nested1;
+    uint32_t flags;         /* BSDFFlags of the whole BSDF (bsdf.h:37-86) */
+    uint32_t pad;
+    float refl[3];
+    float alpha_u, alpha_v; /* raw (eval_roughness) */
+    float eta[3], k[3], spec[3];
+};
+
+struct DEmitter {
+    int32_t shape;
+    uint32_t pad;
+    float radiance[3];
+    float pad2;
+};
+
+struct DView {
+    float to_world[12];
+    float to_world_inv[12];
+    float sample_to_camera[16];
+    float camera_to_sample[16];
+    float near_clip, far_clip, normalization, pad0;
+    float res[2], pp[2];
+};
+
+struct DScene {
+    const DNode *nodes;
+    const DPrim *prims;
+    const DShape *shapes;
+    const DBsdf *bsdfs;
+    const DEmitter *emitters;
+    const float *vpos;      /* xyz per vertex */
+    const float *vnrm;
+    const float *vuv;
+    const uint32_t *faces;  /* 3 per face, indices relative to the shape's vbase */
+    uint32_t n_nodes, n_prims, n_shapes, n_emitters;
+    float emitter_pmf;
+    uint32_t lds_bytes;     /* nodes+prims footprint (LDS staging when small) */
+};
+
+} // namespace amvpt

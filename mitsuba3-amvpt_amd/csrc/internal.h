@@ -1,0 +1,28 @@
+/*
+ * internal.h -- host-side state shared by the C-ABI (amvpt_capi.cpp) and the
+ * kernel launcher (amvpt_render.hip).  Not part of the public interface.
+ */
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/amvpt.h"
+#include "dscene.h"
+
+struct amvpt_scene {
+    amvpt::DScene dev;          /* device pointers */
+    void *dev_scene_struct = nullptr; /* device copy of `dev` */
+    std::vector<void *> allocations;
+    uint32_t n_nodes = 0, n_prims = 0;
+    int device = 0;
+};
+
+namespace amvpt {
+void set_error(const std::string &msg);
+amvpt_status hip_fail(const char *what, int err);
+amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                         uint64_t lane_begin, uint64_t lane_end, float *film, void *stream,
+                         amvpt_counters *counters, float *records, uint32_t record_pass);
+amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream);
+extern uint64_t g_chunk_lanes;
+} // namespace amvpt

@@ -1,0 +1,99 @@
+"""
+oracle.py -- TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU parity oracle
+(oracle/build/liboracle.so, built from oracle/amvpt_oracle.cpp by oracle/Makefile).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module; the product path never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ORACLE_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+_lib = None
+
+
+class OracleStats(ctypes.Structure):
+    _fields_ = [("lanes", ctypes.c_uint64), ("vertices", ctypes.c_uint64), ("reuse_lanes", ctypes.c_uint64),
+                ("visibility_rays", ctypes.c_uint64), ("adaptive_lanes", ctypes.c_uint64),
+                ("seconds", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.oracle_render.restype = ctypes.c_int
+        L.oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                    ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_uint32, ctypes.POINTER(OracleStats)]
+        L.oracle_plan.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
+        L.oracle_tea_float32.restype = ctypes.c_float
+        L.oracle_tea_float64.restype = ctypes.c_double
+        L.oracle_gaussian_eval.restype = ctypes.c_float
+        L.oracle_gaussian_eval.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.oracle_microfacet_eval.restype = ctypes.c_float
+        L.oracle_microfacet_eval.argtypes = [ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        L.oracle_microfacet_smith_g1.restype = ctypes.c_float
+        L.oracle_microfacet_smith_g1.argtypes = [ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+                                                 ctypes.c_void_p]
+        L.oracle_microfacet_pdf.restype = ctypes.c_float
+        L.oracle_microfacet_pdf.argtypes = [ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_microfacet_sample.argtypes = [ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+                                               ctypes.c_void_p]
+        L.oracle_fresnel_conductor.restype = ctypes.c_float
+        L.oracle_fresnel_conductor.argtypes = [ctypes.c_float] * 3
+        _lib = L
+    return _lib
+
+
+def plan(params):
+    L = lib()
+    a, b, c, g = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    lanes = ctypes.c_uint64()
+    L.oracle_plan(ctypes.byref(params), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(lanes),
+                  ctypes.byref(g))
+    return dict(spp=a.value, spp_per_pass=b.value, passes=c.value, lanes=lanes.value, group=g.value)
+
+
+def render(scene_desc_ptr, views_ptr, params, lane_begin=0, lane_end=2 ** 64 - 1, threads=0,
+           record_pass=None, film=None):
+    """Render into a (H, W, C) float32 film; optionally return per-lane records of one pass."""
+    L = lib()
+    C = 5 if params.film_alpha else 4
+    if film is None:
+        film = np.zeros((params.film_height, params.film_width, C), dtype=np.float32)
+    rec = None
+    if record_pass is not None:
+        pl = plan(params)
+        end = min(lane_end, pl["lanes"])
+        rec = np.zeros((max(0, end - lane_begin), pl["group"], 8), dtype=np.float32)
+    st = OracleStats()
+    rc = L.oracle_render(ctypes.cast(scene_desc_ptr, ctypes.c_void_p), ctypes.cast(views_ptr, ctypes.c_void_p),
+                         ctypes.addressof(params), lane_begin, lane_end, film.ctypes.data, threads,
+                         rec.ctypes.data if rec is not None else None,
+                         record_pass if record_pass is not None else 0, ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError("oracle_render failed (status %d: unsupported configuration)" % rc)
+    return film, rec, st.as_dict()
+
+
+def develop(film, alpha=False):
+    """hdrfilm develop: RGB[A] / W (W == 0 -> 1), hdrfilm.cpp:400."""
+    w = film[..., -1:]
+    n = 4 if alpha else 3
+    return film[..., :n] / np.where(w == 0, 1.0, w)

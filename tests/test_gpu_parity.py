@@ -1,0 +1,129 @@
+"""GPU parity: the HIP pipeline (through the C-ABI) against the CPU oracle.
+
+Bar (DESIGN.md "Parity"): every per-lane, per-view ImageBlock::put record
+(position, RGB value, alpha, weight, validity) is bit-identical to the
+oracle's on the same seeds; the accumulated film agrees to float-atomic
+reordering (relative 1e-5 of the film's scale); sharded lane ranges sum to the
+full frame.  Sizes are chosen so the oracle finishes in seconds.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import SCENES
+
+pytestmark = pytest.mark.gpu
+
+CBOX = os.path.join(SCENES, "cbox_grid.xml")
+CBOX_PATH = os.path.join(SCENES, "cbox_path.xml")
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records=True):
+    torch = _torch()
+    dev = amvpt_mod.DeviceScene(sd)
+    C = 5 if p.film_alpha else 4
+    lane_end = plan["lanes"] if lane_end is None else lane_end
+    film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
+    rec = None
+    if records:
+        rec = torch.zeros((lane_end - lane_begin, plan["group"], 8), dtype=torch.float32, device="cuda")
+        dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, lane_begin, lane_end)
+    else:
+        dev.render(vd, p, film.data_ptr(), lane_begin, lane_end)
+    torch.cuda.synchronize()
+    return film.cpu().numpy(), (rec.cpu().numpy() if rec is not None else None)
+
+
+def _bit_equal(a, b):
+    return (a == b) | (np.isnan(a) & np.isnan(b))
+
+
+def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0):
+    sd, vd, p = scene.describe(0, seed, spp)
+    plan = oracle.plan(p)
+    gfilm, grec = _gpu_render(amvpt_mod, sd, vd, p, plan)
+    ofilm, orec, _ = oracle.render(sd, vd, p, threads=16, record_pass=0)
+    eq = _bit_equal(grec, orec)
+    match = eq.all(axis=(1, 2)).mean()
+    if match < min_match:
+        bad = np.argwhere(~eq.all(axis=(1, 2)))[:5, 0]
+        for lane in bad:
+            print("lane", lane, "\ngpu", grec[lane], "\noracle", orec[lane])
+    assert match >= min_match, "lane records: %.6f bit-identical" % match
+    scale = np.abs(ofilm).max()
+    err = np.abs(gfilm - ofilm).max() / scale
+    assert err < 1e-5, "film max relative difference %.3e" % err
+    return gfilm, ofilm
+
+
+def test_mvpath_single_view_reuse_off(gpu_ready, amvpt_mod, oracle):
+    """G = 1 (render_sample / sample_single), 4-view grid, 16 spp."""
+    s = amvpt_mod.load_file(CBOX, res=48, spp=16, reuse=1)
+    _check(amvpt_mod, oracle, s)
+
+
+def test_mvpath_amvpt_mis_g4(gpu_ready, amvpt_mod, oracle):
+    """C2 shape at reduced size: 4 views, reuse 4, sa_mis (camera selection + MIS weights)."""
+    s = amvpt_mod.load_file(CBOX, res=48, spp=16)
+    _check(amvpt_mod, oracle, s)
+
+
+def test_mvpath_amvpt_mis_g8_two_passes(gpu_ready, amvpt_mod, oracle):
+    """M shape at reduced size: 8 views (4x2 grid), reuse 8, 32 spp in 2 passes of 16."""
+    s = amvpt_mod.load_file(CBOX, res=24, spp=32, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert oracle.plan(p)["passes"] == 2
+    _check(amvpt_mod, oracle, s)
+
+
+def test_mvpath_reuse_without_mis(gpu_ready, amvpt_mod, oracle):
+    s = amvpt_mod.load_file(CBOX, res=48, spp=16, sa_mis="false")
+    _check(amvpt_mod, oracle, s)
+
+
+def test_mvpath_fast_mis(gpu_ready, amvpt_mod, oracle):
+    s = amvpt_mod.load_file(CBOX, res=48, spp=16, fast_mis="true")
+    _check(amvpt_mod, oracle, s)
+
+
+def test_mvpath_seed_and_odd_spp(gpu_ready, amvpt_mod, oracle):
+    """Non-power-of-two spp per pass (idx / spp division path) and a non-zero seed."""
+    s = amvpt_mod.load_file(CBOX, res=32, spp=12, spp_pass_lim=6)
+    _check(amvpt_mod, oracle, s, seed=7)
+
+
+def test_path_integrator_c1(gpu_ready, amvpt_mod, oracle):
+    """C1 plumbing: stock `path` on a single perspective camera (reduced resolution)."""
+    s = amvpt_mod.load_file(CBOX_PATH, res=64, spp=16)
+    _check(amvpt_mod, oracle, s)
+
+
+def test_sharded_lanes_sum_to_frame(gpu_ready, amvpt_mod, oracle):
+    """Multi-GPU partitioning contract: lane ranges keep their global TEA seeds."""
+    s = amvpt_mod.load_file(CBOX, res=32, spp=16)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    L = plan["lanes"]
+    full, _ = _gpu_render(amvpt_mod, sd, vd, p, plan, records=False)
+    cuts = [0, L // 3, (2 * L) // 3 + 5, L]
+    parts = sum(_gpu_render(amvpt_mod, sd, vd, p, plan, a, b, records=False)[0] for a, b in zip(cuts, cuts[1:]))
+    err = np.abs(parts - full).max() / np.abs(full).max()
+    assert err < 1e-5
+
+
+def test_host_render_matches_oracle_develop(gpu_ready, amvpt_mod, oracle):
+    """Integrator::render() through the host framework (develop=True) vs oracle develop()."""
+    s = amvpt_mod.load_file(CBOX, res=32, spp=16)
+    img = amvpt_mod.render(s)
+    sd, vd, p = s.describe(0, 0, 0)
+    ofilm, _, _ = oracle.render(sd, vd, p, threads=16)
+    ref = oracle.develop(ofilm)
+    rmse = float(np.sqrt(np.mean((img - ref) ** 2)))
+    assert rmse < 1e-5, rmse
