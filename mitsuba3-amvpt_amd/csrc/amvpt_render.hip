@@ -270,6 +270,145 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
     }
 }
 
+/* ------------------------------------------------------------------ */
+/* Block-cooperative ImageBlock::put                                   */
+/* ------------------------------------------------------------------ */
+/*
+ * Every thread of a 256-thread block calls block_put() with its own sample
+ * (`valid` may be false).  The block's footprints are accumulated in an LDS
+ * window with LDS float atomics and the window is flushed once with global
+ * float atomics (skipping cells that received nothing), so the film sees about
+ * one atomic per touched pixel-channel per block instead of one per sample.
+ * Footprints that do not fit the window fall back to direct global atomics.
+ * The per-cell weights are exactly those of film_put (imageblock.cpp:174-559).
+ */
+constexpr int kWinW = 64, kWinH = 16;
+struct SplatLds {
+    float win[kWinW * kWinH * 5];
+    int bb[4][4];
+};
+
+struct Foot { int x0, y0, nx, ny; float rx, ry; bool ok; };
+
+AD Foot footprint(const KParams &P, float px, float py, bool coalesce) {
+    Foot f;
+    const int W = (int) P.W, H = (int) P.H;
+    if (P.box) {
+        int ix = (int) floorf(px), iy = (int) floorf(py);
+        f.ok = (uint32_t) ix < (uint32_t) W && (uint32_t) iy < (uint32_t) H;
+        f.x0 = ix; f.y0 = iy; f.nx = f.ny = 1; f.rx = f.ry = 0.f;
+        return f;
+    }
+    const float radius = P.filt.radius;
+    if (!coalesce) {
+        float pfx = px + (0.f - 0.5f), pfy = py + (0.f - 0.5f);
+        int p0x = max((int) ceilf(pfx - radius), 0), p0y = max((int) ceilf(pfy - radius), 0);
+        int p1x = min((int) floorf(pfx + radius), W - 1), p1y = min((int) floorf(pfy + radius), H - 1);
+        f.ok = (uint32_t) p0x <= (uint32_t) p1x && (uint32_t) p0y <= (uint32_t) p1y;
+        f.x0 = p0x; f.y0 = p0y;
+        f.nx = p1x - p0x + 1; f.ny = p1y - p0y + 1;
+        const int count = (int) ceilf(2.f * radius);
+        f.nx = min(f.nx, count); f.ny = min(f.ny, count);
+        f.rx = (float) (uint32_t) p0x - pfx;
+        f.ry = (float) (uint32_t) p0y - pfy;
+        return f;
+    }
+    const int n = (int) ceilf(radius - .5f), count = 2 * n + 1;
+    int pix = (int) floorf(px) - n, piy = (int) floorf(py) - n;
+    f.rx = ((float) pix + .5f) - px;
+    f.ry = ((float) piy + .5f) - py;
+    /* clip to the film; the skipped leading cells shift the relative coordinate */
+    int sx = max(0, -pix), sy = max(0, -piy);
+    f.x0 = pix + sx; f.y0 = piy + sy;
+    f.nx = min(count, W - pix) - sx;
+    f.ny = min(count, H - piy) - sy;
+    f.rx = f.rx;  /* weights are evaluated at rel + (cell - pix) below */
+    f.ok = f.nx > 0 && f.ny > 0;
+    f.x0 = pix + sx;
+    f.y0 = piy + sy;
+    return f;
+}
+
+AD int wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+AD int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+AD void block_put(const KParams &P, float *film, SplatLds &L, float px, float py, const float *vals, bool valid,
+                  bool coalesce) {
+    const int C = (int) P.C;
+    Foot f;
+    f.ok = false;
+    f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
+    int base_x = 0, base_y = 0; /* film coordinate of weight index 0 */
+    if (valid) {
+        f = footprint(P, px, py, coalesce);
+        if (!P.box && coalesce) {
+            const int n = (int) ceilf(P.filt.radius - .5f);
+            base_x = (int) floorf(px) - n;
+            base_y = (int) floorf(py) - n;
+        } else {
+            base_x = f.x0;
+            base_y = f.y0;
+        }
+    }
+    bool act = valid && f.ok;
+    int lx = act ? f.x0 : 0x7fffffff, ly = act ? f.y0 : 0x7fffffff;
+    int hx = act ? f.x0 + f.nx : (int) 0x80000000, hy = act ? f.y0 + f.ny : (int) 0x80000000;
+    lx = wave_min(lx); ly = wave_min(ly); hx = wave_max(hx); hy = wave_max(hy);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { L.bb[wave][0] = lx; L.bb[wave][1] = ly; L.bb[wave][2] = hx; L.bb[wave][3] = hy; }
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    int bx0 = 0x7fffffff, by0 = 0x7fffffff, bx1 = (int) 0x80000000, by1 = (int) 0x80000000;
+    for (int w = 0; w < nw; ++w) {
+        bx0 = min(bx0, L.bb[w][0]); by0 = min(by0, L.bb[w][1]);
+        bx1 = max(bx1, L.bb[w][2]); by1 = max(by1, L.bb[w][3]);
+    }
+    const bool any = bx0 <= bx1 && bx0 != 0x7fffffff;
+    const int ww = any ? min(bx1 - bx0, kWinW) : 0, wh = any ? min(by1 - by0, kWinH) : 0;
+    for (int c = threadIdx.x; c < ww * wh * C; c += blockDim.x) L.win[c] = 0.f;
+    __syncthreads();
+    if (act) {
+        const bool in_win = f.x0 + f.nx <= bx0 + ww && f.y0 + f.ny <= by0 + wh;
+        const float *filt_c = P.filt.c;
+        (void) filt_c;
+        for (int ys = 0; ys < f.ny; ++ys) {
+            const int y = f.y0 + ys;
+            float wy = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) (y - base_y));
+            for (int xs = 0; xs < f.nx; ++xs) {
+                const int x = f.x0 + xs;
+                float wx = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) (x - base_x));
+                float w = wx * wy;
+                if (in_win) {
+                    float *cell = L.win + ((y - by0) * ww + (x - bx0)) * C;
+                    for (int k = 0; k < C; ++k) atomicAdd(cell + k, P.box ? vals[k] : vals[k] * w);
+                } else {
+                    float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
+                    for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < ww * wh; c += blockDim.x) {
+        const int cy = c / ww, cx = c - cy * ww;
+        const float *cell = L.win + c * C;
+        float *ptr = film + ((size_t) (by0 + cy) * P.W + (size_t) (bx0 + cx)) * C;
+        for (int k = 0; k < C; ++k) {
+            float v = cell[k];
+            if (v != 0.f || v != v) film_add(ptr + k, v);
+        }
+    }
+    __syncthreads();
+}
+
 AD void pack_vals(const KParams &P, C3 v, float alpha, float weight, float *vals) {
     vals[0] = v.r; vals[1] = v.g; vals[2] = v.b;
     if (P.C == 4) { vals[3] = weight; vals[4] = 0.f; }
@@ -473,26 +612,31 @@ __global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Buf
 /* ------------------------------------------------------------------ */
 
 __global__ void __launch_bounds__(256) k_splat_single(KParams P, Bufs B) {
+    __shared__ SplatLds L;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.chunk_n) return;
-    uint32_t lane = (uint32_t) (P.chunk_begin + i);
-    int px, py;
-    lane_pixel(P, lane, px, py);
-    Pcg rng = lane_rng(P.seed_value, lane);
-    float jx = rng.next_1d(), jy = rng.next_1d();
-    float sx = (float) px + jx, sy = (float) py + jy;
-    float4 lo = B.lane_out[i];
-    bool valid = lo.w != 0.f;
-    C3 spec = valid ? C3{lo.x, lo.y, lo.z} : c3(0.f);
-    float alpha = valid ? 1.f : 0.f;
-    float vals[5];
-    pack_vals(P, spec, alpha, 1.f, vals);
-    float putx = P.path_box_pos ? (float) px : sx, puty = P.path_box_pos ? (float) py : sy;
-    film_put(P, B.film, putx, puty, vals, P.coalesce_single != 0);
-    if (P.record) {
-        float *r = B.records + (size_t) i * 8;
-        r[0] = sx; r[1] = sy; r[2] = spec.r; r[3] = spec.g; r[4] = spec.b; r[5] = alpha; r[6] = 1.f; r[7] = 1.f;
+    const bool ok = i < P.chunk_n;
+    float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float putx = 0.f, puty = 0.f;
+    if (ok) {
+        uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        int px, py;
+        lane_pixel(P, lane, px, py);
+        Pcg rng = lane_rng(P.seed_value, lane);
+        float jx = rng.next_1d(), jy = rng.next_1d();
+        float sx = (float) px + jx, sy = (float) py + jy;
+        float4 lo = B.lane_out[i];
+        bool valid = lo.w != 0.f;
+        C3 spec = valid ? C3{lo.x, lo.y, lo.z} : c3(0.f);
+        float alpha = valid ? 1.f : 0.f;
+        pack_vals(P, spec, alpha, 1.f, vals);
+        putx = P.path_box_pos ? (float) px : sx;
+        puty = P.path_box_pos ? (float) py : sy;
+        if (P.record) {
+            float *r = B.records + (size_t) i * 8;
+            r[0] = sx; r[1] = sy; r[2] = spec.r; r[3] = spec.g; r[4] = spec.b; r[5] = alpha; r[6] = 1.f; r[7] = 1.f;
+        }
     }
+    block_put(P, B.film, L, putx, puty, vals, ok, P.coalesce_single != 0);
 }
 
 /* ------------------------------------------------------------------ */
@@ -825,10 +969,12 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
 
 template <int G>
 __global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
+    __shared__ SplatLds L;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.chunk_n) return;
+    const bool ok = i < P.chunk_n;
     const uint32_t n = P.chunk_n;
-    float4 lr = B.lane_rec[i], lo = B.lane_out[i];
+    float4 lr = make_float4(0.f, 0.f, 0.f, 0.f), lo = lr;
+    if (ok) { lr = B.lane_rec[i]; lo = B.lane_out[i]; }
     uint32_t lflags = fbits(lr.y);
     float pdfW = lr.x;
     bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
@@ -837,49 +983,47 @@ __global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
     C3 indirect = C3{lo.x, lo.y, lo.z};
     float alpha = valid_ray ? 1.f : 0.f;
     C3 res0 = c3(0.f);
-    if (!mis) {
+    if (ok && !mis) {
         float4 r0 = B.view_rec[(size_t) G * n + i];
         res0 = C3{r0.x, r0.y, r0.z} + indirect;
     }
     unsigned long long splats = 0;
-#pragma unroll
     for (int k = 0; k < G; ++k) {
         size_t o = (size_t) k * n + i;
-        float4 a = B.view_rec[o];
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) a = B.view_rec[o];
         uint32_t vf = fbits(a.w);
-        bool valid = (vf & VF_VALID) != 0;
+        bool valid = ok && (vf & VF_VALID) != 0;
         float weight = a.z;
-        C3 result;
-        if (mis) {
-            float4 r = B.view_rec[(size_t) G * n + o], bvv = B.view_rec[(size_t) 2 * G * n + o];
-            result = C3{r.x, r.y, r.z};
-            if (vf & VF_INDIRECT) result = cfma(C3{bvv.x, bvv.y, bvv.z} * pdfW, indirect, result);
-        } else {
-            result = res0;
+        C3 result = c3(0.f);
+        if (ok) {
+            if (mis) {
+                float4 r = B.view_rec[(size_t) G * n + o], bvv = B.view_rec[(size_t) 2 * G * n + o];
+                result = C3{r.x, r.y, r.z};
+                if (vf & VF_INDIRECT) result = cfma(C3{bvv.x, bvv.y, bvv.z} * pdfW, indirect, result);
+            } else {
+                result = res0;
+            }
         }
         if (k == 0 && P.n_adapt && adapt_mask) weight = weight * P.adapt_w;
         C3 v = {weight * result.r, weight * result.g, weight * result.b};
+        float vals[5];
         if (P.debug) {
-            if (k == 0) {
-                float vals[5];
-                pack_vals(P, c3(adapt_mask ? 1.f : 0.f), alpha, 1.f, vals);
-                film_put(P, B.film, a.x, a.y, vals, true);
-            }
+            if (k > 0) break; /* uniform: every thread breaks at k == 1 */
+            pack_vals(P, c3(adapt_mask ? 1.f : 0.f), alpha, 1.f, vals);
+            block_put(P, B.film, L, a.x, a.y, vals, ok, true);
             continue;
         }
-        if (valid) {
-            float vals[5];
-            pack_vals(P, v, alpha, weight, vals);
-            film_put(P, B.film, a.x, a.y, vals, k == 0);
-            ++splats;
-        }
-        if (P.record) {
+        pack_vals(P, v, alpha, weight, vals);
+        block_put(P, B.film, L, a.x, a.y, vals, valid, k == 0);
+        splats += valid ? 1 : 0;
+        if (ok && P.record) {
             float *rr = B.records + ((size_t) i * G + k) * 8;
             rr[0] = a.x; rr[1] = a.y; rr[2] = v.r; rr[3] = v.g; rr[4] = v.b; rr[5] = alpha; rr[6] = weight;
             rr[7] = valid ? 1.f : 0.f;
         }
     }
-    if (B.stats && splats) atomicAdd(&B.stats[3], splats);
+    if (B.stats) stat_add(&B.stats[3], splats);
 }
 
 /* develop: rgb / W (hdrfilm.cpp:400) */
