@@ -183,7 +183,8 @@ def main():
                                    "frac": round(pipeline_gbs / HBM_PEAK_GBS, 5)},
             },
             "cpu_baseline": cpu,
-            "counters": {k: c[k] for k in ("lanes", "vertices", "reuse_lanes", "visibility_rays", "view_splats")},
+            "counters": {k: c[k] for k in ("lanes", "vertices", "reuse_lanes", "visibility_rays", "view_splats",
+                                             "splat_fallback")},
         }
         print(json.dumps(out))
     if world > 1:

@@ -177,6 +177,7 @@ typedef struct amvpt_counters {
     double kernel_ms_bounce;
     double kernel_ms_splat;
     double total_ms;
+    uint64_t splat_fallback;   /* view samples splatted with direct global atomics (LDS window miss) */
 } amvpt_counters;
 
 typedef struct amvpt_scene amvpt_scene; /* opaque device-resident scene */

@@ -72,7 +72,7 @@ class Counters(ctypes.Structure):
     _fields_ = [("lanes", u64), ("passes", u64), ("vertices", u64), ("reuse_lanes", u64),
                 ("visibility_rays", u64), ("view_splats", u64), ("adaptive_lanes", u64),
                 ("kernel_ms_primary", f64), ("kernel_ms_bounce", f64), ("kernel_ms_splat", f64),
-                ("total_ms", f64)]
+                ("total_ms", f64), ("splat_fallback", u64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -282,14 +282,16 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
  * Footprints that do not fit the window fall back to direct global atomics.
  * The per-cell weights are exactly those of film_put (imageblock.cpp:174-559).
  */
-constexpr int kWinW = 64, kWinH = 16;
+constexpr int kWinW = 96, kWinH = 16, kMaxWaves = 16, kMaxFoot = 5;
 struct SplatLds {
-    float win[kWinW * kWinH * 5];
-    int bb[4][4];
+    float win[kWinW * kWinH * 5];   /* channel-planar: win[k * (ww*wh) + cell] */
+    int bb[kMaxWaves][4];
 };
 
 struct Foot { int x0, y0, nx, ny; float rx, ry; bool ok; };
 
+/* Footprint of ImageBlock::put: first covered pixel (x0, y0), extent (nx, ny) after
+ * clipping, and the filter argument rx/ry of pixel (x0, y0). */
 AD Foot footprint(const KParams &P, float px, float py, bool coalesce) {
     Foot f;
     const int W = (int) P.W, H = (int) P.H;
@@ -301,31 +303,29 @@ AD Foot footprint(const KParams &P, float px, float py, bool coalesce) {
     }
     const float radius = P.filt.radius;
     if (!coalesce) {
+        /* non-coalesced method (imageblock.cpp:265-427) */
         float pfx = px + (0.f - 0.5f), pfy = py + (0.f - 0.5f);
         int p0x = max((int) ceilf(pfx - radius), 0), p0y = max((int) ceilf(pfy - radius), 0);
         int p1x = min((int) floorf(pfx + radius), W - 1), p1y = min((int) floorf(pfy + radius), H - 1);
         f.ok = (uint32_t) p0x <= (uint32_t) p1x && (uint32_t) p0y <= (uint32_t) p1y;
-        f.x0 = p0x; f.y0 = p0y;
-        f.nx = p1x - p0x + 1; f.ny = p1y - p0y + 1;
         const int count = (int) ceilf(2.f * radius);
-        f.nx = min(f.nx, count); f.ny = min(f.ny, count);
+        f.x0 = p0x; f.y0 = p0y;
+        f.nx = min(p1x - p0x + 1, count); f.ny = min(p1y - p0y + 1, count);
         f.rx = (float) (uint32_t) p0x - pfx;
         f.ry = (float) (uint32_t) p0y - pfy;
         return f;
     }
+    /* coalesced method (imageblock.cpp:433-558): count = 2n+1 cells from floor(pos) - n */
     const int n = (int) ceilf(radius - .5f), count = 2 * n + 1;
     int pix = (int) floorf(px) - n, piy = (int) floorf(py) - n;
+    int sx = max(0, -pix), sy = max(0, -piy);
+    /* weights are evaluated at ((pix + .5) - pos) + xs, xs counted from pix */
     f.rx = ((float) pix + .5f) - px;
     f.ry = ((float) piy + .5f) - py;
-    /* clip to the film; the skipped leading cells shift the relative coordinate */
-    int sx = max(0, -pix), sy = max(0, -piy);
-    f.x0 = pix + sx; f.y0 = piy + sy;
-    f.nx = min(count, W - pix) - sx;
-    f.ny = min(count, H - piy) - sy;
-    f.rx = f.rx;  /* weights are evaluated at rel + (cell - pix) below */
-    f.ok = f.nx > 0 && f.ny > 0;
-    f.x0 = pix + sx;
-    f.y0 = piy + sy;
+    f.x0 = pix; f.y0 = piy;
+    f.nx = min(count, W - pix);
+    f.ny = min(count, H - piy);
+    f.ok = f.nx > sx && f.ny > sy;
     return f;
 }
 
@@ -340,26 +340,21 @@ AD int wave_max(int v) {
     return v;
 }
 
+/*
+ * Block-cooperative put.  Cells xs in [0, nx) x ys in [0, ny) of the footprint with
+ * x0 + xs >= 0 and y0 + ys >= 0 are accumulated (the coalesced footprint may start
+ * left/above the film).  Weight of a cell = eval(rx + xs) * eval(ry + ys).
+ */
 AD void block_put(const KParams &P, float *film, SplatLds &L, float px, float py, const float *vals, bool valid,
-                  bool coalesce) {
+                  bool coalesce, unsigned long long *fallback = nullptr) {
     const int C = (int) P.C;
     Foot f;
     f.ok = false;
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
-    int base_x = 0, base_y = 0; /* film coordinate of weight index 0 */
-    if (valid) {
-        f = footprint(P, px, py, coalesce);
-        if (!P.box && coalesce) {
-            const int n = (int) ceilf(P.filt.radius - .5f);
-            base_x = (int) floorf(px) - n;
-            base_y = (int) floorf(py) - n;
-        } else {
-            base_x = f.x0;
-            base_y = f.y0;
-        }
-    }
-    bool act = valid && f.ok;
-    int lx = act ? f.x0 : 0x7fffffff, ly = act ? f.y0 : 0x7fffffff;
+    if (valid) f = footprint(P, px, py, coalesce);
+    const bool act = valid && f.ok;
+    const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
+    int lx = act ? cx0 : 0x7fffffff, ly = act ? cy0 : 0x7fffffff;
     int hx = act ? f.x0 + f.nx : (int) 0x80000000, hy = act ? f.y0 + f.ny : (int) 0x80000000;
     lx = wave_min(lx); ly = wave_min(ly); hx = wave_max(hx); hy = wave_max(hy);
     const int wave = threadIdx.x >> 6;
@@ -371,24 +366,32 @@ AD void block_put(const KParams &P, float *film, SplatLds &L, float px, float py
         bx0 = min(bx0, L.bb[w][0]); by0 = min(by0, L.bb[w][1]);
         bx1 = max(bx1, L.bb[w][2]); by1 = max(by1, L.bb[w][3]);
     }
-    const bool any = bx0 <= bx1 && bx0 != 0x7fffffff;
+    const bool any = bx0 != 0x7fffffff && bx0 < bx1;
     const int ww = any ? min(bx1 - bx0, kWinW) : 0, wh = any ? min(by1 - by0, kWinH) : 0;
-    for (int c = threadIdx.x; c < ww * wh * C; c += blockDim.x) L.win[c] = 0.f;
+    const int plane = ww * wh;
+    for (int c = threadIdx.x; c < plane * C; c += blockDim.x) L.win[c] = 0.f;
     __syncthreads();
     if (act) {
-        const bool in_win = f.x0 + f.nx <= bx0 + ww && f.y0 + f.ny <= by0 + wh;
-        const float *filt_c = P.filt.c;
-        (void) filt_c;
-        for (int ys = 0; ys < f.ny; ++ys) {
+        const bool in_win = cx0 >= bx0 && cy0 >= by0 && f.x0 + f.nx <= bx0 + ww && f.y0 + f.ny <= by0 + wh;
+        if (!in_win && fallback) ++*fallback;
+        float wx[kMaxFoot], wy[kMaxFoot];
+#pragma unroll
+        for (int t = 0; t < kMaxFoot; ++t) {
+            wx[t] = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
+            wy[t] = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
+        }
+#pragma unroll
+        for (int ys = 0; ys < kMaxFoot; ++ys) {
             const int y = f.y0 + ys;
-            float wy = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) (y - base_y));
-            for (int xs = 0; xs < f.nx; ++xs) {
+            if (ys >= f.ny || y < 0) continue;
+#pragma unroll
+            for (int xs = 0; xs < kMaxFoot; ++xs) {
                 const int x = f.x0 + xs;
-                float wx = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) (x - base_x));
-                float w = wx * wy;
+                if (xs >= f.nx || x < 0) continue;
+                const float w = wx[xs] * wy[ys];
                 if (in_win) {
-                    float *cell = L.win + ((y - by0) * ww + (x - bx0)) * C;
-                    for (int k = 0; k < C; ++k) atomicAdd(cell + k, P.box ? vals[k] : vals[k] * w);
+                    float *cell = L.win + ((y - by0) * ww + (x - bx0));
+                    for (int k = 0; k < C; ++k) atomicAdd(cell + k * plane, P.box ? vals[k] : vals[k] * w);
                 } else {
                     float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
                     for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
@@ -397,16 +400,31 @@ AD void block_put(const KParams &P, float *film, SplatLds &L, float px, float py
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < ww * wh; c += blockDim.x) {
-        const int cy = c / ww, cx = c - cy * ww;
-        const float *cell = L.win + c * C;
-        float *ptr = film + ((size_t) (by0 + cy) * P.W + (size_t) (bx0 + cx)) * C;
-        for (int k = 0; k < C; ++k) {
-            float v = cell[k];
-            if (v != 0.f || v != v) film_add(ptr + k, v);
-        }
+    /* flush: consecutive threads take consecutive floats of the film row segment */
+    for (int e = threadIdx.x; e < plane * C; e += blockDim.x) {
+        const int cell = e / C, k = e - cell * C;
+        const int cy = cell / ww, cx = cell - cy * ww;
+        const float v = L.win[k * plane + cell];
+        if (v != 0.f || v != v) film_add(film + ((size_t) (by0 + cy) * P.W + (size_t) (bx0 + cx)) * C + k, v);
     }
     __syncthreads();
+}
+
+/* Splat-kernel lane order: thread t of a 1024-thread block takes the block-local lane
+ * (t % pixels_per_block) * spp + t / pixels_per_block, so a wave holds 64 different
+ * pixels and the LDS atomics of one instruction hit 64 different cells. */
+constexpr int kSplatBlock = 1024;
+AD uint32_t splat_lane(const KParams &P, uint32_t &valid_n) {
+    const uint32_t base = blockIdx.x * kSplatBlock;
+    const uint32_t t = threadIdx.x;
+    const uint32_t remain = P.chunk_n > base ? P.chunk_n - base : 0;
+    valid_n = remain < (uint32_t) kSplatBlock ? remain : (uint32_t) kSplatBlock;
+    const uint32_t S = P.spp_pp;
+    if (valid_n == (uint32_t) kSplatBlock && P.pow2 && S > 1 && S <= (uint32_t) kSplatBlock) {
+        const uint32_t ppb = (uint32_t) kSplatBlock >> P.log_spp;
+        return base + (t % ppb) * S + t / ppb;
+    }
+    return base + t;
 }
 
 AD void pack_vals(const KParams &P, C3 v, float alpha, float weight, float *vals) {
@@ -611,10 +629,11 @@ __global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Buf
 /* k_splat_single: ImageBlock::put of render_sample                    */
 /* ------------------------------------------------------------------ */
 
-__global__ void __launch_bounds__(256) k_splat_single(KParams P, Bufs B) {
+__global__ void __launch_bounds__(1024) k_splat_single(KParams P, Bufs B) {
     __shared__ SplatLds L;
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool ok = i < P.chunk_n;
+    uint32_t vn;
+    const uint32_t i = splat_lane(P, vn);
+    const bool ok = threadIdx.x < vn;
     float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     float putx = 0.f, puty = 0.f;
     if (ok) {
@@ -968,10 +987,11 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
 /* ------------------------------------------------------------------ */
 
 template <int G>
-__global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
+__global__ void __launch_bounds__(1024) k_splat_multi(KParams P, Bufs B) {
     __shared__ SplatLds L;
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool ok = i < P.chunk_n;
+    uint32_t vn;
+    const uint32_t i = splat_lane(P, vn);
+    const bool ok = threadIdx.x < vn;
     const uint32_t n = P.chunk_n;
     float4 lr = make_float4(0.f, 0.f, 0.f, 0.f), lo = lr;
     if (ok) { lr = B.lane_rec[i]; lo = B.lane_out[i]; }
@@ -987,7 +1007,7 @@ __global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
         float4 r0 = B.view_rec[(size_t) G * n + i];
         res0 = C3{r0.x, r0.y, r0.z} + indirect;
     }
-    unsigned long long splats = 0;
+    unsigned long long splats = 0, fallback = 0;
     for (int k = 0; k < G; ++k) {
         size_t o = (size_t) k * n + i;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1015,7 +1035,7 @@ __global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
             continue;
         }
         pack_vals(P, v, alpha, weight, vals);
-        block_put(P, B.film, L, a.x, a.y, vals, valid, k == 0);
+        block_put(P, B.film, L, a.x, a.y, vals, valid, k == 0, &fallback);
         splats += valid ? 1 : 0;
         if (ok && P.record) {
             float *rr = B.records + ((size_t) i * G + k) * 8;
@@ -1023,7 +1043,7 @@ __global__ void __launch_bounds__(256) k_splat_multi(KParams P, Bufs B) {
             rr[7] = valid ? 1.f : 0.f;
         }
     }
-    if (B.stats) stat_add(&B.stats[3], splats);
+    if (B.stats) { stat_add(&B.stats[3], splats); stat_add(&B.stats[4], fallback); }
 }
 
 /* develop: rgb / W (hdrfilm.cpp:400) */
@@ -1119,7 +1139,7 @@ static void launch_primary(dim3 grid, size_t lds, hipStream_t st, const KParams 
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G>), grid, dim3(256), 0, st, P, B);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G>), grid, dim3(kSplatBlock), 0, st, P, B);
 }
 
 typedef void (*primary_fn)(dim3, size_t, hipStream_t, const KParams &, const DScene *, const DView *, const Bufs &);
@@ -1288,8 +1308,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 }
             }
             HIPCHK(hipEventRecord(ev[2], st));
-            if (G == 1) hipLaunchKernelGGL(k_splat_single, grid, dim3(256), 0, st, P, B);
-            else kSplat[G](grid, st, P, B);
+            const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
+            if (G == 1) hipLaunchKernelGGL(k_splat_single, sgrid, dim3(kSplatBlock), 0, st, P, B);
+            else kSplat[G](sgrid, st, P, B);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[3], st));
             if (counters) {
@@ -1314,6 +1335,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.reuse_lanes = hs[1];
         c.visibility_rays = hs[2];
         c.view_splats = hs[3];
+        c.splat_fallback = hs[4];
         c.kernel_ms_primary = ms_primary;
         c.kernel_ms_bounce = ms_bounce;
         c.kernel_ms_splat = ms_splat;
