@@ -274,19 +274,37 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
 /* Block-cooperative ImageBlock::put                                   */
 /* ------------------------------------------------------------------ */
 /*
- * Every thread of a 256-thread block calls block_put() with its own sample
- * (`valid` may be false).  The block's footprints are accumulated in an LDS
- * window with LDS float atomics and the window is flushed once with global
- * float atomics (skipping cells that received nothing), so the film sees about
- * one atomic per touched pixel-channel per block instead of one per sample.
- * Footprints that do not fit the window fall back to direct global atomics.
- * The per-cell weights are exactly those of film_put (imageblock.cpp:174-559).
+ * Every thread of a splat block calls block_put() with its own sample (`valid`
+ * may be false).  The block's footprints are accumulated in an LDS window and
+ * the window is flushed once with global float atomics (skipping cells that
+ * received nothing), so the film sees about one atomic per touched
+ * pixel-channel per block instead of one per sample.  Footprints that do not
+ * fit the window fall back to direct global atomics.  The per-cell weights are
+ * exactly those of film_put (imageblock.cpp:174-559).
+ *
+ * LDS float adds: gfx950's ds_add_f32 retires ~0.33 lanes/clk/CU
+ * (tools/ubench_lds.hip) -- 40x slower than ds_add_u32 -- so the window holds
+ * channel PAIRS (R,G), (B,W|A), (W,-) as 64-bit words updated with
+ * ds_cmpst_rtn_b64 (compare-and-swap on the bit pattern): one read and one CAS
+ * per pair, retried only when another lane changed the word in between.
+ * Bit-pattern comparison keeps NaN contributions terminating and propagating.
+ *
+ * The window is double-buffered (view k uses buffer k & 1) and the flush
+ * writes zeros back, so one put costs two block barriers and no zeroing pass.
  */
 constexpr int kWinW = 96, kWinH = 16, kMaxWaves = 16, kMaxFoot = 5;
-struct SplatLds {
-    float win[kWinW * kWinH * 5];   /* channel-planar: win[k * (ww*wh) + cell] */
-    int bb[kMaxWaves][4];
+constexpr int kWinCells = kWinW * kWinH;
+template <int C> struct SplatLds {
+    static constexpr int NP = (C + 1) / 2;  /* channel pairs per cell */
+    uint64_t win[2][kWinCells * NP];        /* pair p of cell c at win[b][p * plane + c] */
+    int bb[2][kMaxWaves][4];
 };
+
+template <int C> AD void splat_lds_init(SplatLds<C> &L) {
+    uint64_t *w = &L.win[0][0];
+    for (int c = threadIdx.x; c < 2 * kWinCells * SplatLds<C>::NP; c += blockDim.x) w[c] = 0ull;
+    __syncthreads();
+}
 
 struct Foot { int x0, y0, nx, ny; float rx, ry; bool ok; };
 
@@ -340,14 +358,26 @@ AD int wave_max(int v) {
     return v;
 }
 
+AD uint64_t pair_add(uint64_t w, float a, float b) {
+    const float lo = __uint_as_float((uint32_t) w) + a, hi = __uint_as_float((uint32_t) (w >> 32)) + b;
+    return (uint64_t) __float_as_uint(lo) | ((uint64_t) __float_as_uint(hi) << 32);
+}
+AD bool lds_cas64(uint64_t *p, uint64_t &expect, uint64_t nw) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+AD uint64_t lds_load64(uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
 /*
- * Block-cooperative put.  Cells xs in [0, nx) x ys in [0, ny) of the footprint with
- * x0 + xs >= 0 and y0 + ys >= 0 are accumulated (the coalesced footprint may start
- * left/above the film).  Weight of a cell = eval(rx + xs) * eval(ry + ys).
+ * Block-cooperative put into window buffer `buf`.  Cells xs in [0, nx) x ys in
+ * [0, ny) of the footprint with x0 + xs >= 0 and y0 + ys >= 0 are accumulated (the
+ * coalesced footprint may start left/above the film).  Weight of a cell =
+ * eval(rx + xs) * eval(ry + ys).  `coalesce` is uniform over the block.
  */
-AD void block_put(const KParams &P, float *film, SplatLds &L, float px, float py, const float *vals, bool valid,
-                  bool coalesce, unsigned long long *fallback = nullptr) {
-    const int C = (int) P.C;
+template <int C>
+AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float px, float py, const float *vals,
+                  bool valid, bool coalesce, unsigned long long *fallback = nullptr) {
+    constexpr int NP = SplatLds<C>::NP;
     Foot f;
     f.ok = false;
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
@@ -358,56 +388,101 @@ AD void block_put(const KParams &P, float *film, SplatLds &L, float px, float py
     int hx = act ? f.x0 + f.nx : (int) 0x80000000, hy = act ? f.y0 + f.ny : (int) 0x80000000;
     lx = wave_min(lx); ly = wave_min(ly); hx = wave_max(hx); hy = wave_max(hy);
     const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { L.bb[wave][0] = lx; L.bb[wave][1] = ly; L.bb[wave][2] = hx; L.bb[wave][3] = hy; }
+    if ((threadIdx.x & 63) == 0) {
+        L.bb[buf][wave][0] = lx; L.bb[buf][wave][1] = ly; L.bb[buf][wave][2] = hx; L.bb[buf][wave][3] = hy;
+    }
     __syncthreads();
     const int nw = blockDim.x >> 6;
     int bx0 = 0x7fffffff, by0 = 0x7fffffff, bx1 = (int) 0x80000000, by1 = (int) 0x80000000;
     for (int w = 0; w < nw; ++w) {
-        bx0 = min(bx0, L.bb[w][0]); by0 = min(by0, L.bb[w][1]);
-        bx1 = max(bx1, L.bb[w][2]); by1 = max(by1, L.bb[w][3]);
+        bx0 = min(bx0, L.bb[buf][w][0]); by0 = min(by0, L.bb[buf][w][1]);
+        bx1 = max(bx1, L.bb[buf][w][2]); by1 = max(by1, L.bb[buf][w][3]);
     }
     const bool any = bx0 != 0x7fffffff && bx0 < bx1;
     const int ww = any ? min(bx1 - bx0, kWinW) : 0, wh = any ? min(by1 - by0, kWinH) : 0;
     const int plane = ww * wh;
-    for (int c = threadIdx.x; c < plane * C; c += blockDim.x) L.win[c] = 0.f;
-    __syncthreads();
+    uint64_t *win = L.win[buf];
     if (act) {
         const bool in_win = cx0 >= bx0 && cy0 >= by0 && f.x0 + f.nx <= bx0 + ww && f.y0 + f.ny <= by0 + wh;
-        if (!in_win && fallback) ++*fallback;
         float wx[kMaxFoot], wy[kMaxFoot];
 #pragma unroll
         for (int t = 0; t < kMaxFoot; ++t) {
             wx[t] = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
             wy[t] = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
         }
+        if (in_win) {
+            uint64_t *row = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
 #pragma unroll
-        for (int ys = 0; ys < kMaxFoot; ++ys) {
-            const int y = f.y0 + ys;
-            if (ys >= f.ny || y < 0) continue;
+            for (int ys = 0; ys < kMaxFoot; ++ys, row += ww) {
+                if (ys >= f.ny || f.y0 + ys < 0) continue;
+                /* one row: all reads, then all CAS; failures retry below */
+                uint64_t o[kMaxFoot][NP];
+                uint32_t m = 0;
 #pragma unroll
-            for (int xs = 0; xs < kMaxFoot; ++xs) {
-                const int x = f.x0 + xs;
-                if (xs >= f.nx || x < 0) continue;
-                const float w = wx[xs] * wy[ys];
-                if (in_win) {
-                    float *cell = L.win + ((y - by0) * ww + (x - bx0));
-                    for (int k = 0; k < C; ++k) atomicAdd(cell + k * plane, P.box ? vals[k] : vals[k] * w);
-                } else {
+                for (int xs = 0; xs < kMaxFoot; ++xs)
+                    if (xs < f.nx && f.x0 + xs >= 0) m |= 1u << xs;
+#pragma unroll
+                for (int xs = 0; xs < kMaxFoot; ++xs)
+                    if (m >> xs & 1u) {
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) o[xs][q] = lds_load64(row + xs + q * plane);
+                    }
+                uint32_t fail = 0;
+#pragma unroll
+                for (int xs = 0; xs < kMaxFoot; ++xs)
+                    if (m >> xs & 1u) {
+                        const float w = wx[xs] * wy[ys];
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
+                            const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
+                            if (!lds_cas64(row + xs + q * plane, o[xs][q], pair_add(o[xs][q], a0, a1)))
+                                fail |= 1u << (xs * NP + q);
+                        }
+                    }
+                while (fail) {
+                    const int bit = __builtin_ctz(fail);
+                    const int xs = bit / NP, q = bit - xs * NP;
+                    const float w = wx[xs] * wy[ys];
+                    const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
+                    const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
+                    uint64_t *cp = row + xs + q * plane;
+                    uint64_t e = lds_load64(cp);
+                    while (!lds_cas64(cp, e, pair_add(e, a0, a1))) {}
+                    fail &= fail - 1u;
+                }
+            }
+        } else {
+            if (fallback) ++*fallback;
+#pragma unroll
+            for (int ys = 0; ys < kMaxFoot; ++ys) {
+                const int y = f.y0 + ys;
+                if (ys >= f.ny || y < 0) continue;
+#pragma unroll
+                for (int xs = 0; xs < kMaxFoot; ++xs) {
+                    const int x = f.x0 + xs;
+                    if (xs >= f.nx || x < 0) continue;
+                    const float w = wx[xs] * wy[ys];
                     float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
+#pragma unroll
                     for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
                 }
             }
         }
     }
     __syncthreads();
-    /* flush: consecutive threads take consecutive floats of the film row segment */
+    /* flush + re-zero: consecutive threads take consecutive floats of the film row segment */
+    float *wf = reinterpret_cast<float *>(win);
     for (int e = threadIdx.x; e < plane * C; e += blockDim.x) {
         const int cell = e / C, k = e - cell * C;
         const int cy = cell / ww, cx = cell - cy * ww;
-        const float v = L.win[k * plane + cell];
-        if (v != 0.f || v != v) film_add(film + ((size_t) (by0 + cy) * P.W + (size_t) (bx0 + cx)) * C + k, v);
+        float *src = wf + 2 * ((k >> 1) * plane + cell) + (k & 1);
+        const float v = *src;
+        if (__float_as_uint(v) != 0u) {
+            *src = 0.f;
+            if (v != 0.f || v != v) film_add(film + ((size_t) (by0 + cy) * P.W + (size_t) (bx0 + cx)) * C + k, v);
+        }
     }
-    __syncthreads();
 }
 
 /* Splat-kernel lane order: thread t of a 1024-thread block takes the block-local lane
@@ -629,8 +704,10 @@ __global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Buf
 /* k_splat_single: ImageBlock::put of render_sample                    */
 /* ------------------------------------------------------------------ */
 
+template <int C>
 __global__ void __launch_bounds__(1024) k_splat_single(KParams P, Bufs B) {
-    __shared__ SplatLds L;
+    __shared__ SplatLds<C> L;
+    splat_lds_init(L);
     uint32_t vn;
     const uint32_t i = splat_lane(P, vn);
     const bool ok = threadIdx.x < vn;
@@ -655,7 +732,7 @@ __global__ void __launch_bounds__(1024) k_splat_single(KParams P, Bufs B) {
             r[0] = sx; r[1] = sy; r[2] = spec.r; r[3] = spec.g; r[4] = spec.b; r[5] = alpha; r[6] = 1.f; r[7] = 1.f;
         }
     }
-    block_put(P, B.film, L, putx, puty, vals, ok, P.coalesce_single != 0);
+    block_put<C>(P, B.film, L, 0, putx, puty, vals, ok, P.coalesce_single != 0);
 }
 
 /* ------------------------------------------------------------------ */
@@ -986,9 +1063,10 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
 /* k_splat_multi<G>: indirect accumulation + splats (mvpath_multi.h:343-368,44-76) */
 /* ------------------------------------------------------------------ */
 
-template <int G>
+template <int G, int C>
 __global__ void __launch_bounds__(1024) k_splat_multi(KParams P, Bufs B) {
-    __shared__ SplatLds L;
+    __shared__ SplatLds<C> L;
+    splat_lds_init(L);
     uint32_t vn;
     const uint32_t i = splat_lane(P, vn);
     const bool ok = threadIdx.x < vn;
@@ -1031,11 +1109,11 @@ __global__ void __launch_bounds__(1024) k_splat_multi(KParams P, Bufs B) {
         if (P.debug) {
             if (k > 0) break; /* uniform: every thread breaks at k == 1 */
             pack_vals(P, c3(adapt_mask ? 1.f : 0.f), alpha, 1.f, vals);
-            block_put(P, B.film, L, a.x, a.y, vals, ok, true);
+            block_put<C>(P, B.film, L, 0, a.x, a.y, vals, ok, true);
             continue;
         }
         pack_vals(P, v, alpha, weight, vals);
-        block_put(P, B.film, L, a.x, a.y, vals, valid, k == 0, &fallback);
+        block_put<C>(P, B.film, L, k & 1, a.x, a.y, vals, valid, k == 0, &fallback);
         splats += valid ? 1 : 0;
         if (ok && P.record) {
             float *rr = B.records + ((size_t) i * G + k) * 8;
@@ -1139,7 +1217,8 @@ static void launch_primary(dim3 grid, size_t lds, hipStream_t st, const KParams 
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G>), grid, dim3(kSplatBlock), 0, st, P, B);
+    if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5>), grid, dim3(kSplatBlock), 0, st, P, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4>), grid, dim3(kSplatBlock), 0, st, P, B);
 }
 
 typedef void (*primary_fn)(dim3, size_t, hipStream_t, const KParams &, const DScene *, const DView *, const Bufs &);
@@ -1309,7 +1388,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             }
             HIPCHK(hipEventRecord(ev[2], st));
             const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
-            if (G == 1) hipLaunchKernelGGL(k_splat_single, sgrid, dim3(kSplatBlock), 0, st, P, B);
+            if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
+            else if (G == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else kSplat[G](sgrid, st, P, B);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[3], st));
