@@ -297,7 +297,7 @@ constexpr int kWinCells = kWinW * kWinH;
 template <int C> struct SplatLds {
     static constexpr int NP = (C + 1) / 2;  /* channel pairs per cell */
     uint64_t win[2][kWinCells * NP];        /* pair p of cell c at win[b][p * plane + c] */
-    int bb[2][kMaxWaves][4];
+    alignas(16) int bb[2][kMaxWaves][4];
 };
 
 template <int C> AD void splat_lds_init(SplatLds<C> &L) {
@@ -392,11 +392,19 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
         L.bb[buf][wave][0] = lx; L.bb[buf][wave][1] = ly; L.bb[buf][wave][2] = hx; L.bb[buf][wave][3] = hy;
     }
     __syncthreads();
-    const int nw = blockDim.x >> 6;
     int bx0 = 0x7fffffff, by0 = 0x7fffffff, bx1 = (int) 0x80000000, by1 = (int) 0x80000000;
-    for (int w = 0; w < nw; ++w) {
-        bx0 = min(bx0, L.bb[buf][w][0]); by0 = min(by0, L.bb[buf][w][1]);
-        bx1 = max(bx1, L.bb[buf][w][2]); by1 = max(by1, L.bb[buf][w][3]);
+    {
+        const int l = threadIdx.x & 63;
+        if (l < (int) (blockDim.x >> 6)) {
+            const int4 q = *reinterpret_cast<const int4 *>(&L.bb[buf][l][0]);
+            bx0 = q.x; by0 = q.y; bx1 = q.z; by1 = q.w;
+        }
+#pragma unroll
+        for (int o = kMaxWaves / 2; o > 0; o >>= 1) {
+            bx0 = min(bx0, __shfl_xor(bx0, o)); by0 = min(by0, __shfl_xor(by0, o));
+            bx1 = max(bx1, __shfl_xor(bx1, o)); by1 = max(by1, __shfl_xor(by1, o));
+        }
+        bx0 = __shfl(bx0, 0); by0 = __shfl(by0, 0); bx1 = __shfl(bx1, 0); by1 = __shfl(by1, 0);
     }
     const bool any = bx0 != 0x7fffffff && bx0 < bx1;
     const int ww = any ? min(bx1 - bx0, kWinW) : 0, wh = any ? min(by1 - by0, kWinH) : 0;
@@ -473,33 +481,46 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     __syncthreads();
     /* flush + re-zero: consecutive threads take consecutive floats of the film row segment */
     float *wf = reinterpret_cast<float *>(win);
+    const int rowlen = ww * C;
+    const float inv_rowlen = 1.f / (float) max(rowlen, 1);
+    float *film0 = film + ((size_t) by0 * P.W + (size_t) bx0) * C;
     for (int e = threadIdx.x; e < plane * C; e += blockDim.x) {
-        const int cell = e / C, k = e - cell * C;
-        const int cy = cell / ww, cx = cell - cy * ww;
+        int cy = (int) ((float) e * inv_rowlen);            /* e < 2^24: off by at most one */
+        cy -= (cy * rowlen > e) ? 1 : 0;
+        cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
+        const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
+        const int cell = cy * ww + cx;
         float *src = wf + 2 * ((k >> 1) * plane + cell) + (k & 1);
         const float v = *src;
         if (__float_as_uint(v) != 0u) {
             *src = 0.f;
-            if (v != 0.f || v != v) film_add(film + ((size_t) (by0 + cy) * P.W + (size_t) (bx0 + cx)) * C + k, v);
+            if (v != 0.f || v != v) film_add(film0 + (size_t) cy * P.W * C + r, v);
         }
     }
 }
 
-/* Splat-kernel lane order: thread t of a 1024-thread block takes the block-local lane
- * (t % pixels_per_block) * spp + t / pixels_per_block, so a wave holds 64 different
- * pixels and the LDS atomics of one instruction hit 64 different cells. */
-constexpr int kSplatBlock = 1024;
+/* Splat-kernel lane order.  Lanes are taken in super-blocks of kSplatSuper = 1024
+ * (= pixels_per_super * spp); each super-block is split over kSplatSplit blocks of
+ * kSplatBlock threads that take disjoint sample subsets of the same pixels:
+ * thread t of part h takes lane (t % ppb) * spp + h * (spp / split) + t / ppb, so a
+ * wave holds 64 different pixels (no CAS conflicts inside a wave) and the blocks of
+ * a super-block write the same small film window. */
+constexpr int kSplatBlock = 512, kSplatSuper = 1024, kSplatSplit = kSplatSuper / kSplatBlock;
 AD uint32_t splat_lane(const KParams &P, uint32_t &valid_n) {
-    const uint32_t base = blockIdx.x * kSplatBlock;
+    const uint32_t super = blockIdx.x / kSplatSplit, h = blockIdx.x % kSplatSplit;
+    const uint32_t base = super * kSplatSuper;
     const uint32_t t = threadIdx.x;
     const uint32_t remain = P.chunk_n > base ? P.chunk_n - base : 0;
-    valid_n = remain < (uint32_t) kSplatBlock ? remain : (uint32_t) kSplatBlock;
     const uint32_t S = P.spp_pp;
-    if (valid_n == (uint32_t) kSplatBlock && P.pow2 && S > 1 && S <= (uint32_t) kSplatBlock) {
-        const uint32_t ppb = (uint32_t) kSplatBlock >> P.log_spp;
-        return base + (t % ppb) * S + t / ppb;
+    if (remain >= (uint32_t) kSplatSuper && P.pow2 && S >= (uint32_t) kSplatSplit && S <= (uint32_t) kSplatBlock) {
+        valid_n = kSplatBlock;
+        const uint32_t ppb = (uint32_t) kSplatSuper >> P.log_spp;
+        return base + (t % ppb) * S + h * (S / kSplatSplit) + t / ppb;
     }
-    return base + t;
+    const uint32_t off = h * kSplatBlock;
+    const uint32_t r = remain > off ? remain - off : 0;
+    valid_n = r < (uint32_t) kSplatBlock ? r : (uint32_t) kSplatBlock;
+    return base + off + t;
 }
 
 AD void pack_vals(const KParams &P, C3 v, float alpha, float weight, float *vals) {
@@ -705,7 +726,7 @@ __global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Buf
 /* ------------------------------------------------------------------ */
 
 template <int C>
-__global__ void __launch_bounds__(1024) k_splat_single(KParams P, Bufs B) {
+__global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B) {
     __shared__ SplatLds<C> L;
     splat_lds_init(L);
     uint32_t vn;
@@ -1064,7 +1085,7 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
 /* ------------------------------------------------------------------ */
 
 template <int G, int C>
-__global__ void __launch_bounds__(1024) k_splat_multi(KParams P, Bufs B) {
+__global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) {
     __shared__ SplatLds<C> L;
     splat_lds_init(L);
     uint32_t vn;
@@ -1387,7 +1408,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 }
             }
             HIPCHK(hipEventRecord(ev[2], st));
-            const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
+            const dim3 sgrid((uint32_t) ((cn + kSplatSuper - 1) / kSplatSuper) * kSplatSplit);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else if (G == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else kSplat[G](sgrid, st, P, B);
