@@ -60,9 +60,12 @@ struct Box {
 
 struct BuildPrim { Box box; float c[3]; uint32_t idx; };
 
+/* Binary SAH tree as built (children of inner node i at left, left + 1). */
+struct BNode { Box box; uint32_t left_or_first, count; };
+
 struct Builder {
     std::vector<BuildPrim> &prims;
-    std::vector<DNode> nodes;
+    std::vector<BNode> nodes;
     explicit Builder(std::vector<BuildPrim> &p) : prims(p) {}
 
     static void pad(Box &b) {
@@ -74,14 +77,15 @@ struct Builder {
     void set(uint32_t ni, const Box &b) {
         Box pb = b;
         pad(pb);
-        for (int i = 0; i < 3; ++i) { nodes[ni].lo[i] = pb.lo[i]; nodes[ni].hi[i] = pb.hi[i]; }
+        nodes[ni].box = pb;
     }
+    /* every split leaves both halves non-empty, so the recursion ends with leaves of <= 4 prims */
     void build(uint32_t ni, uint32_t begin, uint32_t end, int depth) {
         Box b, cb;
         for (uint32_t i = begin; i < end; ++i) { b.grow(prims[i].box); cb.grow(prims[i].c); }
         set(ni, b);
         uint32_t n = end - begin;
-        if (n <= 2 || depth >= 40) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
+        if (n <= 2) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
         const int NB = 16;
         float best_cost = INFINITY;
         int best_axis = -1, best_split = -1;
@@ -137,6 +141,20 @@ struct Builder {
         nodes[ni].left_or_first = l; nodes[ni].count = 0;
         build(l, begin, mid, depth + 1);
         build(l + 1, mid, end, depth + 1);
+    }
+    /* depth-first pre-order with skip links (DNode) */
+    void flatten(uint32_t ni, std::vector<DNode> &out) const {
+        const BNode &bn = nodes[ni];
+        const uint32_t at = (uint32_t) out.size();
+        DNode d{};
+        for (int i = 0; i < 3; ++i) { d.lo[i] = bn.box.lo[i]; d.hi[i] = bn.box.hi[i]; }
+        d.first = bn.count ? bn.left_or_first : 0u;
+        out.push_back(d);
+        if (!bn.count) {
+            flatten(bn.left_or_first, out);
+            flatten(bn.left_or_first + 1, out);
+        }
+        out[at].skip_count = ((uint32_t) out.size() & kNodeSkipMask) | (bn.count << kNodeCountShift);
     }
 };
 
@@ -339,25 +357,23 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     std::vector<DNode> nodes;
     std::vector<DPrim> prims;
     if (bprims.empty()) {
+        /* one inner node with an empty box: every ray misses it and skips to the end */
         DNode root{};
         root.lo[0] = root.lo[1] = root.lo[2] = 1.f;
         root.hi[0] = root.hi[1] = root.hi[2] = -1.f;
-        root.left_or_first = 0;
-        root.count = 0;
-        /* an empty inner node whose children are never reached: make it an empty leaf */
+        root.first = 0;
+        root.skip_count = 1u;
         nodes.push_back(root);
-        nodes[0].count = 0;
-        DNode c{};
-        c.lo[0] = c.lo[1] = c.lo[2] = 1.f; c.hi[0] = c.hi[1] = c.hi[2] = -1.f;
-        nodes[0].left_or_first = 1;
-        nodes.push_back(c); nodes.push_back(c);
-        nodes[1].count = 0; nodes[2].count = 0;
-        nodes[1].left_or_first = 1; nodes[2].left_or_first = 1; /* never visited: empty boxes */
     } else {
         Builder b(bprims);
         b.nodes.resize(1);
         b.build(0, 0, (uint32_t) bprims.size(), 0);
-        nodes = std::move(b.nodes);
+        nodes.reserve(b.nodes.size());
+        b.flatten(0, nodes);
+        if (nodes.size() > kNodeSkipMask) {
+            set_error("BVH too large (more than 2^28 nodes)");
+            return AMVPT_ERR_INVALID;
+        }
         prims.resize(bprims.size());
         for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
     }

@@ -77,6 +77,7 @@ constexpr uint32_t kLdsSceneBytes = 48 * 1024;
 AD SceneRef stage_scene(const DScene &S, char *lds) {
     SceneRef sc;
     sc.g = &S;
+    sc.n_nodes = S.n_nodes;
     if (S.lds_bytes <= kLdsSceneBytes) {
         const uint32_t nn = S.n_nodes * (uint32_t) sizeof(DNode) / 16, np = S.n_prims * (uint32_t) sizeof(DPrim) / 16;
         float4 *dst = (float4 *) lds;
@@ -795,6 +796,14 @@ AD float tv_pdf_fast(f3 wo_l, f3 wi_k, float p_k, const BD &bd, bool active) {
 }
 AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 
+/*
+ * Per-view state lives in small SoA register arrays indexed by the (wave-uniform)
+ * view counter of non-unrolled loops, so each per-view body (a visibility ray,
+ * three BSDF evaluations, ...) is emitted once: the fully unrolled form did not
+ * fit the register file and spilled the whole SampleData array to scratch.
+ * View records are written as soon as each part is final:
+ *   rec0[k] = (splat x, splat y, weight, flags), rec1[k] = result, rec2[k] = bsdf_val.
+ */
 template <int G>
 __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -818,17 +827,37 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
         float sx = (float) px + jx, sy = (float) py + jy;
         uint32_t p_idx;
         Ray pray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), p_idx);
-        SD sd[G];
-        uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u);
+        const uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u);
+        float4 *const rec0 = B.view_rec, *const rec1 = B.view_rec + (size_t) G * n,
+                      *const rec2 = B.view_rec + (size_t) 2 * G * n;
+        /* view index of slot k and its film position (quilt offset for k >= 1) */
+        auto view_of = [&](int k) -> uint32_t {
+            uint32_t id = p_idx + (uint32_t) k;
+            return id < max_idx ? id : id - (uint32_t) G;
+        };
+        auto put_pos = [&](int k, float x, float y) {
+            if (k > 0) {
+                uint32_t id = view_of(k);
+                uint32_t yy = id / P.gx, xx = id - yy * P.gx;
+                if (P.rev_x) xx = (P.gx - 1) - xx;
+                if (P.rev_y) yy = (P.gy - 1) - yy;
+                x += (float) (xx * P.sres_x);
+                y += (float) (yy * P.sres_y);
+            }
+            reinterpret_cast<float2 *>(&rec0[(size_t) k * n + i])[0] = make_float2(x, y);
+        };
+        float v_pdf[G], v_pdflk[G], v_Jp[G], v_pdfM[G], v_wx[G], v_wy[G], v_wz[G], v_br[G], v_bg[G], v_bb[G], v_w[G];
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            sd[k].result = c3(0.f); sd[k].bsdf_val = c3(0.f); sd[k].wi = mk(0.f, 0.f, 0.f);
-            sd[k].px = sd[k].py = sd[k].weight = sd[k].pdfM = sd[k].pdf = sd[k].pdf_lk = sd[k].Jp = sd[k].iJp = 0.f;
-            uint32_t id = p_idx + (uint32_t) k;
-            sd[k].idx = id < max_idx ? id : id - (uint32_t) G;
-            sd[k].indirect = false; sd[k].valid = false;
+            v_pdf[k] = v_pdflk[k] = v_Jp[k] = v_pdfM[k] = 0.f;
+            v_wx[k] = v_wy[k] = v_wz[k] = 0.f;
+            v_br[k] = v_bg[k] = v_bb[k] = 0.f;
+            v_w[k] = 0.f;
         }
-        sd[0].px = sx; sd[0].py = sy;
+        uint32_t vflags = 0;   /* bit k: valid, bit 16 + k: indirect */
+        C3 result0 = c3(0.f);  /* slot-0 emission + direct, for the non-MIS path */
+        bool records_done = false;
+        put_pos(0, sx, sy);
 
         /* ---- sample_multi (mvpath_multi.h:130-369) ---- */
         bool valid_ray = false, adapt_mask = false;
@@ -839,7 +868,7 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
             bool p_hit = si.valid();
             int32_t em = si_emitter(sc, si);
             bool direct_em = em >= 0;
-            if (direct_em) sd[0].result = emitter_eval(sc, em, si, true);
+            C3 emitted = direct_em ? emitter_eval(sc, em, si, true) : c3(0.f);
             int32_t b = p_hit ? S.shapes[si.shape].bsdf : -1;
             bool bsdf_smooth = (bsdf_flags(S.bsdfs, b) & BF_Smooth) != 0;
             bool active_em = p_hit && bsdf_smooth;
@@ -872,139 +901,129 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                 bd.rsqrt_a = rsqrt_(bd.alpha);
                 bd.diffuse = flag_diff;
                 bd.reuse = reuse;
-                sd[0].bsdf_val = bsdf_val;
+                v_br[0] = bsdf_val.r; v_bg[0] = bsdf_val.g; v_bb[0] = bsdf_val.b;
                 /* ---- camera_selection (mvpath_multi.h:371-464) ---- */
-                {
-                    Surf p0 = persp_sample_surface(V[sd[0].idx], si, p_hit);
-                    sd[0].pdf = p0.pdf;
-                    sd[0].pdf_lk = p0.pdf;
-                    sd[0].Jp = p0.Jp;
-                    sd[0].iJp = p_hit ? rcp(p0.Jp) : 0.f;
-                    sd[0].wi = si.wi;
-                    sd[0].valid = p_hit;
-                    sd[0].indirect = p_hit;
-                    f3 wo_r0 = reflect_l(si.wi);
-                    sd[0].pdfM = P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
-                                            : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit);
-                    if (bd.diffuse) sd[0].pdfM = 1.f;
-                    float n_direct = 1.f, n_indir = 2.f;
-#pragma unroll
-                    for (int k = 1; k < G; ++k) {
-                        Surf r = persp_sample_surface(V[sd[k].idx], si, bd.reuse);
-                        bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
-                        if (valid) {
-                            ++st_vis;
-                            Ray vr = spawn_ray_to(si.p, si.n, r.p);
-                            valid = !trace_any(sc, vr);
-                        }
-                        f3 wik = si.sh.to_local(r.d);
-                        sd[k].wi = wik;
-                        f3 wor = reflect_l(wik);
-                        sd[k].pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
-                                                : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
-                        float pdf_Mat = P.fast_mis ? tv_pdf_fast(wo_r0, wik, sd[k].pdfM, bd, valid)
-                                                   : tv_pdf(S.bsdfs, wo_r0, wik, sd[k].pdfM, bd, valid);
-                        if (bd.diffuse) pdf_Mat = 1.f;
-                        float J = r.Jp * sd[0].iJp;
-                        float pdf_J = J > 1.f ? rcp(J) : J;
-                        float pdf_Sel = pdf_Mat * pdf_J;
-                        valid = valid && (rng.next_1d() < pdf_Sel);
-                        sd[k].Jp = r.Jp;
-                        sd[k].iJp = valid ? rcp(r.Jp) : 0.f;
-                        sd[k].px = r.uvx;
-                        sd[k].py = r.uvy;
-                        sd[k].pdf = valid ? r.pdf : 0.f;
-                        sd[k].pdf_lk = valid ? sd[0].pdf * J * pdf_Sel : 0.f;
-                        sd[k].valid = valid;
-                        bool indirect = valid, direct = valid;
-                        bool replace = n_indir * rng.next_1d() < 1.f;
-                        C3 bvk;
-                        float bpk;
-                        BSample bsk;
-                        C3 bwk;
-                        bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
-                        bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
-                        direct = direct && bpk > 0.f;
-                        sd[k].bsdf_val = bvk;
-                        direct_pdf += direct ? bpk : 0.f;
-                        n_direct += (float) direct;
-                        indirect = indirect && bsk.type == bsmp.type;
-                        if (indirect && replace) bsmp.wo = bsk.wo;
-                        n_indir += (float) indirect;
-                        sd[k].indirect = indirect;
-                    }
-                    direct_pdf /= n_direct;
-                }
-                /* ---- mis_weights (mvpath_multi.h:466-523) ---- */
-#pragma unroll
-                for (int k = 0; k < G; ++k) {
-                    float pdfSum = sd[k].pdf_lk;
-                    if (k > 0) pdfSum += sd[k].pdf;
-                    bool cond = k > 0 ? sd[k].valid : bd.reuse;
-                    float add;
-                    if (cond && !bd.diffuse) {
-                        float acc = 0.f;
-#pragma unroll
-                        for (int j = 1; j < G; ++j) {
-                            if (j == k) continue;
-                            float pdf_J = vmin(sqr(sd[j].Jp * sd[k].iJp), 1.f);
-                            f3 worj = reflect_l(sd[j].wi);
-                            float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, sd[k].wi, sd[k].pdfM, bd, sd[j].valid)
-                                                       : tv_pdf(S.bsdfs, worj, sd[k].wi, sd[k].pdfM, bd, sd[j].valid);
-                            acc = fmadd(sd[j].pdf, pdf_J * pdf_Mat, acc);
-                        }
-                        add = acc;
-                    } else {
-                        float acc = 0.f;
-#pragma unroll
-                        for (int j = 1; j < G; ++j) {
-                            if (j == k) continue;
-                            float pdf_J = vmin(sqr(sd[j].Jp * sd[k].iJp), 1.f);
-                            acc = fmadd(sd[j].pdf, pdf_J, acc);
-                        }
-                        add = cond ? acc : 0.f;
-                    }
-                    pdfSum += add;
-                    sd[k].weight = sd[k].pdf_lk / pdfSum;
-                }
-            } else {
-                sd[0].valid = p_hit;
-#pragma unroll
+                Surf p0 = persp_sample_surface(V[view_of(0)], si, p_hit);
+                const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
+                v_pdf[0] = pdf0; v_pdflk[0] = pdf0; v_Jp[0] = Jp0;
+                v_wx[0] = si.wi.x; v_wy[0] = si.wi.y; v_wz[0] = si.wi.z;
+                vflags |= p_hit ? (1u | (1u << 16)) : 0u;
+                const f3 wo_r0 = reflect_l(si.wi);
+                v_pdfM[0] = P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
+                                       : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit);
+                if (bd.diffuse) v_pdfM[0] = 1.f;
+                float n_direct = 1.f, n_indir = 2.f;
+#pragma unroll 1
                 for (int k = 1; k < G; ++k) {
-                    Surf r = persp_sample_surface(V[sd[k].idx], si, reuse);
+                    Surf r = persp_sample_surface(V[view_of(k)], si, bd.reuse);
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
                         Ray vr = spawn_ray_to(si.p, si.n, r.p);
                         valid = !trace_any(sc, vr);
                     }
-                    sd[k].px = r.uvx;
-                    sd[k].py = r.uvy;
-                    sd[k].valid = valid;
+                    f3 wik = si.sh.to_local(r.d);
+                    v_wx[k] = wik.x; v_wy[k] = wik.y; v_wz[k] = wik.z;
+                    f3 wor = reflect_l(wik);
+                    float pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
+                                            : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
+                    v_pdfM[k] = pdfM;
+                    float pdf_Mat = P.fast_mis ? tv_pdf_fast(wo_r0, wik, pdfM, bd, valid)
+                                               : tv_pdf(S.bsdfs, wo_r0, wik, pdfM, bd, valid);
+                    if (bd.diffuse) pdf_Mat = 1.f;
+                    float J = r.Jp * iJp0;
+                    float pdf_J = J > 1.f ? rcp(J) : J;
+                    float pdf_Sel = pdf_Mat * pdf_J;
+                    valid = valid && (rng.next_1d() < pdf_Sel);
+                    v_Jp[k] = r.Jp;
+                    put_pos(k, r.uvx, r.uvy);
+                    v_pdf[k] = valid ? r.pdf : 0.f;
+                    v_pdflk[k] = valid ? pdf0 * J * pdf_Sel : 0.f;
+                    bool indirect = valid, direct = valid;
+                    bool replace = n_indir * rng.next_1d() < 1.f;
+                    C3 bvk;
+                    float bpk;
+                    BSample bsk;
+                    C3 bwk;
+                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
+                    bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
+                    direct = direct && bpk > 0.f;
+                    v_br[k] = bvk.r; v_bg[k] = bvk.g; v_bb[k] = bvk.b;
+                    direct_pdf += direct ? bpk : 0.f;
+                    n_direct += (float) direct;
+                    indirect = indirect && bsk.type == bsmp.type;
+                    if (indirect && replace) bsmp.wo = bsk.wo;
+                    n_indir += (float) indirect;
+                    vflags |= (valid ? (1u << k) : 0u) | (indirect ? (1u << (16 + k)) : 0u);
+                }
+                direct_pdf /= n_direct;
+                /* ---- mis_weights (mvpath_multi.h:466-523) ---- */
+#pragma unroll 1
+                for (int k = 0; k < G; ++k) {
+                    const bool vk = (vflags >> k) & 1u;
+                    const float iJpk = k == 0 ? iJp0 : (vk ? rcp(v_Jp[k]) : 0.f);
+                    const f3 wik = mk(v_wx[k], v_wy[k], v_wz[k]);
+                    const float pdfMk = v_pdfM[k];
+                    float pdfSum = v_pdflk[k];
+                    if (k > 0) pdfSum += v_pdf[k];
+                    bool cond = k > 0 ? vk : bd.reuse;
+                    float acc = 0.f;
+                    if (cond && !bd.diffuse) {
+#pragma unroll 1
+                        for (int j = 1; j < G; ++j) {
+                            if (j == k) continue;
+                            float pdf_J = vmin(sqr(v_Jp[j] * iJpk), 1.f);
+                            f3 worj = reflect_l(mk(v_wx[j], v_wy[j], v_wz[j]));
+                            const bool vj = (vflags >> j) & 1u;
+                            float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
+                                                       : tv_pdf(S.bsdfs, worj, wik, pdfMk, bd, vj);
+                            acc = fmadd(v_pdf[j], pdf_J * pdf_Mat, acc);
+                        }
+                    } else {
+#pragma unroll 1
+                        for (int j = 1; j < G; ++j) {
+                            if (j == k) continue;
+                            float pdf_J = vmin(sqr(v_Jp[j] * iJpk), 1.f);
+                            acc = fmadd(v_pdf[j], pdf_J, acc);
+                        }
+                        acc = cond ? acc : 0.f;
+                    }
+                    pdfSum += acc;
+                    v_w[k] = v_pdflk[k] / pdfSum;
+                }
+            } else {
+                vflags |= p_hit ? 1u : 0u;
+#pragma unroll 1
+                for (int k = 1; k < G; ++k) {
+                    Surf r = persp_sample_surface(V[view_of(k)], si, reuse);
+                    bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
+                    if (valid) {
+                        ++st_vis;
+                        Ray vr = spawn_ray_to(si.p, si.n, r.p);
+                        valid = !trace_any(sc, vr);
+                    }
+                    put_pos(k, r.uvx, r.uvy);
+                    vflags |= valid ? (1u << k) : 0u;
                 }
             }
             /* ---- emitter sampling contribution ---- */
-            {
-                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
-                C3 emis_mis = em_w * mis_em;
-                if (should_mis) {
-#pragma unroll
-                    for (int k = 0; k < G; ++k)
-                        if (active_em && sd[k].valid) sd[k].result = cfma(sd[k].bsdf_val, emis_mis, sd[k].result);
-                } else {
-                    if (active_em) sd[0].result = cfma(bsdf_val, emis_mis, sd[0].result);
-                }
-            }
+            float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
+            C3 emis_mis = em_w * mis_em;
             /* ---- BSDF sampling / multi-view mixture pdf ---- */
             Ray pd_ray = spawn_ray(si.p, si.n, si.sh.to_world(bsmp.wo));
             if (should_mis) {
                 float n_indir = 0.f, pdf = 0.f;
-#pragma unroll
+#pragma unroll 1
                 for (int k = 0; k < G; ++k) {
-                    bool valid = sd[k].indirect;
+                    const size_t o = (size_t) k * n + i;
+                    /* result: emission (slot 0) + direct light through this view's BSDF value */
+                    C3 res = k == 0 ? emitted : c3(0.f);
+                    if (active_em && ((vflags >> k) & 1u)) res = cfma(C3{v_br[k], v_bg[k], v_bb[k]}, emis_mis, res);
+                    rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
+                    bool valid = (vflags >> (16 + k)) & 1u;
                     C3 bv;
                     float bp;
-                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, sd[k].wi, bsmp.wo, valid, bv, bp);
+                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, mk(v_wx[k], v_wy[k], v_wz[k]), bsmp.wo, valid, bv, bp);
                     if (k == 0) {
                         bv = p_not_delta ? bv : bsdf_weight;
                         bp = p_not_delta ? bp : bsmp.pdf;
@@ -1013,13 +1032,18 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                     bool pvalid = bp > 0.f;
                     valid = valid && ((k == 0) ? (pvalid || delta) : pvalid);
                     bp = valid ? bp : 0.f;
-                    sd[k].bsdf_val = valid ? bv : c3(0.f);
+                    bv = valid ? bv : c3(0.f);
+                    rec2[o] = make_float4(bv.r, bv.g, bv.b, 0.f);
                     pdf += bp;
                     n_indir += (float) valid;
-                    sd[k].indirect = sd[k].indirect && valid;
+                    if (!valid) vflags &= ~(1u << (16 + k));
                 }
                 bsmp.pdf = p_not_delta ? pdf / n_indir : bsmp.pdf;
                 adapt_mask = p_hit && !flag_null && (n_indir <= 1.f);
+                records_done = true;
+            } else {
+                result0 = emitted;
+                if (active_em) result0 = cfma(bsdf_val, emis_mis, result0);
             }
             C3 thr = should_mis ? c3(1.f) : bsdf_weight;
             valid_ray = valid_ray || (p_hit && !flag_null);
@@ -1042,33 +1066,33 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                 ps.rng_seq = v1;
                 push = true;
             }
-            (void) rand_1;
             /* p_sample.weight/valid finalisation happens after the suffix */
             if (!should_mis) {
 #pragma unroll
-                for (int k = 0; k < G; ++k) sd[k].weight = 1.f;
+                for (int k = 0; k < G; ++k) v_w[k] = 1.f;
             }
-            sd[0].weight = p_hit ? sd[0].weight : 1.f;
-            sd[0].valid = true;
+            v_w[0] = p_hit ? v_w[0] : 1.f;
+            vflags |= 1u;
         }
         if (!push) B.lane_out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) | (should_mis ? LF_MIS : 0u);
         B.lane_rec[i] = make_float4(pdfW, bitsf(lflags), 0.f, 0.f);
-#pragma unroll
+        if (P.max_depth == 0) {
+            /* no intersection at all: slots k >= 1 keep position 0 (+ quilt offset), slot 0 stays invalid */
+#pragma unroll 1
+            for (int k = 1; k < G; ++k) put_pos(k, 0.f, 0.f);
+            vflags = 0;
+        }
+#pragma unroll 1
         for (int k = 0; k < G; ++k) {
-            float px_k = sd[k].px, py_k = sd[k].py;
-            if (k > 0) {
-                uint32_t y = sd[k].idx / P.gx, x = sd[k].idx - y * P.gx;
-                if (P.rev_x) x = (P.gx - 1) - x;
-                if (P.rev_y) y = (P.gy - 1) - y;
-                px_k += (float) (x * P.sres_x);
-                py_k += (float) (y * P.sres_y);
+            const size_t o = (size_t) k * n + i;
+            uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
+            reinterpret_cast<float2 *>(&rec0[o])[1] = make_float2(v_w[k], bitsf(vf));
+            if (!records_done) {
+                C3 res = k == 0 ? result0 : c3(0.f);
+                rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
+                rec2[o] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            uint32_t vf = (sd[k].valid ? VF_VALID : 0u) | (sd[k].indirect ? VF_INDIRECT : 0u);
-            size_t o = (size_t) k * n + i;
-            B.view_rec[o] = make_float4(px_k, py_k, sd[k].weight, bitsf(vf));
-            B.view_rec[(size_t) G * n + o] = make_float4(sd[k].result.r, sd[k].result.g, sd[k].result.b, 0.f);
-            B.view_rec[(size_t) 2 * G * n + o] = make_float4(sd[k].bsdf_val.r, sd[k].bsdf_val.g, sd[k].bsdf_val.b, 0.f);
         }
     }
     uint32_t slot = queue_slot(push, B.cnt_out);

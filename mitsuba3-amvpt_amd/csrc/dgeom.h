@@ -28,6 +28,7 @@ struct SceneRef {
     const DNode *nodes;
     const DPrim *prims;
     const DScene *g;
+    uint32_t n_nodes;
 };
 
 struct Hit { float t, u, v; int32_t prim; };
@@ -116,32 +117,34 @@ AD bool box_hit(const DNode &n, f3 o, f3 inv_d, float tmax, float &tnear) {
     return tmin <= tm;
 }
 
-constexpr int kStack = 48;
-
-/* Closest hit over the BVH (ties broken toward the lower primitive index). */
 /* 1/d with zero components replaced by +-1e-30 so that (bound - o) * inv never is 0*inf */
 AD f3 safe_inv(f3 d) {
     return {1.f / (d.x != 0.f ? d.x : mulsign(1e-30f, d.x)), 1.f / (d.y != 0.f ? d.y : mulsign(1e-30f, d.y)),
             1.f / (d.z != 0.f ? d.z : mulsign(1e-30f, d.z))};
 }
 
+/*
+ * Closest hit over the threaded BVH (dscene.h): one box test per visited node,
+ * no traversal stack (so nothing is spilled to scratch).  Ties resolve toward
+ * the lower scene-order primitive index, so the hit equals a brute-force scan.
+ */
 AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
-    f3 inv_d = safe_inv(ray.d);
-    uint32_t stack[kStack];
-    int sp = 0;
-    uint32_t node = 0;
+    const f3 inv_d = safe_inv(ray.d);
     float tmax_box = ray.maxt;
-    while (true) {
+    uint32_t node = 0;
+    while (node < sc.n_nodes) {
         const DNode n = sc.nodes[node];
-        if (n.count) {
-            for (uint32_t i = 0; i < n.count; ++i) {
-                uint32_t pi = n.left_or_first + i;
+        float tn;
+        const bool hit = box_hit(n, ray.o, inv_d, tmax_box, tn);
+        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+        if (hit && count) {
+            for (uint32_t i = 0; i < count; ++i) {
+                const uint32_t pi = n.first + i;
                 const DPrim p = sc.prims[pi];
                 float t, u, v;
                 if (prim_hit(p, ray, t, u, v)) {
-                    /* ties resolve toward the lower scene-order primitive index (p.pad) */
                     if (t < best.t || (t == best.t && p.pad < best_orig)) {
                         best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
                         best_orig = p.pad;
@@ -149,56 +152,29 @@ AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
                     }
                 }
             }
-        } else {
-            uint32_t l = n.left_or_first, r = l + 1;
-            float tl, tr;
-            bool hl = box_hit(sc.nodes[l], ray.o, inv_d, tmax_box, tl);
-            bool hr = box_hit(sc.nodes[r], ray.o, inv_d, tmax_box, tr);
-            if (hl && hr) {
-                uint32_t first = tl <= tr ? l : r, second = tl <= tr ? r : l;
-                if (sp < kStack) stack[sp++] = second;
-                node = first;
-                continue;
-            }
-            if (hl) { node = l; continue; }
-            if (hr) { node = r; continue; }
         }
-        if (sp == 0) break;
-        node = stack[--sp];
-        /* prune with the current best */
+        node = (hit && !count) ? node + 1 : skip;
     }
     return best;
 }
 
 /* Any hit in [0, maxt] (Scene::ray_test). */
 AD bool trace_any(const SceneRef &sc, const Ray &ray) {
-    f3 inv_d = safe_inv(ray.d);
-    uint32_t stack[kStack];
-    int sp = 0;
+    const f3 inv_d = safe_inv(ray.d);
     uint32_t node = 0;
-    while (true) {
+    while (node < sc.n_nodes) {
         const DNode n = sc.nodes[node];
-        if (n.count) {
-            for (uint32_t i = 0; i < n.count; ++i) {
-                const DPrim p = sc.prims[n.left_or_first + i];
+        float tn;
+        const bool hit = box_hit(n, ray.o, inv_d, ray.maxt, tn);
+        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+        if (hit && count) {
+            for (uint32_t i = 0; i < count; ++i) {
+                const DPrim p = sc.prims[n.first + i];
                 float t, u, v;
                 if (prim_hit(p, ray, t, u, v)) return true;
             }
-        } else {
-            uint32_t l = n.left_or_first, r = l + 1;
-            float tl, tr;
-            bool hl = box_hit(sc.nodes[l], ray.o, inv_d, ray.maxt, tl);
-            bool hr = box_hit(sc.nodes[r], ray.o, inv_d, ray.maxt, tr);
-            if (hl && hr) {
-                if (sp < kStack) stack[sp++] = r;
-                node = l;
-                continue;
-            }
-            if (hl) { node = l; continue; }
-            if (hr) { node = r; continue; }
         }
-        if (sp == 0) break;
-        node = stack[--sp];
+        node = (hit && !count) ? node + 1 : skip;
     }
     return false;
 }

@@ -19,12 +19,19 @@ namespace amvpt {
 
 enum : uint32_t { PRIM_RECT = 0, PRIM_TRI = 1, PRIM_SPHERE = 2 };
 
+/*
+ * Threaded (stackless) BVH node, nodes stored in depth-first pre-order: the
+ * first child of an inner node is the next node, and `skip` is the node that
+ * follows the whole subtree (n_nodes for the last one).  Traversal is
+ * "hit -> descend (node + 1) or test the leaf, miss/leaf -> skip": no stack.
+ */
 struct alignas(16) DNode {
     float lo[3];
-    uint32_t left_or_first;  /* inner: index of left child (right = left + 1); leaf: first prim */
+    uint32_t first;          /* leaf: first prim; inner: unused */
     float hi[3];
-    uint32_t count;          /* 0: inner node; >0: leaf with `count` prims */
+    uint32_t skip_count;     /* bits 0..27: skip node index; bits 28..31: prim count (0 = inner node) */
 };
+constexpr uint32_t kNodeSkipMask = 0x0fffffffu, kNodeCountShift = 28, kMaxLeafPrims = 15;
 
 struct alignas(16) DPrim {
     /* rect: rows 0..2 of to_object; tri: p0, p1, p2 (xyz); sphere: a = (center, radius) */
