@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(os.path.dirname(_HERE), "lib")
+# AMVPT_LIB_DIR selects a variant build (Makefile LIB=...) for A/B measurements.
+LIB_DIR = os.environ.get("AMVPT_LIB_DIR") or os.path.join(os.path.dirname(_HERE), "lib")
 HIP_LIB_PATH = os.path.join(LIB_DIR, "libamvpt_hip.so")
 HOST_LIB_PATH = os.path.join(LIB_DIR, "libamvpt_host.so")
 

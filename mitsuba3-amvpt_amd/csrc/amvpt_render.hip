@@ -73,12 +73,26 @@ struct Bufs {
 /* ------------------------------------------------------------------ */
 
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;
+constexpr int kPrimBlock = 128;
+enum { F_PDF, F_PDFLK, F_JP, F_PDFM, F_WX, F_WY, F_WZ, F_BR, F_BG, F_BB, F_W, VS_FIELDS };
+
+/* Small BVHs are walked wave-uniformly from global memory (scalar loads) and not
+ * staged; mid-size ones are staged in LDS; large ones stay in global memory. */
+__host__ __device__ inline bool scene_staged(uint32_t n_nodes, uint32_t lds_bytes) {
+    return n_nodes > kUniformNodeLimit && lds_bytes <= kLdsSceneBytes;
+}
+__host__ __device__ inline uint32_t scene_lds_bytes(const DScene &S) {
+    return scene_staged(S.n_nodes, S.lds_bytes) ? (S.lds_bytes + 15u) & ~15u : 0u;
+}
 
 AD SceneRef stage_scene(const DScene &S, char *lds) {
     SceneRef sc;
     sc.g = &S;
     sc.n_nodes = S.n_nodes;
-    if (S.lds_bytes <= kLdsSceneBytes) {
+    sc.gnodes = S.nodes;
+    sc.gprims = S.prims;
+    sc.uniform = S.n_nodes <= kUniformNodeLimit;
+    if (scene_staged(S.n_nodes, S.lds_bytes)) {
         const uint32_t nn = S.n_nodes * (uint32_t) sizeof(DNode) / 16, np = S.n_prims * (uint32_t) sizeof(DPrim) / 16;
         float4 *dst = (float4 *) lds;
         const float4 *sn = (const float4 *) S.nodes, *spr = (const float4 *) S.prims;
@@ -797,18 +811,24 @@ AD float tv_pdf_fast(f3 wo_l, f3 wi_k, float p_k, const BD &bd, bool active) {
 AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 
 /*
- * Per-view state lives in small SoA register arrays indexed by the (wave-uniform)
- * view counter of non-unrolled loops, so each per-view body (a visibility ray,
- * three BSDF evaluations, ...) is emitted once: the fully unrolled form did not
- * fit the register file and spilled the whole SampleData array to scratch.
+ * Per-view state lives in LDS (VS_FIELDS floats per view slot, thread-minor so
+ * every access is bank-conflict free) and the per-view loops are not unrolled, so
+ * each per-view body (a visibility ray, three BSDF evaluations, ...) is emitted
+ * once: the unrolled form with register arrays needed > 256 VGPRs and spilled.
  * View records are written as soon as each part is final:
  *   rec0[k] = (splat x, splat y, weight, flags), rec1[k] = result, rec2[k] = bsdf_val.
  */
 template <int G>
-__global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+#ifndef AMVPT_PRIM_WAVES
+#define AMVPT_PRIM_WAVES 1
+#endif
+__global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DScene S = *Sp;
     SceneRef sc = stage_scene(S, lds);
+    /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
+    float *const vs = reinterpret_cast<float *>(lds + scene_lds_bytes(S)) + threadIdx.x;
+#define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = i < P.chunk_n;
     PathState ps;
@@ -846,14 +866,8 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
             }
             reinterpret_cast<float2 *>(&rec0[(size_t) k * n + i])[0] = make_float2(x, y);
         };
-        float v_pdf[G], v_pdflk[G], v_Jp[G], v_pdfM[G], v_wx[G], v_wy[G], v_wz[G], v_br[G], v_bg[G], v_bb[G], v_w[G];
-#pragma unroll
-        for (int k = 0; k < G; ++k) {
-            v_pdf[k] = v_pdflk[k] = v_Jp[k] = v_pdfM[k] = 0.f;
-            v_wx[k] = v_wy[k] = v_wz[k] = 0.f;
-            v_br[k] = v_bg[k] = v_bb[k] = 0.f;
-            v_w[k] = 0.f;
-        }
+#pragma unroll 1
+        for (int f = 0; f < VS_FIELDS * G; ++f) vs[f * kPrimBlock] = 0.f;
         uint32_t vflags = 0;   /* bit k: valid, bit 16 + k: indirect */
         C3 result0 = c3(0.f);  /* slot-0 emission + direct, for the non-MIS path */
         bool records_done = false;
@@ -901,17 +915,17 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                 bd.rsqrt_a = rsqrt_(bd.alpha);
                 bd.diffuse = flag_diff;
                 bd.reuse = reuse;
-                v_br[0] = bsdf_val.r; v_bg[0] = bsdf_val.g; v_bb[0] = bsdf_val.b;
+                VSF(F_BR, 0) = bsdf_val.r; VSF(F_BG, 0) = bsdf_val.g; VSF(F_BB, 0) = bsdf_val.b;
                 /* ---- camera_selection (mvpath_multi.h:371-464) ---- */
                 Surf p0 = persp_sample_surface(V[view_of(0)], si, p_hit);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
-                v_pdf[0] = pdf0; v_pdflk[0] = pdf0; v_Jp[0] = Jp0;
-                v_wx[0] = si.wi.x; v_wy[0] = si.wi.y; v_wz[0] = si.wi.z;
+                VSF(F_PDF, 0) = pdf0; VSF(F_PDFLK, 0) = pdf0; VSF(F_JP, 0) = Jp0;
+                VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
                 vflags |= p_hit ? (1u | (1u << 16)) : 0u;
                 const f3 wo_r0 = reflect_l(si.wi);
-                v_pdfM[0] = P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
+                VSF(F_PDFM, 0) = P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
                                        : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit);
-                if (bd.diffuse) v_pdfM[0] = 1.f;
+                if (bd.diffuse) VSF(F_PDFM, 0) = 1.f;
                 float n_direct = 1.f, n_indir = 2.f;
 #pragma unroll 1
                 for (int k = 1; k < G; ++k) {
@@ -923,11 +937,11 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                         valid = !trace_any(sc, vr);
                     }
                     f3 wik = si.sh.to_local(r.d);
-                    v_wx[k] = wik.x; v_wy[k] = wik.y; v_wz[k] = wik.z;
+                    VSF(F_WX, k) = wik.x; VSF(F_WY, k) = wik.y; VSF(F_WZ, k) = wik.z;
                     f3 wor = reflect_l(wik);
                     float pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
                                             : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
-                    v_pdfM[k] = pdfM;
+                    VSF(F_PDFM, k) = pdfM;
                     float pdf_Mat = P.fast_mis ? tv_pdf_fast(wo_r0, wik, pdfM, bd, valid)
                                                : tv_pdf(S.bsdfs, wo_r0, wik, pdfM, bd, valid);
                     if (bd.diffuse) pdf_Mat = 1.f;
@@ -935,10 +949,10 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                     float pdf_J = J > 1.f ? rcp(J) : J;
                     float pdf_Sel = pdf_Mat * pdf_J;
                     valid = valid && (rng.next_1d() < pdf_Sel);
-                    v_Jp[k] = r.Jp;
+                    VSF(F_JP, k) = r.Jp;
                     put_pos(k, r.uvx, r.uvy);
-                    v_pdf[k] = valid ? r.pdf : 0.f;
-                    v_pdflk[k] = valid ? pdf0 * J * pdf_Sel : 0.f;
+                    VSF(F_PDF, k) = valid ? r.pdf : 0.f;
+                    VSF(F_PDFLK, k) = valid ? pdf0 * J * pdf_Sel : 0.f;
                     bool indirect = valid, direct = valid;
                     bool replace = n_indir * rng.next_1d() < 1.f;
                     C3 bvk;
@@ -948,7 +962,7 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                     bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
                     bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
                     direct = direct && bpk > 0.f;
-                    v_br[k] = bvk.r; v_bg[k] = bvk.g; v_bb[k] = bvk.b;
+                    VSF(F_BR, k) = bvk.r; VSF(F_BG, k) = bvk.g; VSF(F_BB, k) = bvk.b;
                     direct_pdf += direct ? bpk : 0.f;
                     n_direct += (float) direct;
                     indirect = indirect && bsk.type == bsmp.type;
@@ -961,35 +975,35 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
 #pragma unroll 1
                 for (int k = 0; k < G; ++k) {
                     const bool vk = (vflags >> k) & 1u;
-                    const float iJpk = k == 0 ? iJp0 : (vk ? rcp(v_Jp[k]) : 0.f);
-                    const f3 wik = mk(v_wx[k], v_wy[k], v_wz[k]);
-                    const float pdfMk = v_pdfM[k];
-                    float pdfSum = v_pdflk[k];
-                    if (k > 0) pdfSum += v_pdf[k];
+                    const float iJpk = k == 0 ? iJp0 : (vk ? rcp(VSF(F_JP, k)) : 0.f);
+                    const f3 wik = mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
+                    const float pdfMk = VSF(F_PDFM, k);
+                    float pdfSum = VSF(F_PDFLK, k);
+                    if (k > 0) pdfSum += VSF(F_PDF, k);
                     bool cond = k > 0 ? vk : bd.reuse;
                     float acc = 0.f;
                     if (cond && !bd.diffuse) {
 #pragma unroll 1
                         for (int j = 1; j < G; ++j) {
                             if (j == k) continue;
-                            float pdf_J = vmin(sqr(v_Jp[j] * iJpk), 1.f);
-                            f3 worj = reflect_l(mk(v_wx[j], v_wy[j], v_wz[j]));
+                            float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
+                            f3 worj = reflect_l(mk(VSF(F_WX, j), VSF(F_WY, j), VSF(F_WZ, j)));
                             const bool vj = (vflags >> j) & 1u;
                             float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
                                                        : tv_pdf(S.bsdfs, worj, wik, pdfMk, bd, vj);
-                            acc = fmadd(v_pdf[j], pdf_J * pdf_Mat, acc);
+                            acc = fmadd(VSF(F_PDF, j), pdf_J * pdf_Mat, acc);
                         }
                     } else {
 #pragma unroll 1
                         for (int j = 1; j < G; ++j) {
                             if (j == k) continue;
-                            float pdf_J = vmin(sqr(v_Jp[j] * iJpk), 1.f);
-                            acc = fmadd(v_pdf[j], pdf_J, acc);
+                            float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
+                            acc = fmadd(VSF(F_PDF, j), pdf_J, acc);
                         }
                         acc = cond ? acc : 0.f;
                     }
                     pdfSum += acc;
-                    v_w[k] = v_pdflk[k] / pdfSum;
+                    VSF(F_W, k) = VSF(F_PDFLK, k) / pdfSum;
                 }
             } else {
                 vflags |= p_hit ? 1u : 0u;
@@ -1018,12 +1032,12 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
                     const size_t o = (size_t) k * n + i;
                     /* result: emission (slot 0) + direct light through this view's BSDF value */
                     C3 res = k == 0 ? emitted : c3(0.f);
-                    if (active_em && ((vflags >> k) & 1u)) res = cfma(C3{v_br[k], v_bg[k], v_bb[k]}, emis_mis, res);
+                    if (active_em && ((vflags >> k) & 1u)) res = cfma(C3{VSF(F_BR, k), VSF(F_BG, k), VSF(F_BB, k)}, emis_mis, res);
                     rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
                     bool valid = (vflags >> (16 + k)) & 1u;
                     C3 bv;
                     float bp;
-                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, mk(v_wx[k], v_wy[k], v_wz[k]), bsmp.wo, valid, bv, bp);
+                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k)), bsmp.wo, valid, bv, bp);
                     if (k == 0) {
                         bv = p_not_delta ? bv : bsdf_weight;
                         bp = p_not_delta ? bp : bsmp.pdf;
@@ -1069,9 +1083,9 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
             /* p_sample.weight/valid finalisation happens after the suffix */
             if (!should_mis) {
 #pragma unroll
-                for (int k = 0; k < G; ++k) v_w[k] = 1.f;
+                for (int k = 0; k < G; ++k) VSF(F_W, k) = 1.f;
             }
-            v_w[0] = p_hit ? v_w[0] : 1.f;
+            VSF(F_W, 0) = p_hit ? VSF(F_W, 0) : 1.f;
             vflags |= 1u;
         }
         if (!push) B.lane_out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1087,7 +1101,7 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
         for (int k = 0; k < G; ++k) {
             const size_t o = (size_t) k * n + i;
             uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
-            reinterpret_cast<float2 *>(&rec0[o])[1] = make_float2(v_w[k], bitsf(vf));
+            reinterpret_cast<float2 *>(&rec0[o])[1] = make_float2(VSF(F_W, k), bitsf(vf));
             if (!records_done) {
                 C3 res = k == 0 ? result0 : c3(0.f);
                 rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
@@ -1103,6 +1117,7 @@ __global__ void __launch_bounds__(256) k_mv_primary(KParams P, const DScene *Sp,
         stat_add(&B.stats[0], (ok && P.max_depth != 0) ? 1ull : 0ull);
     }
 }
+#undef VSF
 
 /* ------------------------------------------------------------------ */
 /* k_splat_multi<G>: indirect accumulation + splats (mvpath_multi.h:343-368,44-76) */
@@ -1258,7 +1273,8 @@ static Arena g_arena;
 template <int G>
 static void launch_primary(dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *S, const DView *V,
                            const Bufs &B) {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G>), grid, dim3(256), lds, st, P, S, V, B);
+    const size_t lds_view = (size_t) VS_FIELDS * G * kPrimBlock * sizeof(float);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G>), grid, dim3(kPrimBlock), lds + lds_view, st, P, S, V, B);
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
@@ -1382,7 +1398,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     B.stats = dstats;
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
-    const size_t lds = scene->dev.lds_bytes <= kLdsSceneBytes ? scene->dev.lds_bytes : 0;
+    const size_t lds = scene_staged(scene->dev.n_nodes, scene->dev.lds_bytes) ? (scene->dev.lds_bytes + 15u) & ~15u : 0;
     hipEvent_t ev[4];
     for (auto &e : ev) HIPCHK(hipEventCreate(&e));
     float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;
@@ -1406,7 +1422,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             if (G == 1) {
                 hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
             } else {
-                kPrimary[G](grid, lds, st, P, dS, dviews, B);
+                kPrimary[G](dim3((cn + kPrimBlock - 1) / kPrimBlock), lds, st, P, dS, dviews, B);
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[1], st));

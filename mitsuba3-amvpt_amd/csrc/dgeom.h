@@ -25,11 +25,17 @@ AD f3 ray_at(const Ray &r, float t) { return fma3(r.d, t, r.o); }
 
 /* Scene tables as seen by a kernel; nodes/prims may point into LDS. */
 struct SceneRef {
-    const DNode *nodes;
+    const DNode *nodes;       /* LDS copy when staged, else global */
     const DPrim *prims;
+    const DNode *gnodes;      /* global tables (scalar loads on the wave-uniform path) */
+    const DPrim *gprims;
     const DScene *g;
     uint32_t n_nodes;
+    bool uniform;             /* small BVH: wave-uniform traversal (see trace_closest) */
 };
+
+/* BVHs up to this many nodes are traversed wave-uniformly. */
+constexpr uint32_t kUniformNodeLimit = 255;
 
 struct Hit { float t, u, v; int32_t prim; };
 
@@ -123,16 +129,78 @@ AD f3 safe_inv(f3 d) {
             1.f / (d.z != 0.f ? d.z : mulsign(1e-30f, d.z))};
 }
 
+AD uint32_t ufirst(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+/* Scalar (s_load) reads of read-only scene records at a wave-uniform index: the
+ * constant address space tells the backend the bytes are not written by the kernel. */
+template <typename T> AD T load_uniform(const T *base, uint32_t idx) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(4))) const v4u cv4u;
+    static_assert(sizeof(T) % 16 == 0, "16-byte records");
+    constexpr int W = (int) (sizeof(T) / 16);
+    const cv4u *p = (const cv4u *) (uintptr_t) base + (size_t) ufirst(idx) * W;
+    T out;
+    v4u *o = reinterpret_cast<v4u *>(&out);
+#pragma unroll
+    for (int k = 0; k < W; ++k) o[k] = p[k];
+    return out;
+}
+AD bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
+
+/* Primitive test with a wave-uniform primitive type (no divergence between shapes). */
+AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
+    if (type == PRIM_RECT) return rect_hit(p, r, t, u, v);
+    if (type == PRIM_TRI) return tri_hit(p, r, t, u, v);
+    u = v = 0.f;
+    return sphere_hit(p, r, t);
+}
+
 /*
- * Closest hit over the threaded BVH (dscene.h): one box test per visited node,
- * no traversal stack (so nothing is spilled to scratch).  Ties resolve toward
- * the lower scene-order primitive index, so the hit equals a brute-force scan.
+ * Closest hit over the threaded BVH (dscene.h), no traversal stack (nothing is
+ * spilled to scratch).  Ties resolve toward the lower scene-order primitive
+ * index, so the hit equals a brute-force scan whatever the traversal visits.
+ *
+ * Small BVHs (sc.uniform) are walked wave-uniformly: the wave enters a node if
+ * any active lane's ray hits its box and every active lane tests the leaf's
+ * primitives.  Node and primitive records are then wave-uniform scalar loads,
+ * the primitive type is a uniform branch, and there is no per-lane divergence.
+ * Testing a primitive for a lane whose own box test failed cannot change that
+ * lane's result (its box is padded and inclusive), so both walks are exact.
  */
 AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
     const f3 inv_d = safe_inv(ray.d);
     float tmax_box = ray.maxt;
+    if (sc.uniform) {
+        const uint32_t nn = ufirst(sc.n_nodes);
+        uint32_t node = 0;
+        while (node < nn) {
+            const DNode n = load_uniform(sc.gnodes, node);
+            float tn;
+            const bool enter = wave_any(box_hit(n, ray.o, inv_d, tmax_box, tn));
+            const uint32_t skc = ufirst(n.skip_count);
+            const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
+            if (enter && count) {
+                const uint32_t first = ufirst(n.first);
+                for (uint32_t i = 0; i < count; ++i) {
+                    const uint32_t pi = first + i;
+                    const DPrim p = load_uniform(sc.gprims, pi);
+                    float t, u, v;
+                    if (prim_hit_u(p, ufirst(p.type), ray, t, u, v)) {
+                        const uint32_t orig = ufirst(p.pad);
+                        if (t < best.t || (t == best.t && orig < best_orig)) {
+                            best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                            best_orig = orig;
+                            tmax_box = t;
+                        }
+                    }
+                }
+            }
+            node = (enter && !count) ? node + 1 : skip;
+        }
+        return best;
+    }
     uint32_t node = 0;
     while (node < sc.n_nodes) {
         const DNode n = sc.nodes[node];
@@ -158,9 +226,33 @@ AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     return best;
 }
 
-/* Any hit in [0, maxt] (Scene::ray_test). */
+/* Any hit in [0, maxt] (Scene::ray_test); same two walks as trace_closest. */
 AD bool trace_any(const SceneRef &sc, const Ray &ray) {
     const f3 inv_d = safe_inv(ray.d);
+    if (sc.uniform) {
+        const uint32_t nn = ufirst(sc.n_nodes);
+        bool found = false;
+        uint32_t node = 0;
+        while (node < nn) {
+            const DNode n = load_uniform(sc.gnodes, node);
+            float tn;
+            const bool enter = wave_any(!found && box_hit(n, ray.o, inv_d, ray.maxt, tn));
+            const uint32_t skc = ufirst(n.skip_count);
+            const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
+            if (enter && count) {
+                const uint32_t first = ufirst(n.first);
+                for (uint32_t i = 0; i < count; ++i) {
+                    const DPrim p = load_uniform(sc.gprims, first + i);
+                    float t, u, v;
+                    const bool h = prim_hit_u(p, ufirst(p.type), ray, t, u, v);
+                    found = found || h;
+                }
+                if (!wave_any(!found)) break;
+            }
+            node = (enter && !count) ? node + 1 : skip;
+        }
+        return found;
+    }
     uint32_t node = 0;
     while (node < sc.n_nodes) {
         const DNode n = sc.nodes[node];
