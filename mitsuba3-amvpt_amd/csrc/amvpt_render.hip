@@ -308,10 +308,12 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
  * writes zeros back, so one put costs two block barriers and no zeroing pass.
  */
 constexpr int kWinW = 96, kWinH = 16, kMaxWaves = 16, kMaxFoot = 5;
+constexpr int kSplatBlock = 512;   /* threads per splat block (see splat_lane) */
 constexpr int kWinCells = kWinW * kWinH;
 template <int C> struct SplatLds {
     static constexpr int NP = (C + 1) / 2;  /* channel pairs per cell */
     uint64_t win[2][kWinCells * NP];        /* pair p of cell c at win[b][p * plane + c] */
+    uint64_t dummy[NP * kSplatBlock];       /* per-lane sink for clipped footprint cells */
     alignas(16) int bb[2][kMaxWaves][4];
 };
 
@@ -433,42 +435,57 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
             wx[t] = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
             wy[t] = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
         }
-        if (in_win) {
+        /* cells per footprint side: uniform over the call (filter radius and method only) */
+        const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
+        if (in_win && cnt <= kMaxFoot) {
+            /* Straight-line rows: every lane runs cnt x cnt cells; clipped cells are redirected
+             * to the lane's private dummy words so no cell needs its own branch.  Per row: all
+             * reads, then all CAS; the rare CAS that lost a race is retried below. */
             uint64_t *row = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
+            uint64_t *const dummy = L.dummy + threadIdx.x;   /* pair q at dummy + q * kSplatBlock */
 #pragma unroll
             for (int ys = 0; ys < kMaxFoot; ++ys, row += ww) {
-                if (ys >= f.ny || f.y0 + ys < 0) continue;
-                /* one row: all reads, then all CAS; failures retry below */
+                if (ys >= cnt) break;
+                const bool rok = ys < f.ny && f.y0 + ys >= 0;
+                uint64_t *base[kMaxFoot];
+                int stride[kMaxFoot];
+                float w[kMaxFoot];
+                uint32_t okm = 0;   /* cells that are real (not redirected to the dummy) */
+#pragma unroll
+                for (int xs = 0; xs < kMaxFoot; ++xs) {
+                    const bool ok = rok && xs < f.nx && f.x0 + xs >= 0;
+                    okm |= ok ? 1u << xs : 0u;
+                    base[xs] = ok ? row + xs : dummy;
+                    stride[xs] = ok ? plane : kSplatBlock;
+                    w[xs] = wx[xs] * wy[ys];
+                }
                 uint64_t o[kMaxFoot][NP];
-                uint32_t m = 0;
 #pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs)
-                    if (xs < f.nx && f.x0 + xs >= 0) m |= 1u << xs;
+                for (int xs = 0; xs < kMaxFoot; ++xs) {
+                    if (xs >= cnt) break;
 #pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs)
-                    if (m >> xs & 1u) {
-#pragma unroll
-                        for (int q = 0; q < NP; ++q) o[xs][q] = lds_load64(row + xs + q * plane);
-                    }
+                    for (int q = 0; q < NP; ++q) o[xs][q] = lds_load64(base[xs] + q * stride[xs]);
+                }
                 uint32_t fail = 0;
 #pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs)
-                    if (m >> xs & 1u) {
-                        const float w = wx[xs] * wy[ys];
+                for (int xs = 0; xs < kMaxFoot; ++xs) {
+                    if (xs >= cnt) break;
 #pragma unroll
-                        for (int q = 0; q < NP; ++q) {
-                            const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
-                            const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
-                            if (!lds_cas64(row + xs + q * plane, o[xs][q], pair_add(o[xs][q], a0, a1)))
-                                fail |= 1u << (xs * NP + q);
-                        }
+                    for (int q = 0; q < NP; ++q) {
+                        const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w[xs];
+                        const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w[xs]) : 0.f;
+                        /* several clipped cells share the dummy word: their CAS may "fail", ignore it */
+                        if (!lds_cas64(base[xs] + q * stride[xs], o[xs][q], pair_add(o[xs][q], a0, a1)) &&
+                            (okm >> xs & 1u))
+                            fail |= 1u << (xs * NP + q);
                     }
+                }
                 while (fail) {
                     const int bit = __builtin_ctz(fail);
                     const int xs = bit / NP, q = bit - xs * NP;
-                    const float w = wx[xs] * wy[ys];
-                    const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
-                    const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
+                    const float ww_ = wx[xs] * wy[ys];
+                    const float a0 = P.box ? vals[2 * q] : vals[2 * q] * ww_;
+                    const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * ww_) : 0.f;
                     uint64_t *cp = row + xs + q * plane;
                     uint64_t e = lds_load64(cp);
                     while (!lds_cas64(cp, e, pair_add(e, a0, a1))) {}
@@ -476,16 +493,17 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
                 }
             }
         } else {
-            if (fallback) ++*fallback;
-#pragma unroll
-            for (int ys = 0; ys < kMaxFoot; ++ys) {
+            /* window miss (or a filter wider than kMaxFoot): direct global atomics */
+            if (fallback && !in_win) ++*fallback;
+            for (int ys = 0; ys < f.ny; ++ys) {
                 const int y = f.y0 + ys;
-                if (ys >= f.ny || y < 0) continue;
-#pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs) {
+                if (y < 0) continue;
+                const float wyv = ys < kMaxFoot ? wy[ys] : (P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) ys));
+                for (int xs = 0; xs < f.nx; ++xs) {
                     const int x = f.x0 + xs;
-                    if (xs >= f.nx || x < 0) continue;
-                    const float w = wx[xs] * wy[ys];
+                    if (x < 0) continue;
+                    const float wxv = xs < kMaxFoot ? wx[xs] : (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs));
+                    const float w = wxv * wyv;
                     float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
 #pragma unroll
                     for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
@@ -520,7 +538,7 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
  * thread t of part h takes lane (t % ppb) * spp + h * (spp / split) + t / ppb, so a
  * wave holds 64 different pixels (no CAS conflicts inside a wave) and the blocks of
  * a super-block write the same small film window. */
-constexpr int kSplatBlock = 512, kSplatSuper = 1024, kSplatSplit = kSplatSuper / kSplatBlock;
+constexpr int kSplatSuper = 1024, kSplatSplit = kSplatSuper / kSplatBlock;
 AD uint32_t splat_lane(const KParams &P, uint32_t &valid_n) {
     const uint32_t super = blockIdx.x / kSplatSplit, h = blockIdx.x % kSplatSplit;
     const uint32_t base = super * kSplatSuper;
