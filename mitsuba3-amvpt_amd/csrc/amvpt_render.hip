@@ -438,55 +438,61 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
         /* cells per footprint side: uniform over the call (filter radius and method only) */
         const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
         if (in_win && cnt <= kMaxFoot) {
-            /* Straight-line rows: every lane runs cnt x cnt cells; clipped cells are redirected
-             * to the lane's private dummy words so no cell needs its own branch.  Per row: all
-             * reads, then all CAS; the rare CAS that lost a race is retried below. */
-            uint64_t *row = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
+            /* Straight-line columns: every lane runs cnt x cnt cells; clipped cells are
+             * redirected to the lane's private dummy words so no cell needs its own branch.
+             * One batch = one footprint COLUMN (all reads, then all CAS): the lanes of a wave
+             * hold neighbouring pixels of one film row, whose footprints overlap only at
+             * different column offsets, so a batch never reads a word that a neighbour's CAS
+             * of the same batch changes (batching a ROW would make every such CAS fail).
+             * The CAS that lost a race against another wave is retried below. */
+            uint64_t *const col0 = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
             uint64_t *const dummy = L.dummy + threadIdx.x;   /* pair q at dummy + q * kSplatBlock */
+            uint32_t rowm = 0;
 #pragma unroll
-            for (int ys = 0; ys < kMaxFoot; ++ys, row += ww) {
-                if (ys >= cnt) break;
-                const bool rok = ys < f.ny && f.y0 + ys >= 0;
+            for (int ys = 0; ys < kMaxFoot; ++ys) rowm |= (ys < f.ny && f.y0 + ys >= 0) ? 1u << ys : 0u;
+#pragma unroll
+            for (int xs = 0; xs < kMaxFoot; ++xs) {
+                if (xs >= cnt) break;
+                const bool cok = xs < f.nx && f.x0 + xs >= 0;
                 uint64_t *base[kMaxFoot];
                 int stride[kMaxFoot];
-                float w[kMaxFoot];
                 uint32_t okm = 0;   /* cells that are real (not redirected to the dummy) */
 #pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs) {
-                    const bool ok = rok && xs < f.nx && f.x0 + xs >= 0;
-                    okm |= ok ? 1u << xs : 0u;
-                    base[xs] = ok ? row + xs : dummy;
-                    stride[xs] = ok ? plane : kSplatBlock;
-                    w[xs] = wx[xs] * wy[ys];
+                for (int ys = 0; ys < kMaxFoot; ++ys) {
+                    const bool ok = cok && (rowm >> ys & 1u);
+                    okm |= ok ? 1u << ys : 0u;
+                    base[ys] = ok ? col0 + ys * ww + xs : dummy;
+                    stride[ys] = ok ? plane : kSplatBlock;
                 }
                 uint64_t o[kMaxFoot][NP];
 #pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs) {
-                    if (xs >= cnt) break;
+                for (int ys = 0; ys < kMaxFoot; ++ys) {
+                    if (ys >= cnt) break;
 #pragma unroll
-                    for (int q = 0; q < NP; ++q) o[xs][q] = lds_load64(base[xs] + q * stride[xs]);
+                    for (int q = 0; q < NP; ++q) o[ys][q] = lds_load64(base[ys] + q * stride[ys]);
                 }
                 uint32_t fail = 0;
 #pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs) {
-                    if (xs >= cnt) break;
+                for (int ys = 0; ys < kMaxFoot; ++ys) {
+                    if (ys >= cnt) break;
+                    const float w = wx[xs] * wy[ys];
 #pragma unroll
                     for (int q = 0; q < NP; ++q) {
-                        const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w[xs];
-                        const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w[xs]) : 0.f;
+                        const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
+                        const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
                         /* several clipped cells share the dummy word: their CAS may "fail", ignore it */
-                        if (!lds_cas64(base[xs] + q * stride[xs], o[xs][q], pair_add(o[xs][q], a0, a1)) &&
-                            (okm >> xs & 1u))
-                            fail |= 1u << (xs * NP + q);
+                        if (!lds_cas64(base[ys] + q * stride[ys], o[ys][q], pair_add(o[ys][q], a0, a1)) &&
+                            (okm >> ys & 1u))
+                            fail |= 1u << (ys * NP + q);
                     }
                 }
                 while (fail) {
                     const int bit = __builtin_ctz(fail);
-                    const int xs = bit / NP, q = bit - xs * NP;
-                    const float ww_ = wx[xs] * wy[ys];
-                    const float a0 = P.box ? vals[2 * q] : vals[2 * q] * ww_;
-                    const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * ww_) : 0.f;
-                    uint64_t *cp = row + xs + q * plane;
+                    const int ys = bit / NP, q = bit - ys * NP;
+                    const float w = wx[xs] * wy[ys];
+                    const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
+                    const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
+                    uint64_t *cp = col0 + ys * ww + xs + q * plane;
                     uint64_t e = lds_load64(cp);
                     while (!lds_cas64(cp, e, pair_add(e, a0, a1))) {}
                     fail &= fail - 1u;
