@@ -64,6 +64,7 @@ def main():
     import torch.distributed as dist
 
     import amvpt
+    from amvpt import dist as adist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -77,9 +78,10 @@ def main():
     scene = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), res=args.res, spp=args.spp,
                             gx=args.gx, gy=args.gy, reuse=args.reuse)
     sd, vd, p = scene.describe(0, 0, 0)
-    spp, spp_pp, n_passes, lanes_per_pass = amvpt.plan(p)
+    plan = amvpt.plan(p)
+    spp, spp_pp, n_passes, lanes_per_pass = plan
     # pass sharding: this rank's passes are [rank*n_passes, (rank+1)*n_passes) of a world*spp frame
-    p.seed = p.seed + spp_pp * n_passes * rank
+    p = adist.pass_shard(p, rank, world, plan)
     dev = amvpt.DeviceScene(sd)
     C = 5 if p.film_alpha else 4
     film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
@@ -90,8 +92,7 @@ def main():
     def step(counters=None):
         film.zero_()
         c = dev.render(vd, p, film.data_ptr(), 0, 2 ** 64 - 1, stream, counters)
-        if world > 1:
-            dist.reduce(film, dst=0)
+        adist.reduce_film(film, dst=0)
         return c
 
     for _ in range(args.warmup):

@@ -1,0 +1,45 @@
+"""Multi-GPU partitioning of the mvpath hot path (one process per GPU).
+
+The path has no exchange step inside a frame: every lane (pixel sample) is
+independent and seeds its own sampler from its global lane index
+(TEA(seed_value, lane), mvpath.cpp:227-235), so a frame shards without any
+data-path collective.  The only collective is the final sum of the RGBW
+ImageBlocks (an RCCL reduce of the film, ImageBlock::put is additive).
+
+Two partitions are provided:
+  * pass_shard  -- weak scaling (bench.py): rank r renders the passes
+    [r * P, (r + 1) * P) of a (world * spp)-spp frame by offsetting the seed by
+    spp_per_pass * P * r -- exactly the seeds those passes get in a single
+    (world * spp)-spp render (seed_value = spp_per_pass * pass + seed).
+  * lane_shard  -- strong scaling: rank r renders lanes [begin, end) of every
+    pass of the same frame (amvpt_render's lane_begin/lane_end).
+"""
+
+
+def pass_shard(params, rank, world, plan):
+    """Params for `rank`'s share of a world * spp frame. `plan` = amvpt.plan(params)."""
+    spp, spp_pp, n_passes, _ = plan
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("rank %d outside world %d" % (rank, world))
+    if params.adaptive and world > 1:
+        raise ValueError("adaptive passes compact the whole frame: pass sharding needs adaptive = 0")
+    p = type(params).from_buffer_copy(params)
+    p.seed = params.seed + spp_pp * n_passes * rank
+    return p
+
+
+def lane_shard(n_lanes, rank, world):
+    """[begin, end) lanes of `rank` (contiguous, sizes differ by at most one)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("rank %d outside world %d" % (rank, world))
+    q, r = divmod(n_lanes, world)
+    begin = rank * q + min(rank, r)
+    return begin, begin + q + (1 if rank < r else 0)
+
+
+def reduce_film(film, dst=0):
+    """Sum the ranks' RGBW ImageBlocks on `dst` (RCCL over xGMI on GPUs, gloo on CPU)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.reduce(film, dst=dst)
+    return film

@@ -91,7 +91,7 @@ AD bool sphere_hit(const DPrim &p, const Ray &ray, float &t_out) {
         double sq = __builtin_sqrt(discrim);
         double temp = -0.5 * (B + __builtin_copysign(sq, B));
         double x0p = temp / A, x1p = C / temp;
-        /* std::min / std::max semantics, as in the oracle */
+        /* std::min / std::max operand order (NaN handling) as Dr.Jit evaluates them */
         double x0m = x1p < x0p ? x1p : x0p, x1m = x0p < x1p ? x1p : x0p;
         x0 = linear ? x0 : x0m;
         x1 = linear ? x0 : x1m;

@@ -600,6 +600,8 @@ static amvpt_params params_for(const amvpt_host_scene &S, const SensorInfo &sn, 
 /* ====================================================================== */
 
 static thread_local std::string g_host_err;
+/* shared with exr.cpp */
+void amvpt_host_set_error(const std::string &msg) { g_host_err = msg; }
 
 template <class F> static int guarded(F &&f) {
     try {

@@ -1648,5 +1648,13 @@ void oracle_microfacet_sample(uint32_t type, float au, float av, uint32_t visibl
     m_out[0] = m.x; m_out[1] = m.y; m_out[2] = m.z;
 }
 float oracle_fresnel_conductor(float ci, float er, float ei) { return fresnel_conductor(ci, er, ei); }
+/* ImageBlock::put of one sample into a W x H x C film (test_imageblock.py) */
+void oracle_film_put(uint32_t W, uint32_t H, uint32_t C, uint32_t box, float stddev, float *data, float x, float y,
+                     const float *values, uint32_t coalesce) {
+    Film f;
+    f.W = W; f.H = H; f.C = C; f.box = box != 0; f.data = data;
+    if (!f.box) f.g.init(stddev);
+    f.put({x, y}, values, true, coalesce != 0);
+}
 
 } // extern "C"

@@ -57,6 +57,17 @@ def lib():
                                                ctypes.c_void_p]
         L.oracle_fresnel_conductor.restype = ctypes.c_float
         L.oracle_fresnel_conductor.argtypes = [ctypes.c_float] * 3
+        L.oracle_film_put.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_float, ctypes.c_void_p, ctypes.c_float,
+                                                             ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32]
+        L.oracle_square_to_cosine_hemisphere.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        L.oracle_square_to_uniform_disk_concentric.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        L.oracle_sincos.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_diffuse_eval_pdf.argtypes = [ctypes.c_void_p] * 5
+        L.oracle_tea.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_tea_float32.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        L.oracle_tea_float64.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        L.oracle_pcg32_u32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_sampler_1d.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -90,6 +101,19 @@ def render(scene_desc_ptr, views_ptr, params, lane_begin=0, lane_end=2 ** 64 - 1
     if rc != 0:
         raise RuntimeError("oracle_render failed (status %d: unsupported configuration)" % rc)
     return film, rec, st.as_dict()
+
+
+def f32(*vals):
+    return np.ascontiguousarray(np.array(vals, dtype=np.float32))
+
+
+def film_put(film, x, y, values, stddev=0.5, box=False, coalesce=True):
+    """ImageBlock::put of one sample into `film` (H, W, C float32, modified in place)."""
+    H, W, C = film.shape
+    v = f32(*values)
+    lib().oracle_film_put(W, H, C, 1 if box else 0, stddev, film.ctypes.data, x, y, v.ctypes.data,
+                          1 if coalesce else 0)
+    return film
 
 
 def develop(film, alpha=False):

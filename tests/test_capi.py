@@ -1,0 +1,85 @@
+"""The drop-in boundary: both product libraries load, export every function the
+public headers declare, and fail loudly (status + message) instead of falling
+back when they cannot run.  No compute calls: these run on CPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADERS = [os.path.join(REPO, "include", h) for h in ("amvpt.h", "amvpt_host.h")]
+
+
+def declared(path):
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    names = set(re.findall(r"\b(amvpt_[a-z0-9_]+)\s*\(", src))
+    return sorted(n for n in names if not n.endswith("_t"))
+
+
+def test_headers_declare_the_boundary():
+    hip = declared(HEADERS[0])
+    for fn in ("amvpt_scene_create", "amvpt_scene_destroy", "amvpt_render", "amvpt_render_records", "amvpt_plan",
+               "amvpt_develop", "amvpt_last_error", "amvpt_abi_version"):
+        assert fn in hip
+    assert "amvpt_host_load_file" in declared(HEADERS[1])
+
+
+def test_hip_library_exports_every_declared_symbol(amvpt_mod):
+    L = amvpt_mod.hip_lib()
+    missing = [n for n in declared(HEADERS[0]) if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_host_library_exports_every_declared_symbol(amvpt_mod):
+    L = amvpt_mod.host_lib()
+    missing = [n for n in declared(HEADERS[1]) if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_abi_version_and_channels(amvpt_mod):
+    L = amvpt_mod.hip_lib()
+    assert L.amvpt_abi_version() >= 1
+    p = amvpt_mod.Params()
+    p.film_alpha = 0
+    assert L.amvpt_film_channels(ctypes.byref(p)) == 4
+    p.film_alpha = 1
+    assert L.amvpt_film_channels(ctypes.byref(p)) == 5
+
+
+def test_invalid_arguments_fail_loudly(amvpt_mod):
+    L = amvpt_mod.hip_lib()
+    h = ctypes.c_void_p()
+    assert L.amvpt_scene_create(None, ctypes.byref(h)) != 0
+    assert L.amvpt_last_error().decode()
+    p = amvpt_mod.Params()
+    rc = L.amvpt_render(None, None, ctypes.byref(p), 0, 1, None, None, None)
+    assert rc != 0 and L.amvpt_last_error().decode()
+
+
+def test_no_device_means_error_not_fallback(amvpt_mod):
+    """Without a HIP device the product path refuses (no CPU fallback exists)."""
+    if amvpt_mod.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    import amvpt
+    from conftest import SCENES
+    s = amvpt.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=8, spp=4)
+    sd, vd, p = s.describe(0, 0, 0)
+    with pytest.raises(RuntimeError):
+        amvpt.DeviceScene(sd)
+    with pytest.raises(RuntimeError):
+        amvpt.render(s)
+
+
+def test_product_modules_never_import_the_oracle():
+    """Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may use oracle/."""
+    pkg = os.path.join(REPO, "mitsuba3-amvpt_amd")
+    bad = re.compile(r"import\s+oracle|from\s+oracle|oracle_math\.h|amvpt_oracle|liboracle|oracle/")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
+                txt = open(os.path.join(root, f), errors="ignore").read()
+                assert not bad.search(txt), os.path.join(root, f)

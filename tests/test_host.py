@@ -1,0 +1,134 @@
+"""Host framework (libamvpt_host.so, CPU side of the product): sensor math
+goldens, XML loading into C-ABI descriptors, EXR I/O and error behaviour.
+Nothing here touches a GPU."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import SCENES
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_kats.json")
+
+
+@pytest.fixture(scope="module")
+def kats():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def test_parse_fov_golden(amvpt_mod, kats):
+    """src/render/tests/test_sensor.py:test01_parse_fov."""
+    for c in kats["parse_fov"]["cases"]:
+        got = amvpt_mod.parse_fov(fov=c.get("fov", 0.0), fov_axis=c.get("fov_axis"),
+                                  focal_length=c.get("focal_length"), aspect=c["aspect"])
+        assert np.isclose(got, c["expected"], rtol=1e-5, atol=1e-8), c
+    # fov_axis has no effect at aspect 1 (except diagonal)
+    for axis in ("x", "y", "smaller", "larger"):
+        assert np.isclose(amvpt_mod.parse_fov(fov=35.0, fov_axis=axis, aspect=1.0), 35.0)
+    assert np.isclose(amvpt_mod.parse_fov(focal_length="25mm", fov_axis="y", aspect=1.0), 62.923526763916016)
+
+
+def test_perspective_projection_golden(amvpt_mod, kats):
+    """src/render/tests/test_sensor.py:test02_perspective_projection."""
+    K = kats["perspective_projection"]
+    m = amvpt_mod.perspective_projection(K["film_size"], K["crop_size"], K["crop_offset"], K["fov_x"], K["near"],
+                                         K["far"])
+    assert np.allclose(m, np.array(K["matrix"], dtype=np.float32), rtol=1e-5, atol=1e-8)
+
+
+def test_parse_fov_errors(amvpt_mod):
+    with pytest.raises(RuntimeError):
+        amvpt_mod.parse_fov(fov=35.0, fov_axis="sideways", aspect=1.0)
+
+
+def test_load_cbox_grid_descriptors(amvpt_mod):
+    """scenes/cbox_grid.xml -> one grid sensor of gx*gy perspective views, mvpath params."""
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=32, spp=16, gx=4, gy=2, reuse=8)
+    assert s.sensor_count() == 1
+    w, h, c, spp = s.film_info(0)
+    assert (w, h, spp) == (32 * 4, 32 * 2, 16) and c == 3
+    sd, vd, p = s.describe(0, 0, 0)
+    assert p.integrator == amvpt_mod.INTEGRATOR_MVPATH
+    assert (p.n_views, p.grid_x, p.grid_y, p.multisensor) == (8, 4, 2, 1)
+    assert (p.film_width, p.film_height) == (128, 64)
+    assert p.max_depth == 8 and p.rr_depth == 5 and p.reuse_count == 8 and p.sa_reuse and p.sa_mis
+    assert np.isclose(p.rfilter_stddev, 0.5)
+    views = [vd[i] for i in range(p.n_views)]
+    for v in views:
+        tw = np.array(v.to_world[:], dtype=np.float64).reshape(4, 4)
+        twi = np.array(v.to_world_inv[:], dtype=np.float64).reshape(4, 4)
+        assert np.allclose(tw @ twi, np.eye(4), atol=1e-4)
+        assert tuple(v.resolution) == (32, 32)
+    # the grid spreads the camera origins: all distinct
+    origins = {tuple(np.round(np.array(v.to_world[:]).reshape(4, 4)[:3, 3], 5)) for v in views}
+    assert len(origins) == 8
+    assert sd[0].shape_count == 8 and sd[0].emitter_count == 1
+
+
+def test_xml_defaults_and_overrides(amvpt_mod):
+    """<default name=...> values and $-substitution, overridden by load-time defines (mi.load_file(**kw))."""
+    xml = """<scene version="3.0.0">
+      <default name="spp" value="8"/>
+      <default name="res" value="16"/>
+      <integrator type="path"><integer name="max_depth" value="3"/></integrator>
+      <sensor type="perspective">
+        <float name="fov" value="45"/>
+        <transform name="to_world"><lookat origin="0, 0, 4" target="0, 0, 0" up="0, 1, 0"/></transform>
+        <sampler type="independent"><integer name="sample_count" value="$spp"/></sampler>
+        <film type="hdrfilm"><integer name="width" value="$res"/><integer name="height" value="$res"/>
+          <rfilter type="box"/></film>
+      </sensor>
+      <shape type="sphere"><float name="radius" value="1"/><bsdf type="diffuse"/></shape>
+      <shape type="rectangle">
+        <transform name="to_world"><translate value="0, 3, 0"/></transform>
+        <emitter type="area"><rgb name="radiance" value="4, 4, 4"/></emitter>
+      </shape>
+    </scene>"""
+    s = amvpt_mod.load_string(xml)
+    assert s.film_info(0)[:2] == (16, 16) and s.film_info(0)[3] == 8
+    s2 = amvpt_mod.load_string(xml, spp=32, res=24)
+    assert s2.film_info(0)[:2] == (24, 24) and s2.film_info(0)[3] == 32
+    sd, vd, p = s2.describe(0, 0, 0)
+    assert p.integrator == amvpt_mod.INTEGRATOR_PATH and p.max_depth == 3 and p.rfilter == 0
+    assert "path" in s2.integrator_string().lower()
+
+
+def test_xml_errors_are_loud(amvpt_mod):
+    # environment emitters are outside the implemented path (DESIGN.md "Scope"): refused, never ignored
+    with pytest.raises(RuntimeError, match="[Ee]nvironment"):
+        amvpt_mod.load_string("<scene version='3.0.0'><emitter type='constant'/></scene>")
+    with pytest.raises(RuntimeError):
+        amvpt_mod.load_string("<scene version='3.0.0'><shape type='nosuchshape'/></scene>")
+    with pytest.raises(RuntimeError):
+        amvpt_mod.load_string("<scene version='3.0.0'><integrator type='mvpath'>")  # truncated
+    with pytest.raises(RuntimeError):
+        amvpt_mod.load_file("/nonexistent/scene.xml")
+
+
+def test_exr_round_trip(amvpt_mod, tmp_path):
+    rng = np.random.default_rng(3)
+    for c in (1, 3, 4):
+        img = rng.standard_normal((7, 11, c)).astype(np.float32)
+        img[0, 0, 0] = np.inf
+        img[1, 1, 0] = np.nan
+        path = str(tmp_path / ("t%d.exr" % c))
+        amvpt_mod.write_exr(path, img)
+        back = amvpt_mod.read_exr(path, 11, 7, c)
+        assert np.array_equal(np.isnan(back), np.isnan(img))
+        ok = ~np.isnan(img)
+        assert np.array_equal(back[ok], img[ok])
+        with open(path, "rb") as f:
+            assert f.read(4) == b"\x76\x2f\x31\x01"  # OpenEXR magic
+
+
+def test_plan_matches_oracle(amvpt_mod, oracle):
+    """amvpt_plan (C-ABI, host-only) agrees with the oracle's pass plan for several configurations."""
+    for kw in (dict(res=32, spp=16), dict(res=24, spp=64, gx=4, gy=2, reuse=8), dict(res=32, spp=12, spp_pass_lim=6),
+               dict(res=16, spp=1), dict(res=1024, spp=64, gx=4, gy=2, reuse=8)):
+        s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), **kw)
+        _, _, p = s.describe(0, 0, 0)
+        spp, spl, npass, lanes = amvpt_mod.plan(p)
+        o = oracle.plan(p)
+        assert (spp, spl, npass, lanes) == (o["spp"], o["spp_per_pass"], o["passes"], o["lanes"]), kw

@@ -1,0 +1,91 @@
+"""Multi-rank partitioning on CPU (gloo, world_size 2): the shards of
+amvpt.dist rendered by the CPU oracle and summed with a collective equal the
+single-process frame.  This is the same code path bench.py runs over RCCL
+(pass_shard + reduce_film); only the renderer (oracle on CPU instead of the
+HIP pipeline) differs."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO, SCENES
+
+CBOX = os.path.join(SCENES, "cbox_grid.xml")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, mode, out_dir):
+    import sys
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import amvpt
+    from amvpt import dist as adist
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = amvpt.load_file(CBOX, res=16, spp=16, gx=2, gy=2, reuse=4)
+        sd, vd, p = s.describe(0, 0, 0)
+        plan = amvpt.plan(p)
+        if mode == "pass":
+            pr = adist.pass_shard(p, rank, world, plan)
+            film, _, _ = O.render(sd, vd, pr, threads=2)
+        else:
+            b, e = adist.lane_shard(plan[3], rank, world)
+            film, _, _ = O.render(sd, vd, p, lane_begin=b, lane_end=e, threads=2)
+        t = torch.from_numpy(film)
+        adist.reduce_film(t, dst=0)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "film.npy"), t.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(mode, world=2):
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), mode, d), nprocs=world, join=True)
+        return np.load(os.path.join(d, "film.npy"))
+
+
+def test_lane_sharded_frame_equals_single_process(oracle, amvpt_mod):
+    got = _run("lane")
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16, gx=2, gy=2, reuse=4)
+    sd, vd, p = s.describe(0, 0, 0)
+    ref, _, _ = oracle.render(sd, vd, p, threads=4)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_pass_sharded_frame_equals_double_spp_frame(oracle, amvpt_mod):
+    """bench.py's weak scaling: 2 ranks x 16 spp == one 32-spp frame (2 passes of 16)."""
+    got = _run("pass")
+    s = amvpt_mod.load_file(CBOX, res=16, spp=32, gx=2, gy=2, reuse=4)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert amvpt_mod.plan(p)[2] == 2
+    ref, _, _ = oracle.render(sd, vd, p, threads=4)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_shard_arithmetic(amvpt_mod):
+    from amvpt import dist as adist
+    for n in (0, 1, 7, 1000, 2 ** 33 + 3):
+        for w in (1, 2, 3, 8):
+            spans = [adist.lane_shard(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(e - b for b, e in spans) - min(e - b for b, e in spans) <= 1
+    with pytest.raises(ValueError):
+        adist.lane_shard(10, 2, 2)
