@@ -31,6 +31,7 @@ for _p in (REPO, PKG):
 
 METRIC = "Msamples/sec (whole node), 8-view 1024² 64spp; per-pixel RMSE vs llvm_rgb"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CHUNK_LANES = 1 << 23  # amvpt_render's default lane chunk (g_chunk_lanes)
 
 
 def group_size(p):
@@ -139,6 +140,11 @@ def main():
     }
     dom = max(stage_ms, key=lambda k: stage_ms[k])
     achieved = bytes_stage[dom] / (stage_ms[dom] * 1e-3) / 1e9
+    kernel_name = {"primary": "k_mv_primary<%d>" % G if G > 1 else "k_raygen_single", "bounce": "k_bounce",
+                   "splat": "k_splat_multi<%d, %d>" % (G, C) if G > 1 else "k_splat_single<%d>" % C}[dom]
+    chunks = n_passes * ((lanes_per_pass + CHUNK_LANES - 1) // CHUNK_LANES)
+    launches = {"primary": chunks, "splat": chunks, "bounce": None}[dom]
+    traffic, traffic_src = pmc_traffic(kernel_name, args.res == 1024)
     # SURVEY 8(d) whole-pipeline byte model
     P = p.film_width * p.film_height
     B_sample = 336.0 * vbar + 120.0 * (G - 1) * hbar + 32.0 * P / samples_per_rank
@@ -171,12 +177,15 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {"primary": "k_mv_primary<%d>" % G, "bounce": "k_bounce", "splat": "k_splat_multi<%d>" % G}[dom],
+                "kernel": kernel_name,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": (bytes_stage[dom] // launches) if launches else None,
+                "launches_per_step": launches,
                 "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
                 "stage_bytes": bytes_stage,
                 "pipeline_model": {"B_sample": round(B_sample, 1), "vbar": round(vbar, 4), "hbar": round(hbar, 4),
@@ -190,6 +199,23 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel_name, full_size):
+    """HBM bytes per launch of `kernel_name` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_traffic.json, made by tools/pmc_traffic.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this bench at config M).  None when no summary matches."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_traffic.json")))
+    if not files or not full_size:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    key = kernel_name.replace(" ", "")
+    for k, v in d["kernels"].items():
+        if key in k.replace(" ", ""):
+            return int(v["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+    return None, os.path.relpath(files[-1], REPO)
 
 
 def cpu_baseline(sd, vd, p, target_seconds):
