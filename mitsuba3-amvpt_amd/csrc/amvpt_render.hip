@@ -308,7 +308,7 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
  * writes zeros back, so one put costs two block barriers and no zeroing pass.
  */
 constexpr int kWinW = 96, kWinH = 16, kMaxWaves = 16, kMaxFoot = 5;
-constexpr int kSplatBlock = 512;   /* threads per splat block (see splat_lane) */
+constexpr int kSplatBlock = 512;   /* threads per splat block (see slot_lane) */
 constexpr int kWinCells = kWinW * kWinH;
 template <int C> struct SplatLds {
     static constexpr int NP = (C + 1) / 2;  /* channel pairs per cell */
@@ -538,28 +538,43 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     }
 }
 
-/* Splat-kernel lane order.  Lanes are taken in super-blocks of kSplatSuper = 1024
- * (= pixels_per_super * spp); each super-block is split over kSplatSplit blocks of
- * kSplatBlock threads that take disjoint sample subsets of the same pixels:
- * thread t of part h takes lane (t % ppb) * spp + h * (spp / split) + t / ppb, so a
- * wave holds 64 different pixels (no CAS conflicts inside a wave) and the blocks of
- * a super-block write the same small film window. */
+/*
+ * Record slots.  Per-lane records (lane_out, lane_rec, view_rec planes) are stored
+ * at a SLOT, not at the lane index: lanes are grouped in super-blocks of
+ * kSplatSuper = 1024 (= pixels_per_super * spp) and slot (h * 512 + t) of a
+ * super-block holds lane (t % ppb) * spp + h * (spp / 2) + t / ppb.  The primary
+ * and raygen kernels run one thread per slot (a wave = 64 pixels of one sample:
+ * coherent camera rays) and the splat kernels read slot = blockIdx * 512 + tid
+ * (fully coalesced), so that a splat wave holds 64 different pixels (no CAS
+ * conflicts inside a wave) and the two 512-thread blocks of a super-block write
+ * the same small film window.  Partial super-blocks and non power-of-two spp
+ * use the identity map.  The map is a bijection on [0, chunk_n).
+ */
 constexpr int kSplatSuper = 1024, kSplatSplit = kSplatSuper / kSplatBlock;
-AD uint32_t splat_lane(const KParams &P, uint32_t &valid_n) {
-    const uint32_t super = blockIdx.x / kSplatSplit, h = blockIdx.x % kSplatSplit;
+AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
+    const uint32_t super = slot / (uint32_t) kSplatSuper, within = slot % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
-    const uint32_t t = threadIdx.x;
     const uint32_t remain = P.chunk_n > base ? P.chunk_n - base : 0;
     const uint32_t S = P.spp_pp;
     if (remain >= (uint32_t) kSplatSuper && P.pow2 && S >= (uint32_t) kSplatSplit && S <= (uint32_t) kSplatBlock) {
-        valid_n = kSplatBlock;
+        const uint32_t h = within / (uint32_t) kSplatBlock, t = within % (uint32_t) kSplatBlock;
         const uint32_t ppb = (uint32_t) kSplatSuper >> P.log_spp;
         return base + (t % ppb) * S + h * (S / kSplatSplit) + t / ppb;
     }
-    const uint32_t off = h * kSplatBlock;
-    const uint32_t r = remain > off ? remain - off : 0;
-    valid_n = r < (uint32_t) kSplatBlock ? r : (uint32_t) kSplatBlock;
-    return base + off + t;
+    return slot;
+}
+/* inverse of slot_lane */
+AD uint32_t lane_slot(const KParams &P, uint32_t lane) {
+    const uint32_t super = lane / (uint32_t) kSplatSuper, off = lane % (uint32_t) kSplatSuper;
+    const uint32_t base = super * kSplatSuper;
+    const uint32_t remain = P.chunk_n > base ? P.chunk_n - base : 0;
+    const uint32_t S = P.spp_pp;
+    if (remain >= (uint32_t) kSplatSuper && P.pow2 && S >= (uint32_t) kSplatSplit && S <= (uint32_t) kSplatBlock) {
+        const uint32_t half = S / kSplatSplit, ppb = (uint32_t) kSplatSuper >> P.log_spp;
+        const uint32_t p = off >> P.log_spp, smp = off & (S - 1u);
+        return base + (smp / half) * (uint32_t) kSplatBlock + (smp % half) * ppb + p;
+    }
+    return lane;
 }
 
 AD void pack_vals(const KParams &P, C3 v, float alpha, float weight, float *vals) {
@@ -651,10 +666,11 @@ AD void lane_pixel(const KParams &P, uint32_t lane, int &px, int &py) {
 }
 
 __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V, Bufs B) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool ok = i < P.chunk_n;
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = slot < P.chunk_n;
     PathState s;
     if (ok) {
+        const uint32_t i = slot_lane(P, slot);
         uint32_t lane = (uint32_t) (P.chunk_begin + i);
         int px, py;
         lane_pixel(P, lane, px, py);
@@ -669,16 +685,16 @@ __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V
         s.thr = c3(1.f); s.res = c3(0.f);
         s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
         s.prev_p = mk(0.f, 0.f, 0.f);
-        s.idx = i;
+        s.idx = slot;
         s.rng_state = rng.state;
         s.rng_seq = v1;
         if (P.max_depth == 0) {
-            B.lane_out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
             ok = false;
         }
     }
-    uint32_t slot = queue_slot(ok, B.cnt_out);
-    if (ok) store_state(B.q_out, slot, s);
+    uint32_t qslot = queue_slot(ok, B.cnt_out);
+    if (ok) store_state(B.q_out, qslot, s);
 }
 
 /* ------------------------------------------------------------------ */
@@ -768,9 +784,9 @@ template <int C>
 __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B) {
     __shared__ SplatLds<C> L;
     splat_lds_init(L);
-    uint32_t vn;
-    const uint32_t i = splat_lane(P, vn);
-    const bool ok = threadIdx.x < vn;
+    const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
+    const bool ok = slot < P.chunk_n;
+    const uint32_t i = ok ? slot_lane(P, slot) : 0u;
     float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     float putx = 0.f, puty = 0.f;
     if (ok) {
@@ -780,7 +796,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
         Pcg rng = lane_rng(P.seed_value, lane);
         float jx = rng.next_1d(), jy = rng.next_1d();
         float sx = (float) px + jx, sy = (float) py + jy;
-        float4 lo = B.lane_out[i];
+        float4 lo = B.lane_out[slot];
         bool valid = lo.w != 0.f;
         C3 spec = valid ? C3{lo.x, lo.y, lo.z} : c3(0.f);
         float alpha = valid ? 1.f : 0.f;
@@ -853,8 +869,11 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
     float *const vs = reinterpret_cast<float *>(lds + scene_lds_bytes(S)) + threadIdx.x;
 #define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    /* threads run in lane order (a wave = 4 pixels x 16 samples: coherent rays for the
+     * wave-uniform traversal); records go to the lane's slot (see slot_lane) */
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = i < P.chunk_n;
+    const uint32_t slot = ok ? lane_slot(P, i) : 0u;
     PathState ps;
     bool push = false;
     unsigned long long st_reuse = 0, st_vis = 0;
@@ -888,7 +907,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 x += (float) (xx * P.sres_x);
                 y += (float) (yy * P.sres_y);
             }
-            reinterpret_cast<float2 *>(&rec0[(size_t) k * n + i])[0] = make_float2(x, y);
+            reinterpret_cast<float2 *>(&rec0[(size_t) k * n + slot])[0] = make_float2(x, y);
         };
 #pragma unroll 1
         for (int f = 0; f < VS_FIELDS * G; ++f) vs[f * kPrimBlock] = 0.f;
@@ -1053,7 +1072,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 float n_indir = 0.f, pdf = 0.f;
 #pragma unroll 1
                 for (int k = 0; k < G; ++k) {
-                    const size_t o = (size_t) k * n + i;
+                    const size_t o = (size_t) k * n + slot;
                     /* result: emission (slot 0) + direct light through this view's BSDF value */
                     C3 res = k == 0 ? emitted : c3(0.f);
                     if (active_em && ((vflags >> k) & 1u)) res = cfma(C3{VSF(F_BR, k), VSF(F_BG, k), VSF(F_BB, k)}, emis_mis, res);
@@ -1099,7 +1118,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 ps.prev_delta = flag_delta;
                 ps.valid_ray = false;
                 ps.prev_p = si.p;
-                ps.idx = i;
+                ps.idx = slot;
                 ps.rng_state = rng.state;
                 ps.rng_seq = v1;
                 push = true;
@@ -1112,9 +1131,9 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             VSF(F_W, 0) = p_hit ? VSF(F_W, 0) : 1.f;
             vflags |= 1u;
         }
-        if (!push) B.lane_out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!push) B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
         uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) | (should_mis ? LF_MIS : 0u);
-        B.lane_rec[i] = make_float4(pdfW, bitsf(lflags), 0.f, 0.f);
+        B.lane_rec[slot] = make_float4(pdfW, bitsf(lflags), 0.f, 0.f);
         if (P.max_depth == 0) {
             /* no intersection at all: slots k >= 1 keep position 0 (+ quilt offset), slot 0 stays invalid */
 #pragma unroll 1
@@ -1123,7 +1142,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         }
 #pragma unroll 1
         for (int k = 0; k < G; ++k) {
-            const size_t o = (size_t) k * n + i;
+            const size_t o = (size_t) k * n + slot;
             uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
             reinterpret_cast<float2 *>(&rec0[o])[1] = make_float2(VSF(F_W, k), bitsf(vf));
             if (!records_done) {
@@ -1133,8 +1152,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             }
         }
     }
-    uint32_t slot = queue_slot(push, B.cnt_out);
-    if (push) store_state(B.q_out, slot, ps);
+    const uint32_t qslot = queue_slot(push, B.cnt_out);
+    if (push) store_state(B.q_out, qslot, ps);
     if (B.stats) {
         stat_add(&B.stats[1], st_reuse);
         stat_add(&B.stats[2], st_vis);
@@ -1151,12 +1170,12 @@ template <int G, int C>
 __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) {
     __shared__ SplatLds<C> L;
     splat_lds_init(L);
-    uint32_t vn;
-    const uint32_t i = splat_lane(P, vn);
-    const bool ok = threadIdx.x < vn;
+    const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
+    const bool ok = slot < P.chunk_n;
+    const uint32_t i = ok ? slot_lane(P, slot) : 0u;   /* lane (records test hook only) */
     const uint32_t n = P.chunk_n;
     float4 lr = make_float4(0.f, 0.f, 0.f, 0.f), lo = lr;
-    if (ok) { lr = B.lane_rec[i]; lo = B.lane_out[i]; }
+    if (ok) { lr = B.lane_rec[slot]; lo = B.lane_out[slot]; }
     uint32_t lflags = fbits(lr.y);
     float pdfW = lr.x;
     bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
@@ -1166,12 +1185,12 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
     float alpha = valid_ray ? 1.f : 0.f;
     C3 res0 = c3(0.f);
     if (ok && !mis) {
-        float4 r0 = B.view_rec[(size_t) G * n + i];
+        float4 r0 = B.view_rec[(size_t) G * n + slot];
         res0 = C3{r0.x, r0.y, r0.z} + indirect;
     }
     unsigned long long splats = 0, fallback = 0;
     for (int k = 0; k < G; ++k) {
-        size_t o = (size_t) k * n + i;
+        size_t o = (size_t) k * n + slot;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ok) a = B.view_rec[o];
         uint32_t vf = fbits(a.w);
@@ -1472,7 +1491,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 }
             }
             HIPCHK(hipEventRecord(ev[2], st));
-            const dim3 sgrid((uint32_t) ((cn + kSplatSuper - 1) / kSplatSuper) * kSplatSplit);
+            const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else if (G == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else kSplat[G](sgrid, st, P, B);
