@@ -233,6 +233,9 @@ amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t
 
 /* Tuning knobs (0 keeps the default). chunk_lanes bounds the lane arena per launch. */
 amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes);
+/* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane), 1 force wave-uniform,
+ * 2 force per-lane.  Results are identical in every mode (closest hit = min (t, prim)). */
+amvpt_status amvpt_set_traversal(uint32_t mode);
 
 #ifdef __cplusplus
 }

@@ -97,7 +97,7 @@ def hip_lib():
         L.amvpt_film_channels.restype = u32
         for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
                    "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
-                   "amvpt_develop", "amvpt_set_chunk_lanes"):
+                   "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal"):
             getattr(L, fn).restype = ctypes.c_int
         L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Counters)]
@@ -229,6 +229,17 @@ def plan(params):
     spp, spl, npass, lanes = u32(), u32(), u32(), u64()
     _check(L.amvpt_plan(ctypes.byref(params), spp, spl, npass, lanes), L)
     return spp.value, spl.value, npass.value, lanes.value
+
+
+def set_traversal(mode):
+    """BVH walk: 0 auto, 1 wave-uniform, 2 per-lane (amvpt_set_traversal)."""
+    L = hip_lib()
+    _check(L.amvpt_set_traversal(u32(mode)), L)
+
+
+def set_chunk_lanes(n):
+    L = hip_lib()
+    _check(L.amvpt_set_chunk_lanes(u64(n)), L)
 
 
 def device_count():

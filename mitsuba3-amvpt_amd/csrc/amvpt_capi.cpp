@@ -200,6 +200,12 @@ amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes) {
     return AMVPT_OK;
 }
 
+amvpt_status amvpt_set_traversal(uint32_t mode) {
+    if (mode > 2) { set_error("amvpt_set_traversal: mode must be 0 (auto), 1 (wave-uniform) or 2 (per-lane)"); return AMVPT_ERR_INVALID; }
+    g_traversal = mode;
+    return AMVPT_OK;
+}
+
 amvpt_status amvpt_plan(const amvpt_params *P, uint32_t *spp, uint32_t *spp_pp, uint32_t *n_passes,
                         uint64_t *lanes) {
     if (!P) { set_error("amvpt_plan: null params"); return AMVPT_ERR_INVALID; }

@@ -33,6 +33,7 @@
 namespace amvpt {
 
 uint64_t g_chunk_lanes = 1ull << 23;
+uint32_t g_traversal = 0;
 
 /* ------------------------------------------------------------------ */
 /* Parameters                                                         */
@@ -47,6 +48,7 @@ struct KParams {
     uint32_t multisensor, n_views, gx, gy, rev_x, rev_y, sres_x, sres_y;
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
+    uint32_t trav_mode;     /* amvpt_set_traversal */
     float inv_w, inv_h;
     float adapt_w;
     FilterCoeffs filt;
@@ -78,21 +80,25 @@ enum { F_PDF, F_PDFLK, F_JP, F_PDFM, F_WX, F_WY, F_WZ, F_BR, F_BG, F_BB, F_W, VS
 
 /* Small BVHs are walked wave-uniformly from global memory (scalar loads) and not
  * staged; mid-size ones are staged in LDS; large ones stay in global memory. */
-__host__ __device__ inline bool scene_staged(uint32_t n_nodes, uint32_t lds_bytes) {
-    return n_nodes > kUniformNodeLimit && lds_bytes <= kLdsSceneBytes;
+/* traversal mode (amvpt_set_traversal): 0 auto, 1 wave-uniform, 2 per-lane */
+__host__ __device__ inline bool scene_uniform(uint32_t n_nodes, uint32_t mode) {
+    return mode == 1u || (mode == 0u && n_nodes <= kUniformNodeLimit);
 }
-__host__ __device__ inline uint32_t scene_lds_bytes(const DScene &S) {
-    return scene_staged(S.n_nodes, S.lds_bytes) ? (S.lds_bytes + 15u) & ~15u : 0u;
+__host__ __device__ inline bool scene_staged(uint32_t n_nodes, uint32_t lds_bytes, uint32_t mode) {
+    return !scene_uniform(n_nodes, mode) && lds_bytes <= kLdsSceneBytes;
+}
+__host__ __device__ inline uint32_t scene_lds_bytes(const DScene &S, uint32_t mode) {
+    return scene_staged(S.n_nodes, S.lds_bytes, mode) ? (S.lds_bytes + 15u) & ~15u : 0u;
 }
 
-AD SceneRef stage_scene(const DScene &S, char *lds) {
+AD SceneRef stage_scene(const DScene &S, char *lds, uint32_t mode) {
     SceneRef sc;
     sc.g = &S;
     sc.n_nodes = S.n_nodes;
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
-    sc.uniform = S.n_nodes <= kUniformNodeLimit;
-    if (scene_staged(S.n_nodes, S.lds_bytes)) {
+    sc.uniform = scene_uniform(S.n_nodes, mode);
+    if (scene_staged(S.n_nodes, S.lds_bytes, mode)) {
         const uint32_t nn = S.n_nodes * (uint32_t) sizeof(DNode) / 16, np = S.n_prims * (uint32_t) sizeof(DPrim) / 16;
         float4 *dst = (float4 *) lds;
         const float4 *sn = (const float4 *) S.nodes, *spr = (const float4 *) S.prims;
@@ -704,7 +710,7 @@ __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V
 __global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DScene S = *Sp;
-    SceneRef sc = stage_scene(S, lds);
+    SceneRef sc = stage_scene(S, lds, P.trav_mode);
     const uint32_t count = *B.cnt_in;
     unsigned long long verts = 0;
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < count; i0 += gridDim.x * blockDim.x) {
@@ -865,9 +871,9 @@ template <int G>
 __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DScene S = *Sp;
-    SceneRef sc = stage_scene(S, lds);
+    SceneRef sc = stage_scene(S, lds, P.trav_mode);
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
-    float *const vs = reinterpret_cast<float *>(lds + scene_lds_bytes(S)) + threadIdx.x;
+    float *const vs = reinterpret_cast<float *>(lds + scene_lds_bytes(S, P.trav_mode)) + threadIdx.x;
 #define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
     /* threads run in lane order (a wave = 4 pixels x 16 samples: coherent rays for the
      * wave-uniform traversal); records go to the lane's slot (see slot_lane) */
@@ -1385,6 +1391,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.inv_w = 1.f / (float) P.W;
     P.inv_h = 1.f / (float) P.H;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
+    P.trav_mode = g_traversal;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
 
     /* views to device (tiny) */
@@ -1441,7 +1448,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     B.stats = dstats;
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
-    const size_t lds = scene_staged(scene->dev.n_nodes, scene->dev.lds_bytes) ? (scene->dev.lds_bytes + 15u) & ~15u : 0;
+    const size_t lds = scene_staged(scene->dev.n_nodes, scene->dev.lds_bytes, g_traversal) ? (scene->dev.lds_bytes + 15u) & ~15u : 0;
     hipEvent_t ev[4];
     for (auto &e : ev) HIPCHK(hipEventCreate(&e));
     float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;

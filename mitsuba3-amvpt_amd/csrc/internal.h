@@ -25,4 +25,5 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                          amvpt_counters *counters, float *records, uint32_t record_pass);
 amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream);
 extern uint64_t g_chunk_lanes;
+extern uint32_t g_traversal;
 } // namespace amvpt

@@ -127,3 +127,34 @@ def test_host_render_matches_oracle_develop(gpu_ready, amvpt_mod, oracle):
     ref = oracle.develop(ofilm)
     rmse = float(np.sqrt(np.mean((img - ref) ** 2)))
     assert rmse < 1e-5, rmse
+
+
+VEACH = os.path.join(SCENES, "veach_grid.xml")
+
+
+def test_veach_mis_g8(gpu_ready, amvpt_mod, oracle):
+    """C3 shape at reduced size: GGX rough conductors (tv_pdf MIS terms), twosided, sphere lights (f64 hit,
+    cone sampling), 8 views, reuse 8, sa_mis."""
+    s = amvpt_mod.load_file(VEACH, res=24, spp=16)
+    _check(amvpt_mod, oracle, s)
+
+
+def test_veach_fast_mis_two_passes(gpu_ready, amvpt_mod, oracle):
+    s = amvpt_mod.load_file(VEACH, res=16, spp=32, fast_mis="true")
+    _check(amvpt_mod, oracle, s, seed=3)
+
+
+def test_veach_single_view_g1(gpu_ready, amvpt_mod, oracle):
+    s = amvpt_mod.load_file(VEACH, res=24, spp=16, reuse=1)
+    _check(amvpt_mod, oracle, s)
+
+
+@pytest.mark.parametrize("scene", ["cbox", "veach"])
+def test_per_lane_traversal_matches(gpu_ready, amvpt_mod, oracle, scene):
+    """The per-lane threaded-BVH walk (large scenes) gives the same records as the oracle."""
+    amvpt_mod.set_traversal(2)
+    try:
+        s = amvpt_mod.load_file(CBOX if scene == "cbox" else VEACH, res=24, spp=16, gx=4, gy=2, reuse=8)
+        _check(amvpt_mod, oracle, s)
+    finally:
+        amvpt_mod.set_traversal(0)
