@@ -21,6 +21,7 @@
  * stream: one dwordx4 load/store per lane, 1 KiB per wave instruction).
  */
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -49,6 +50,8 @@ struct KParams {
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
     uint32_t trav_mode;     /* amvpt_set_traversal */
+    uint32_t adapt_seed;    /* adaptive pass: seed of the forked sampler (base_seed + wavefront) */
+    uint32_t pass_seed;     /* adaptive pass: seed_value of the pass whose lanes are refilled */
     float inv_w, inv_h;
     float adapt_w;
     FilterCoeffs filt;
@@ -68,6 +71,8 @@ struct Bufs {
     float *film;
     float *records;       /* optional [n][G][8] */
     unsigned long long *stats; /* [0] vertices [1] reuse lanes [2] visibility rays [3] splats */
+    uint8_t *amask;       /* adaptive: per-lane adapt_mask of the pass (lane order), or null */
+    const uint32_t *asel; /* adaptive: compacted lanes with adapt_mask (ascending) */
 };
 
 /* ------------------------------------------------------------------ */
@@ -704,6 +709,54 @@ __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V
 }
 
 /* ------------------------------------------------------------------ */
+/* Adaptive fill (mvpath_multi.h:79-115): lanes whose primary vertex had at most one
+ * indirect-valid view (adapt_mask) are compacted in lane order, each repeated n_adapt
+ * times (dr::compress + dr::repeat), re-traced from the same jittered position with
+ * sample_single using a forked sampler seeded (wavefront, wavefront), and splatted
+ * (non-coalesced) with value adapt_w * L and weight adapt_w.                        */
+/* ------------------------------------------------------------------ */
+
+/* jittered sample position of a primary lane of the pass (its first two draws) */
+AD void lane_sample_pos(const KParams &P, uint32_t lane, float &sx, float &sy) {
+    int px, py;
+    lane_pixel(P, lane, px, py);
+    Pcg rng = lane_rng(P.pass_seed, lane);
+    const float jx = rng.next_1d(), jy = rng.next_1d();
+    sx = (float) px + jx;
+    sy = (float) py + jy;
+}
+
+__global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V, Bufs B) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = slot < P.chunk_n;
+    PathState s;
+    if (ok) {
+        const uint32_t j = (uint32_t) (P.chunk_begin + slot);      /* index in the adaptive wavefront */
+        const uint32_t lane = B.asel[j / P.n_adapt];
+        float sx, sy;
+        lane_sample_pos(P, lane, sx, sy);
+        uint32_t v0, v1;
+        tea4(P.adapt_seed, j, v0, v1);
+        Pcg rng;
+        rng.seed(v0, v1);
+        uint32_t index;
+        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index);
+        s.thr = c3(1.f); s.res = c3(0.f);
+        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
+        s.prev_p = mk(0.f, 0.f, 0.f);
+        s.idx = slot;
+        s.rng_state = rng.state;
+        s.rng_seq = v1;
+        if (P.max_depth == 0) {
+            B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ok = false;
+        }
+    }
+    uint32_t qslot = queue_slot(ok, B.cnt_out);
+    if (ok) store_state(B.q_out, qslot, s);
+}
+
+/* ------------------------------------------------------------------ */
 /* k_bounce: one loop iteration (mvpath_multi.h:563-686 == mvpath_single.h:130-275) */
 /* ------------------------------------------------------------------ */
 
@@ -815,6 +868,24 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
         }
     }
     block_put<C>(P, B.film, L, 0, putx, puty, vals, ok, P.coalesce_single != 0);
+}
+
+template <int C>
+__global__ void __launch_bounds__(kSplatBlock) k_splat_adapt(KParams P, Bufs B) {
+    __shared__ SplatLds<C> L;
+    splat_lds_init(L);
+    const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
+    const bool ok = slot < P.chunk_n;
+    float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float sx = 0.f, sy = 0.f;
+    if (ok) {
+        const uint32_t j = (uint32_t) (P.chunk_begin + slot);
+        lane_sample_pos(P, B.asel[j / P.n_adapt], sx, sy);
+        const float4 lo = B.lane_out[slot];
+        const float w = P.adapt_w;
+        pack_vals(P, C3{w * lo.x, w * lo.y, w * lo.z}, 1.f, w, vals);
+    }
+    block_put<C>(P, B.film, L, 0, sx, sy, vals, ok, false);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1184,6 +1255,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
     if (ok) { lr = B.lane_rec[slot]; lo = B.lane_out[slot]; }
     uint32_t lflags = fbits(lr.y);
     float pdfW = lr.x;
+    if (ok && B.amask) B.amask[P.chunk_begin + i] = (lflags & LF_ADAPT) ? 1u : 0u;
     bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
     bool mis = (lflags & LF_MIS) != 0;
     bool adapt_mask = (lflags & LF_ADAPT) != 0;
@@ -1353,7 +1425,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const uint32_t G = reuse ? group_size(Pp) : 1;
     if (G > kMaxG) { set_error("amvpt_render: group size > 8 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
-    if (n_adapt) { set_error("amvpt_render: adaptive > 0 not implemented in this build"); return AMVPT_ERR_UNSUPPORTED; }
     if (!is_mv && n_passes > 1) { set_error("path: more than 2^32 lanes per frame"); return AMVPT_ERR_UNSUPPORTED; }
     if (Pp.multisensor && (Pp.grid_x == 0 || Pp.grid_y == 0 || Pp.film_width % Pp.grid_x || Pp.film_height % Pp.grid_y)) {
         set_error("Film size must be divisible by grid dimensions !");
@@ -1368,6 +1439,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     if (lane_begin >= lane_end) {
         if (counters) *counters = amvpt_counters{};
         return AMVPT_OK;
+    }
+    /* the adaptive fill compacts the whole pass (its RNG seeds depend on the global
+     * wavefront), so it cannot be split by lane ranges (shard by passes instead) */
+    const bool do_fill = n_adapt && !Pp.debug;
+    if (do_fill && (lane_begin != 0 || lane_end != L)) {
+        set_error("amvpt_render: adaptive > 0 needs the whole frame (lane_begin = 0, lane_end = all lanes)");
+        return AMVPT_ERR_UNSUPPORTED;
     }
 
     KParams P{};
@@ -1436,6 +1514,39 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     HIPCHK(hipMemcpyAsync(dviews, hv.data(), hv.size() * sizeof(DView), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(dstats, 0, 64, st));
 
+    /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
+    static struct AdaptArena { void *base = nullptr; size_t bytes = 0; int device = -1; } g_adapt;
+    uint8_t *d_amask = nullptr;
+    uint32_t *d_asel = nullptr, *d_anum = nullptr;
+    void *d_cub = nullptr;
+    size_t cub_bytes = 0;
+    if (do_fill) {
+        HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, cub_bytes, hipcub::CountingInputIterator<uint32_t>(0),
+                                             (const uint8_t *) nullptr, (uint32_t *) nullptr, (uint32_t *) nullptr,
+                                             (int) L, st));
+        const size_t abytes = ((L + 255) & ~(uint64_t) 255) + 4 * ((L + 63) & ~(uint64_t) 63) + 256 + cub_bytes + 256;
+        if (g_adapt.bytes < abytes || g_adapt.device != dev) {
+            if (g_adapt.base) (void) hipFree(g_adapt.base);
+            g_adapt.base = nullptr;
+            g_adapt.bytes = 0;
+            if (hipMalloc(&g_adapt.base, abytes) != hipSuccess) {
+                set_error("amvpt_render: device allocation of the adaptive buffers failed");
+                return AMVPT_ERR_OOM;
+            }
+            g_adapt.bytes = abytes;
+            g_adapt.device = dev;
+        }
+        char *ap = (char *) g_adapt.base;
+        d_amask = (uint8_t *) ap; ap += (L + 255) & ~(uint64_t) 255;
+        d_asel = (uint32_t *) ap; ap += 4 * ((L + 63) & ~(uint64_t) 63);
+        d_anum = (uint32_t *) ap; ap += 256;
+        d_cub = ap;
+    }
+    if (do_fill && L > 0x7fffffffull) {
+        set_error("amvpt_render: adaptive fill over more than 2^31 lanes per pass");
+        return AMVPT_ERR_UNSUPPORTED;
+    }
+
     Bufs B{};
     float4 *qa[6], *qb[6];
     for (int k = 0; k < 6; ++k) qa[k] = (float4 *) carve(16 * chunk);
@@ -1446,6 +1557,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     B.film = film;
     B.records = records;
     B.stats = dstats;
+    B.amask = d_amask;
+    B.asel = d_asel;
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
     const size_t lds = scene_staged(scene->dev.n_nodes, scene->dev.lds_bytes, g_traversal) ? (scene->dev.lds_bytes + 15u) & ~15u : 0;
@@ -1454,6 +1567,33 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;
     auto t0 = std::chrono::steady_clock::now();
     const uint32_t max_bounces = P.max_depth == 0xffffffffu ? 0xffffffffu : P.max_depth + 1;
+
+    /* the shared suffix (sample_suffix / sample_single loop) over the queue the raygen
+     * or primary kernel filled: one k_bounce launch per depth, ping-pong A <-> B */
+    auto run_suffix = [&](uint32_t cn) -> amvpt_status {
+        const uint32_t bgrid = std::min<uint32_t>((cn + 255) / 256, 256 * 16);
+        bool a_is_in = true;
+        for (uint32_t bnc = 0; bnc < max_bounces; ++bnc) {
+            for (int k = 0; k < 6; ++k) {
+                B.q_in[k] = a_is_in ? qa[k] : qb[k];
+                B.q_out[k] = a_is_in ? qb[k] : qa[k];
+            }
+            B.cnt_in = a_is_in ? dcnt : dcnt + 1;
+            B.cnt_out = a_is_in ? dcnt + 1 : dcnt;
+            HIPCHK(hipMemsetAsync(B.cnt_out, 0, sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_bounce, dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            HIPCHK(hipGetLastError());
+            a_is_in = !a_is_in;
+            if (bnc >= 15 && (bnc & 7) == 7) { /* unbounded depth: poll the live count */
+                uint32_t live = 0;
+                HIPCHK(hipMemcpyAsync(&live, B.cnt_out, 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                if (live == 0) break;
+            }
+        }
+        return AMVPT_OK;
+    };
+    uint64_t adaptive_lanes = 0;
 
     for (uint32_t pass = 0; pass < n_passes; ++pass) {
         P.seed_value = Pp.base_seed + (is_mv ? (spp_pp * pass + Pp.seed) : Pp.seed);
@@ -1477,26 +1617,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[1], st));
             /* suffix bounces: ping-pong A <-> B */
-            const uint32_t bgrid = std::min<uint32_t>((cn + 255) / 256, 256 * 16);
-            bool a_is_in = true;
-            for (uint32_t bnc = 0; bnc < max_bounces; ++bnc) {
-                for (int k = 0; k < 6; ++k) {
-                    B.q_in[k] = a_is_in ? qa[k] : qb[k];
-                    B.q_out[k] = a_is_in ? qb[k] : qa[k];
-                }
-                B.cnt_in = a_is_in ? dcnt : dcnt + 1;
-                B.cnt_out = a_is_in ? dcnt + 1 : dcnt;
-                HIPCHK(hipMemsetAsync(B.cnt_out, 0, sizeof(uint32_t), st));
-                hipLaunchKernelGGL(k_bounce, dim3(bgrid), dim3(256), lds, st, P, dS, B);
-                HIPCHK(hipGetLastError());
-                a_is_in = !a_is_in;
-                if (bnc >= 15 && (bnc & 7) == 7) { /* unbounded depth: poll the live count */
-                    uint32_t live = 0;
-                    HIPCHK(hipMemcpyAsync(&live, B.cnt_out, 4, hipMemcpyDeviceToHost, st));
-                    HIPCHK(hipStreamSynchronize(st));
-                    if (live == 0) break;
-                }
-            }
+            { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
             HIPCHK(hipEventRecord(ev[2], st));
             const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
@@ -1513,6 +1634,37 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 ms_primary += a; ms_bounce += b; ms_splat += c;
             }
         }
+        if (do_fill) {
+            /* compact the pass's adapt_mask lanes in lane order, then n_adapt re-traces each */
+            HIPCHK(hipcub::DeviceSelect::Flagged(d_cub, cub_bytes, hipcub::CountingInputIterator<uint32_t>(0),
+                                                 d_amask, d_asel, d_anum, (int) L, st));
+            uint32_t n_sel = 0;
+            HIPCHK(hipMemcpyAsync(&n_sel, d_anum, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            const uint64_t wf = (uint64_t) n_sel * n_adapt;
+            adaptive_lanes += wf;
+            if (wf > 0xffffffffull) { set_error("amvpt_render: adaptive wavefront over 2^32 lanes"); return AMVPT_ERR_UNSUPPORTED; }
+            KParams Ps = P;
+            P.pass_seed = P.seed_value;
+            P.adapt_seed = Pp.base_seed + (uint32_t) wf;   /* sampler->fork(); seed(wavefront, wavefront) */
+            P.record = 0;
+            for (uint64_t c0 = 0; c0 < wf; c0 += chunk) {
+                const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, wf - c0);
+                P.chunk_begin = c0;
+                P.chunk_n = cn;
+                HIPCHK(hipMemsetAsync(dcnt, 0, 2 * sizeof(uint32_t), st));
+                for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
+                B.cnt_out = dcnt; B.cnt_in = dcnt + 1;
+                hipLaunchKernelGGL(k_raygen_adapt, dim3((cn + 255) / 256), dim3(256), 0, st, P, dviews, B);
+                HIPCHK(hipGetLastError());
+                { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
+                const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
+                if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_adapt<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
+                else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_adapt<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
+                HIPCHK(hipGetLastError());
+            }
+            P = Ps;
+        }
     }
     if (counters) {
         unsigned long long hs[8] = {0};
@@ -1527,6 +1679,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.visibility_rays = hs[2];
         c.view_splats = hs[3];
         c.splat_fallback = hs[4];
+        c.adaptive_lanes = adaptive_lanes;
         c.kernel_ms_primary = ms_primary;
         c.kernel_ms_bounce = ms_bounce;
         c.kernel_ms_splat = ms_splat;

@@ -158,3 +158,30 @@ def test_per_lane_traversal_matches(gpu_ready, amvpt_mod, oracle, scene):
         _check(amvpt_mod, oracle, s)
     finally:
         amvpt_mod.set_traversal(0)
+
+
+@pytest.mark.parametrize("adaptive,extra", [(1, dict()), (3, dict(gx=4, gy=2, reuse=8, spp=32))])
+def test_adaptive_fill(gpu_ready, amvpt_mod, oracle, adaptive, extra):
+    """a13: adaptive fill (mvpath_multi.h:79-115) -- compaction in lane order, n_adapt re-traces per lane
+    with the forked (wavefront, wavefront) sampler, non-coalesced splats of weight 1/(n_adapt+1)."""
+    kw = dict(res=24, spp=16)
+    kw.update(extra)
+    s = amvpt_mod.load_file(CBOX, adaptive=adaptive, **kw)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert p.adaptive == adaptive
+    gf, of = _check(amvpt_mod, oracle, s)
+    cnt = amvpt_mod.Counters()
+    torch = _torch()
+    film = torch.zeros_like(torch.from_numpy(gf)).cuda()
+    amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), counters=cnt)
+    _, _, st = oracle.render(sd, vd, p, threads=16)
+    assert cnt.adaptive_lanes == st["adaptive_lanes"] > 0
+
+
+def test_adaptive_refuses_lane_shards(gpu_ready, amvpt_mod):
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16, adaptive=1)
+    sd, vd, p = s.describe(0, 0, 0)
+    torch = _torch()
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    with pytest.raises(RuntimeError, match="whole frame"):
+        amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), 0, 100)
