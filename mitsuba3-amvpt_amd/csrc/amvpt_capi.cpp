@@ -453,6 +453,13 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;
     D.emitter_pmf = d->emitter_count ? 1.f / (float) d->emitter_count : 0.f;
+    D.n_bsdfs = d->bsdf_count;
+    {
+        const uint32_t tb = tab_round(d->shape_count * (uint32_t) sizeof(DShape)) +
+                            tab_round(d->bsdf_count * (uint32_t) sizeof(DBsdf)) +
+                            tab_round(d->emitter_count * (uint32_t) sizeof(DEmitter));
+        D.tab_bytes = tb <= kTabBytes ? tb : 0u;
+    }
     D.lds_bytes = (uint32_t) (nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim));
     sc->n_nodes = D.n_nodes;
     sc->n_prims = (uint32_t) bprims.size();

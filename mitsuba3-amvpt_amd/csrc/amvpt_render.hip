@@ -96,26 +96,69 @@ __host__ __device__ inline uint32_t scene_lds_bytes(const DScene &S, uint32_t mo
     return scene_staged(S.n_nodes, S.lds_bytes, mode) ? (S.lds_bytes + 15u) & ~15u : 0u;
 }
 
-AD SceneRef stage_scene(const DScene &S, char *lds, uint32_t mode) {
+__host__ __device__ inline uint32_t views_lds_bytes(uint32_t n_views) {
+    const uint32_t b = n_views * (uint32_t) sizeof(DView);
+    return b <= kViewTabBytes ? tab_round(b) : 0u;
+}
+/* tables (+ views) go to LDS when both fit */
+__host__ __device__ inline bool tables_staged(const DScene &S, uint32_t n_views) {
+    return S.tab_bytes != 0 && (n_views == 0 || views_lds_bytes(n_views) != 0);
+}
+/* dynamic LDS in front of a kernel's own region: [BVH][tables][views] */
+__host__ __device__ inline uint32_t staged_lds_bytes(const DScene &S, uint32_t mode, uint32_t n_views) {
+    return scene_lds_bytes(S, mode) + (tables_staged(S, n_views) ? S.tab_bytes + views_lds_bytes(n_views) : 0u);
+}
+
+template <typename T> AD T *copy_to_lds(const T *src, uint32_t bytes, char *&dst) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized records");
+    uint32_t *d = (uint32_t *) dst;
+    const uint32_t *sp = (const uint32_t *) src;
+    for (uint32_t i = threadIdx.x; i < bytes / 4u; i += blockDim.x) d[i] = sp[i];
+    T *r = (T *) dst;
+    dst += tab_round(bytes);
+    return r;
+}
+
+/*
+ * Per-block staging (one __syncthreads): the BVH when it is walked per lane and
+ * fits (<= kLdsSceneBytes), the shape/BSDF/emitter tables when they fit
+ * (S.tab_bytes, <= kTabBytes) and the view table (<= kViewTabBytes): their
+ * lane-divergent reads then hit LDS instead of L1/L2.  S is the kernel's local
+ * copy of the scene header; its table pointers are redirected.
+ */
+template <bool kTab>
+AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0) {
     SceneRef sc;
     sc.g = &S;
     sc.n_nodes = S.n_nodes;
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
     sc.uniform = scene_uniform(S.n_nodes, mode);
+    sc.nodes = S.nodes;
+    sc.prims = S.prims;
+    char *dst = lds;
+    bool sync = false;
     if (scene_staged(S.n_nodes, S.lds_bytes, mode)) {
         const uint32_t nn = S.n_nodes * (uint32_t) sizeof(DNode) / 16, np = S.n_prims * (uint32_t) sizeof(DPrim) / 16;
-        float4 *dst = (float4 *) lds;
+        float4 *d4 = (float4 *) lds;
         const float4 *sn = (const float4 *) S.nodes, *spr = (const float4 *) S.prims;
-        for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) dst[i] = sn[i];
-        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) dst[nn + i] = spr[i];
-        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) d4[i] = sn[i];
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) d4[nn + i] = spr[i];
         sc.nodes = (const DNode *) lds;
         sc.prims = (const DPrim *) (lds + (size_t) nn * 16);
-    } else {
-        sc.nodes = S.nodes;
-        sc.prims = S.prims;
+        dst = lds + scene_lds_bytes(S, mode);
+        sync = true;
     }
+    /* compile-time choice (the host launches the kTab variant only when the tables fit),
+     * so the table pointers are known to be LDS and reads become ds_read, not flat */
+    if (kTab) {
+        S.shapes = copy_to_lds(S.shapes, S.n_shapes * (uint32_t) sizeof(DShape), dst);
+        S.bsdfs = copy_to_lds(S.bsdfs, S.n_bsdfs * (uint32_t) sizeof(DBsdf), dst);
+        S.emitters = copy_to_lds(S.emitters, S.n_emitters * (uint32_t) sizeof(DEmitter), dst);
+        if (V) *V = copy_to_lds(*V, n_views * (uint32_t) sizeof(DView), dst);
+        sync = true;
+    }
+    if (sync) __syncthreads();
     return sc;
 }
 
@@ -760,10 +803,11 @@ __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V,
 /* k_bounce: one loop iteration (mvpath_multi.h:563-686 == mvpath_single.h:130-275) */
 /* ------------------------------------------------------------------ */
 
+template <bool kTab>
 __global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    const DScene S = *Sp;
-    SceneRef sc = stage_scene(S, lds, P.trav_mode);
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<kTab>(S, lds, P.trav_mode);
     const uint32_t count = *B.cnt_in;
     unsigned long long verts = 0;
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < count; i0 += gridDim.x * blockDim.x) {
@@ -935,16 +979,23 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * View records are written as soon as each part is final:
  *   rec0[k] = (splat x, splat y, weight, flags), rec1[k] = result, rec2[k] = bsdf_val.
  */
-template <int G>
+#ifndef AMVPT_BOUNCE_TAB
+#define AMVPT_BOUNCE_TAB 1
+#endif
+#ifndef AMVPT_PRIM_TAB
+#define AMVPT_PRIM_TAB 1
+#endif
 #ifndef AMVPT_PRIM_WAVES
 #define AMVPT_PRIM_WAVES 1
 #endif
+template <int G, bool kTab>
 __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    const DScene S = *Sp;
-    SceneRef sc = stage_scene(S, lds, P.trav_mode);
+    DScene S = *Sp;
+    const uint32_t vs_off = scene_lds_bytes(S, P.trav_mode) + (kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u);
+    SceneRef sc = stage_scene<kTab>(S, lds, P.trav_mode, &V, P.n_views);
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
-    float *const vs = reinterpret_cast<float *>(lds + scene_lds_bytes(S, P.trav_mode)) + threadIdx.x;
+    float *const vs = reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
 #define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
     /* threads run in lane order (a wave = 4 pixels x 16 samples: coherent rays for the
      * wave-uniform traversal); records go to the lane's slot (see slot_lane) */
@@ -1393,9 +1444,10 @@ static Arena g_arena;
 
 template <int G>
 static void launch_primary(dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *S, const DView *V,
-                           const Bufs &B) {
+                           const Bufs &B, bool tab) {
     const size_t lds_view = (size_t) VS_FIELDS * G * kPrimBlock * sizeof(float);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G>), grid, dim3(kPrimBlock), lds + lds_view, st, P, S, V, B);
+    if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true>), grid, dim3(kPrimBlock), lds + lds_view, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false>), grid, dim3(kPrimBlock), lds + lds_view, st, P, S, V, B);
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
@@ -1403,7 +1455,7 @@ static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4>), grid, dim3(kSplatBlock), 0, st, P, B);
 }
 
-typedef void (*primary_fn)(dim3, size_t, hipStream_t, const KParams &, const DScene *, const DView *, const Bufs &);
+typedef void (*primary_fn)(dim3, size_t, hipStream_t, const KParams &, const DScene *, const DView *, const Bufs &, bool);
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
 static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>};
@@ -1561,7 +1613,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     B.asel = d_asel;
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
-    const size_t lds = scene_staged(scene->dev.n_nodes, scene->dev.lds_bytes, g_traversal) ? (scene->dev.lds_bytes + 15u) & ~15u : 0;
+    const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
+    const size_t lds = scene_lds_bytes(scene->dev, g_traversal) + (tab_b ? scene->dev.tab_bytes : 0u);   /* k_bounce */
+    const size_t lds_prim = scene_lds_bytes(scene->dev, g_traversal) +
+                            (tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u);          /* k_mv_primary */
     hipEvent_t ev[4];
     for (auto &e : ev) HIPCHK(hipEventCreate(&e));
     float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;
@@ -1581,7 +1636,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.cnt_in = a_is_in ? dcnt : dcnt + 1;
             B.cnt_out = a_is_in ? dcnt + 1 : dcnt;
             HIPCHK(hipMemsetAsync(B.cnt_out, 0, sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_bounce, dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            if (tab_b) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
             HIPCHK(hipGetLastError());
             a_is_in = !a_is_in;
             if (bnc >= 15 && (bnc & 7) == 7) { /* unbounded depth: poll the live count */
@@ -1612,7 +1668,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             if (G == 1) {
                 hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
             } else {
-                kPrimary[G](dim3((cn + kPrimBlock - 1) / kPrimBlock), lds, st, P, dS, dviews, B);
+                kPrimary[G](dim3((cn + kPrimBlock - 1) / kPrimBlock), lds_prim, st, P, dS, dviews, B, tab_p);
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[1], st));

@@ -180,48 +180,53 @@ AD void leaf_sample(const DBsdf &d, uint32_t ctx, f3 wi, float u1, float u2, BSa
 /* ---------------- dispatch incl. twosided ---------------- */
 AD uint32_t bsdf_flags(const DBsdf *T, int32_t b) { return b < 0 ? 0u : T[b].flags; }
 
+/*
+ * twosided (twosided.cpp:149-296) resolved to ONE leaf call: the leaf BSDF and the
+ * frame flip are chosen first, so each dispatch site inlines a single copy of the
+ * leaf code instead of one per twosided branch (code size: the hot kernels must
+ * fit the instruction cache).  flip: 0 none, 1 back side (negate z), 2 shared
+ * nested BSDF (|wi.z|, wo.z carries wi.z's sign).  leaf < 0: the result is zero.
+ */
+struct TwoSided { int32_t leaf; uint32_t flip; };
+AD TwoSided resolve_twosided(const DBsdf *T, int32_t b, f3 wi) {
+    const DBsdf &d = T[b];
+    if (d.type != BSDF_TWOSIDED) return TwoSided{b, 0u};
+    if (d.nested0 == d.nested1) return TwoSided{d.nested0, 2u};
+    if (wi.z > 0.f) return TwoSided{d.nested0, 0u};
+    if (wi.z < 0.f) return TwoSided{d.nested1, 1u};
+    return TwoSided{-1, 0u};   /* wi.z == 0 or NaN: neither side */
+}
+AD f3 ts_wi(const TwoSided &r, f3 wi) {
+    return r.flip == 1u ? mk(wi.x, wi.y, -wi.z) : (r.flip == 2u ? mk(wi.x, wi.y, fabs_(wi.z)) : wi);
+}
+AD f3 ts_wo(const TwoSided &r, f3 wi, f3 wo) {
+    return r.flip == 1u ? mk(wo.x, wo.y, -wo.z) : (r.flip == 2u ? mk(wo.x, wo.y, mulsign(wo.z, wi.z)) : wo);
+}
+
 AD void bsdf_eval_pdf(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, f3 wo, bool active, C3 &val, float &pdf) {
     val = c3(0.f); pdf = 0.f;
     if (b < 0 || !active) return;
-    const DBsdf &d = T[b];
-    if (d.type != BSDF_TWOSIDED) { leaf_eval_pdf(d, ctx, wi, wo, val, pdf); return; }
-    if (d.nested0 == d.nested1) {
-        f3 wo2 = mk(wo.x, wo.y, mulsign(wo.z, wi.z)), wi2 = mk(wi.x, wi.y, fabs_(wi.z));
-        leaf_eval_pdf(T[d.nested0], ctx, wi2, wo2, val, pdf);
-        return;
-    }
-    if (wi.z > 0.f) leaf_eval_pdf(T[d.nested0], ctx, wi, wo, val, pdf);
-    if (wi.z < 0.f) leaf_eval_pdf(T[d.nested1], ctx, mk(wi.x, wi.y, -wi.z), mk(wo.x, wo.y, -wo.z), val, pdf);
+    const TwoSided r = resolve_twosided(T, b, wi);
+    if (r.leaf < 0) return;
+    leaf_eval_pdf(T[r.leaf], ctx, ts_wi(r, wi), ts_wo(r, wi, wo), val, pdf);
 }
 
 AD float bsdf_pdf(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, f3 wo, bool active) {
     if (b < 0 || !active) return 0.f;
-    const DBsdf &d = T[b];
-    if (d.type != BSDF_TWOSIDED) return leaf_pdf(d, ctx, wi, wo);
-    if (d.nested0 == d.nested1)
-        return leaf_pdf(T[d.nested0], ctx, mk(wi.x, wi.y, fabs_(wi.z)), mk(wo.x, wo.y, mulsign(wo.z, wi.z)));
-    float r = 0.f;
-    if (wi.z > 0.f) r = leaf_pdf(T[d.nested0], ctx, wi, wo);
-    if (wi.z < 0.f) r = leaf_pdf(T[d.nested1], ctx, mk(wi.x, wi.y, -wi.z), mk(wo.x, wo.y, -wo.z));
-    return r;
+    const TwoSided r = resolve_twosided(T, b, wi);
+    if (r.leaf < 0) return 0.f;
+    return leaf_pdf(T[r.leaf], ctx, ts_wi(r, wi), ts_wo(r, wi, wo));
 }
 
 AD void bsdf_sample(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, float u1, float u2, bool active, BSample &bs,
                     C3 &w) {
     bs = bs_zero(); w = c3(0.f);
     if (b < 0 || !active) return;
-    const DBsdf &d = T[b];
-    if (d.type != BSDF_TWOSIDED) { leaf_sample(d, ctx, wi, u1, u2, bs, w); return; }
-    if (d.nested0 == d.nested1) {
-        leaf_sample(T[d.nested0], ctx, mk(wi.x, wi.y, fabs_(wi.z)), u1, u2, bs, w);
-        bs.wo.z = mulsign(bs.wo.z, wi.z);
-        return;
-    }
-    if (wi.z > 0.f) leaf_sample(T[d.nested0], ctx, wi, u1, u2, bs, w);
-    if (wi.z < 0.f) {
-        leaf_sample(T[d.nested1], ctx, mk(wi.x, wi.y, -wi.z), u1, u2, bs, w);
-        bs.wo.z *= -1.f;
-    }
+    const TwoSided r = resolve_twosided(T, b, wi);
+    if (r.leaf < 0) return;
+    leaf_sample(T[r.leaf], ctx, ts_wi(r, wi), u1, u2, bs, w);
+    if (r.flip == 1u) bs.wo.z *= -1.f;
+    if (r.flip == 2u) bs.wo.z = mulsign(bs.wo.z, wi.z);
 }
 
 AD float leaf_roughness(const DBsdf &d) {

@@ -77,6 +77,10 @@ struct DView {
     float res[2], pp[2];
 };
 
+/* Small material/shape/emitter/view tables are copied to LDS by every kernel. */
+constexpr uint32_t kTabBytes = 8192, kViewTabBytes = 8192;
+inline __host__ __device__ uint32_t tab_round(uint32_t b) { return (b + 15u) & ~15u; }
+
 struct DScene {
     const DNode *nodes;
     const DPrim *prims;
@@ -90,6 +94,8 @@ struct DScene {
     uint32_t n_nodes, n_prims, n_shapes, n_emitters;
     float emitter_pmf;
     uint32_t lds_bytes;     /* nodes+prims footprint (LDS staging when small) */
+    uint32_t n_bsdfs;
+    uint32_t tab_bytes;     /* shapes+bsdfs+emitters footprint if <= kTabBytes (staged in LDS), else 0 */
 };
 
 } // namespace amvpt
