@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 1
+#define AMVPT_ABI_VERSION 2
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -162,6 +162,9 @@ typedef struct amvpt_params {
     uint32_t film_alpha;     /* 1 -> RGBAW (5 channels), 0 -> RGBW */
     uint32_t rfilter;        /* AMVPT_RFILTER_* */
     float rfilter_stddev;    /* gaussian stddev (radius = 4*stddev) */
+    /* MultiSensor layout: 0 grid (grid.cpp:268-297), 1 batch (batch.cpp:163-181:
+     * a horizontal strip, grid_y = 1, index clamped before reverse_x) */
+    uint32_t batch;
 } amvpt_params;
 
 /* Per-render counters (device-side lane statistics; SURVEY 8(d) byte model). */

@@ -46,7 +46,7 @@ struct KParams {
     uint32_t max_depth, rr_depth;
     uint32_t sa_mis, fast_mis, debug, n_adapt;
     uint32_t G;
-    uint32_t multisensor, n_views, gx, gy, rev_x, rev_y, sres_x, sres_y;
+    uint32_t multisensor, batch, n_views, gx, gy, rev_x, rev_y, sres_x, sres_y;
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
     uint32_t trav_mode;     /* amvpt_set_traversal */
@@ -242,6 +242,14 @@ AD Ray persp_sample_ray(const DView &v, float x, float y) {
 /* GridSensor::sample_ray_idx (grid.cpp:269-297) */
 AD Ray sample_ray_idx(const KParams &P, const DView *V, float ax, float ay, uint32_t &index) {
     if (!P.multisensor) { index = 0; return persp_sample_ray(V[0], ax, ay); }
+    if (P.batch) {
+        /* BatchSensor::sample_ray_idx (batch.cpp:163-181): clamp, then reverse_x */
+        const float fx = ax * (float) P.n_views;
+        const uint32_t ux = (uint32_t) fx;
+        index = min(ux, P.n_views - 1);
+        if (P.rev_x) index = (P.n_views - 1) - index;
+        return persp_sample_ray(V[index], fx - (float) ux, ay);
+    }
     float fx = ax * (float) P.gx, fy = ay * (float) P.gy;
     uint32_t ux = (uint32_t) fx, uy = (uint32_t) fy;
     uint32_t ix = ux, iy = uy;
@@ -803,8 +811,11 @@ __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V,
 /* k_bounce: one loop iteration (mvpath_multi.h:563-686 == mvpath_single.h:130-275) */
 /* ------------------------------------------------------------------ */
 
+#ifndef AMVPT_BOUNCE_WAVES
+#define AMVPT_BOUNCE_WAVES 4
+#endif
 template <bool kTab>
-__global__ void __launch_bounds__(256) k_bounce(KParams P, const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<kTab>(S, lds, P.trav_mode);
@@ -1510,7 +1521,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.max_depth = Pp.max_depth; P.rr_depth = Pp.rr_depth;
     P.sa_mis = Pp.sa_mis; P.fast_mis = Pp.fast_mis; P.debug = Pp.debug; P.n_adapt = n_adapt;
     P.G = G;
-    P.multisensor = Pp.multisensor; P.n_views = Pp.n_views;
+    P.multisensor = Pp.multisensor; P.batch = Pp.batch; P.n_views = Pp.n_views;
     P.gx = Pp.grid_x ? Pp.grid_x : 1; P.gy = Pp.grid_y ? Pp.grid_y : 1;
     P.rev_x = Pp.reverse_x; P.rev_y = Pp.reverse_y;
     P.sres_x = P.W / P.gx; P.sres_y = P.H / P.gy;

@@ -198,6 +198,7 @@ static amvpt_view_desc make_perspective_view(const Properties &p, const Transfor
 
 struct SensorInfo {
     bool multisensor = false;
+    bool batch = false;
     uint32_t gx = 1, gy = 1;
     bool rev_x = false, rev_y = false;
     FilmInfo film;           /* quilt film */
@@ -216,7 +217,43 @@ static SensorInfo make_sensor(const Object &o) {
                                                 (float) p.get_float("lens_shift", 0.0)));
         return s;
     }
-    if (t != "grid") Throw("Sensor \"" + p.plugin + "\" is not implemented (perspective, grid)");
+    if (t == "batch") {
+        /* BatchSensor (batch.cpp:94-131): child sensors side by side on one film */
+        s.multisensor = true;
+        s.batch = true;
+        s.rev_x = p.get_bool("reverse_x", false);
+        s.rev_y = p.get_bool("reverse_y", false);
+        std::vector<const Object *> kids;
+        for (auto &e : p.entries) {
+            if (e.second.kind != Properties::Obj) continue;
+            const Object &c = *e.second.o;
+            if (c.tag == "sensor") kids.push_back(&c);
+            else if (c.tag == "shape")
+                Throw("BatchSensor: shapes can only be specified as children if a sensor is associated with them!");
+        }
+        if (kids.empty()) Throw("BatchSensor: at least one child sensor must be specified!");
+        const uint32_t n = (uint32_t) kids.size(), sub = s.film.w / n;
+        if (sub * n != s.film.w)
+            Throw("BatchSensor: the horizontal resolution (currently " + std::to_string(s.film.w) +
+                  ") must be divisible by the number of child sensors (" + std::to_string(n) + ")!");
+        s.gx = n;
+        s.gy = 1;
+        for (const Object *c : kids) {
+            const Properties &cp = c->props;
+            std::string ct = lower(cp.plugin);
+            if (ct != "perspective" && ct != "thinlens") Throw("Sensor \"" + cp.plugin + "\" is not implemented (perspective)");
+            /* the child computes its fov from ITS OWN film at construction, then the batch
+             * resizes that film to (sub, h) and rebuilds the projection (batch.cpp:122-126) */
+            FilmInfo cf;
+            SamplerInfo cs;
+            sensor_parts(cp, cf, cs);
+            const double x_fov = parse_fov(cp, (double) cf.w / (double) cf.h);
+            s.views.push_back(make_perspective_view(cp, cp.get_transform("to_world"), sub, s.film.h, x_fov, true,
+                                                    (float) cp.get_float("lens_shift", 0.0)));
+        }
+        return s;
+    }
+    if (t != "grid") Throw("Sensor \"" + p.plugin + "\" is not implemented (perspective, grid, batch)");
     /* GridSensor (grid.cpp:84-236) */
     s.multisensor = true;
     s.rev_x = p.get_bool("reverse_x", false);
@@ -584,6 +621,7 @@ static amvpt_params params_for(const amvpt_host_scene &S, const SensorInfo &sn, 
     p.grid_x = sn.gx;
     p.grid_y = sn.gy;
     p.reverse_x = sn.rev_x;
+    p.batch = sn.batch ? 1u : 0u;
     p.reverse_y = sn.rev_y;
     p.film_width = sn.film.w;
     p.film_height = sn.film.h;

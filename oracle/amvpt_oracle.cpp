@@ -21,6 +21,7 @@
  *   render_sample / sample_single                  src/integrators/mvpath_single.h:50-278
  *   tv_pdf / tv_pdf_fast / mis_weight / sensors_visible  mvpath.h:243-311
  *   GridSensor::sample_ray_idx                     src/sensors/grid.cpp:269-297
+ *   BatchSensor::sample_ray_idx                    src/sensors/batch.cpp:163-181
  *   PerspectiveCamera::sample_ray / sample_surface src/sensors/perspective.cpp:205-241,327-385
  *   PCG32Sampler::seed / IndependentSampler        src/render/sampler.cpp:125-144, independent.cpp:77-97
  *   sample_tea_32                                  include/mitsuba/core/random.h:77-90
@@ -918,6 +919,14 @@ struct Renderer {
         if (!P.multisensor) {
             index = 0;
             return persp_sample_ray(views[0], pos01);
+        }
+        if (P.batch) {
+            /* BatchSensor::sample_ray_idx (batch.cpp:163-181): clamp, then reverse_x */
+            float idx_f = pos01.x * (float) P.n_views;
+            uint32_t idx_u = (uint32_t) idx_f;
+            index = std::min(idx_u, P.n_views - 1);
+            if (P.reverse_x) index = (P.n_views - 1) - index;
+            return persp_sample_ray(views[index], V2{idx_f - (float) idx_u, pos01.y});
         }
         float gx = (float) P.grid_x, gy = (float) P.grid_y;
         V2 idx_f{pos01.x * gx, pos01.y * gy};

@@ -185,3 +185,13 @@ def test_adaptive_refuses_lane_shards(gpu_ready, amvpt_mod):
     film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
     with pytest.raises(RuntimeError, match="whole frame"):
         amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), 0, 100)
+
+
+BATCH = os.path.join(SCENES, "cbox_batch.xml")
+
+
+@pytest.mark.parametrize("rev", ["false", "true"])
+def test_batch_sensor(gpu_ready, amvpt_mod, oracle, rev):
+    """`batch` MultiSensor (batch.cpp:163-181): strip layout, clamp-then-reverse view index."""
+    s = amvpt_mod.load_file(BATCH, res=24, width=96, spp=16, rev=rev)
+    _check(amvpt_mod, oracle, s)

@@ -132,3 +132,13 @@ def test_plan_matches_oracle(amvpt_mod, oracle):
         spp, spl, npass, lanes = amvpt_mod.plan(p)
         o = oracle.plan(p)
         assert (spp, spl, npass, lanes) == (o["spp"], o["spp_per_pass"], o["passes"], o["lanes"]), kw
+
+
+def test_batch_sensor_loading(amvpt_mod):
+    """batch.cpp:94-131: children side by side, horizontal resolution divisible by the child count."""
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_batch.xml"), res=32, width=128, spp=16)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert (p.batch, p.multisensor, p.n_views, p.grid_x, p.grid_y) == (1, 1, 4, 4, 1)
+    assert all(tuple(vd[i].resolution) == (32, 32) for i in range(4))
+    with pytest.raises(RuntimeError, match="divisible"):
+        amvpt_mod.load_file(os.path.join(SCENES, "cbox_batch.xml"), res=32, width=130, spp=16)
