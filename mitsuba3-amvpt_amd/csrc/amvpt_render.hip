@@ -47,6 +47,7 @@ struct KParams {
     uint32_t sa_mis, fast_mis, debug, n_adapt;
     uint32_t G;
     uint32_t multisensor, batch, n_views, gx, gy, rev_x, rev_y, sres_x, sres_y;
+    uint32_t needs_ap;      /* Sensor::needs_aperture_sample: thin-lens views draw a 2-D aperture sample */
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
     uint32_t trav_mode;     /* amvpt_set_traversal */
@@ -240,15 +241,37 @@ AD Ray persp_sample_ray(const DView &v, float x, float y) {
 }
 
 /* GridSensor::sample_ray_idx (grid.cpp:269-297) */
-AD Ray sample_ray_idx(const KParams &P, const DView *V, float ax, float ay, uint32_t &index) {
-    if (!P.multisensor) { index = 0; return persp_sample_ray(V[0], ax, ay); }
+/* ThinLensCamera::sample_ray (thinlens.cpp:220-257); ap = the lane's aperture sample */
+AD Ray thin_sample_ray(const DView &v, float x, float y, float apx, float apy) {
+    f3 near_p = xf_point(v.sample_to_camera, mk(x, y, 0.f));
+    float tx, ty;
+    disk_concentric(apx, apy, tx, ty);
+    const f3 aperture_p = mk(v.aperture_radius * tx, v.aperture_radius * ty, 0.f);
+    const f3 focus_p = near_p * (v.focus_distance / near_p.z);
+    const f3 d = normalize(focus_p - aperture_p);
+    Ray r;
+    r.o = xf_point_affine(v.to_world, aperture_p);
+    r.d = xf_vector(v.to_world, d);
+    float inv_z = rcp(d.z);
+    float near_t = v.near_clip * inv_z, far_t = v.far_clip * inv_z;
+    r.o = r.o + r.d * near_t;
+    r.maxt = far_t - near_t;
+    return r;
+}
+AD Ray camera_sample_ray(const DView &v, float x, float y, float apx, float apy) {
+    return v.type == AMVPT_CAMERA_THINLENS ? thin_sample_ray(v, x, y, apx, apy) : persp_sample_ray(v, x, y);
+}
+
+AD Ray sample_ray_idx(const KParams &P, const DView *V, float ax, float ay, uint32_t &index, float apx = .5f,
+                      float apy = .5f) {
+    if (!P.multisensor) { index = 0; return camera_sample_ray(V[0], ax, ay, apx, apy); }
     if (P.batch) {
         /* BatchSensor::sample_ray_idx (batch.cpp:163-181): clamp, then reverse_x */
         const float fx = ax * (float) P.n_views;
         const uint32_t ux = (uint32_t) fx;
         index = min(ux, P.n_views - 1);
         if (P.rev_x) index = (P.n_views - 1) - index;
-        return persp_sample_ray(V[index], fx - (float) ux, ay);
+        return camera_sample_ray(V[index], fx - (float) ux, ay, apx, apy);
     }
     float fx = ax * (float) P.gx, fy = ay * (float) P.gy;
     uint32_t ux = (uint32_t) fx, uy = (uint32_t) fy;
@@ -257,7 +280,7 @@ AD Ray sample_ray_idx(const KParams &P, const DView *V, float ax, float ay, uint
     if (P.rev_y) iy = (P.gy - 1) - iy;
     index = ix + P.gx * iy;
     index = min(index, P.n_views - 1);
-    return persp_sample_ray(V[index], fx - (float) ux, fy - (float) uy);
+    return camera_sample_ray(V[index], fx - (float) ux, fy - (float) uy, apx, apy);
 }
 
 struct Surf { f3 p, d; float uvx, uvy, pdf, Jp; bool face, valid; };
@@ -289,6 +312,45 @@ AD Surf persp_sample_surface(const DView &v, const SI &it, bool active) {
     r.Jp = (cts * inv_dist * inv_dist) * r.pdf;
     r.valid = a;
     return r;
+}
+
+/* ThinLensCamera::sample_surface (thinlens.cpp:358-418), JIT semantics */
+AD Surf thin_sample_surface(const DView &v, const SI &it, bool active, float apx, float apy) {
+    Surf r;
+    r.p = mk(0.f, 0.f, 0.f); r.d = mk(0.f, 0.f, 0.f);
+    r.uvx = r.uvy = r.pdf = r.Jp = 0.f;
+    r.face = false; r.valid = false;
+    if (!active) return r;
+    const f3 ref_p = xf_point_affine(v.to_world_inv, it.p);
+    bool a = ref_p.z >= v.near_clip && ref_p.z <= v.far_clip;
+    float tx, ty;
+    disk_concentric(apx, apy, tx, ty);
+    const f3 aperture_p = mk(tx * v.aperture_radius, ty * v.aperture_radius, 0.f);
+    f3 local_d = ref_p - aperture_p;
+    const float dist = norm(local_d), inv_dist = rcp(dist);
+    local_d = local_d * inv_dist;
+    const float ictf = rcp(local_d.z), ictf3 = ictf * ictf * ictf;
+    const float inv_f = 1.f / v.focus_distance;
+    const f3 film_plane = mk(aperture_p.x * inv_f + local_d.x / local_d.z, aperture_p.y * inv_f + local_d.y / local_d.z,
+                             aperture_p.z * inv_f + local_d.z / local_d.z);
+    const f3 scr = xf_point_affine(v.camera_to_sample, film_plane);
+    a = a && scr.x >= 0.f && scr.y >= 0.f && scr.x <= 1.f && scr.y <= 1.f;
+    const float pdf_lens = rcp(sqr(v.aperture_radius) * kPi);
+    r.pdf = pdf_lens * (v.normalization * ictf3);
+    r.uvx = scr.x * v.res[0];
+    r.uvy = scr.y * v.res[1];
+    r.p = xf_point_affine(v.to_world, aperture_p);
+    r.d = (r.p - it.p) * inv_dist;
+    float cts = dot(r.d, it.n);
+    r.face = cts > 0.f;
+    cts = fabs_(cts);
+    r.Jp = (cts * inv_dist * inv_dist) * r.pdf;
+    r.valid = a;
+    return r;
+}
+AD Surf camera_sample_surface(const DView &v, const SI &it, bool active, float apx, float apy) {
+    return v.type == AMVPT_CAMERA_THINLENS ? thin_sample_surface(v, it, active, apx, apy)
+                                           : persp_sample_surface(v, it, active);
 }
 
 /* ------------------------------------------------------------------ */
@@ -742,8 +804,10 @@ __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V
         rng.seed(v0, v1);
         float jx = rng.next_1d(), jy = rng.next_1d();
         float sx = (float) px + jx, sy = (float) py + jy;
+        float apx = .5f, apy = .5f;
+        if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
         uint32_t index;
-        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index);
+        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
         s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
         s.prev_p = mk(0.f, 0.f, 0.f);
@@ -768,13 +832,15 @@ __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V
 /* ------------------------------------------------------------------ */
 
 /* jittered sample position of a primary lane of the pass (its first two draws) */
-AD void lane_sample_pos(const KParams &P, uint32_t lane, float &sx, float &sy) {
+AD void lane_sample_pos(const KParams &P, uint32_t lane, float &sx, float &sy, float &apx, float &apy) {
     int px, py;
     lane_pixel(P, lane, px, py);
     Pcg rng = lane_rng(P.pass_seed, lane);
     const float jx = rng.next_1d(), jy = rng.next_1d();
     sx = (float) px + jx;
     sy = (float) py + jy;
+    apx = apy = .5f;
+    if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }   /* nested_gather(aperture_sample) */
 }
 
 __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V, Bufs B) {
@@ -784,14 +850,14 @@ __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V,
     if (ok) {
         const uint32_t j = (uint32_t) (P.chunk_begin + slot);      /* index in the adaptive wavefront */
         const uint32_t lane = B.asel[j / P.n_adapt];
-        float sx, sy;
-        lane_sample_pos(P, lane, sx, sy);
+        float sx, sy, apx, apy;
+        lane_sample_pos(P, lane, sx, sy, apx, apy);
         uint32_t v0, v1;
         tea4(P.adapt_seed, j, v0, v1);
         Pcg rng;
         rng.seed(v0, v1);
         uint32_t index;
-        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index);
+        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
         s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
         s.prev_p = mk(0.f, 0.f, 0.f);
@@ -935,7 +1001,8 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_adapt(KParams P, Bufs B) 
     float sx = 0.f, sy = 0.f;
     if (ok) {
         const uint32_t j = (uint32_t) (P.chunk_begin + slot);
-        lane_sample_pos(P, B.asel[j / P.n_adapt], sx, sy);
+        float apx, apy;
+        lane_sample_pos(P, B.asel[j / P.n_adapt], sx, sy, apx, apy);
         const float4 lo = B.lane_out[slot];
         const float w = P.adapt_w;
         pack_vals(P, C3{w * lo.x, w * lo.y, w * lo.z}, 1.f, w, vals);
@@ -1027,8 +1094,10 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         rng.seed(v0, v1);
         float jx = rng.next_1d(), jy = rng.next_1d();
         float sx = (float) px + jx, sy = (float) py + jy;
+        float apx = .5f, apy = .5f;   /* aperture sample: raygen and every view's sample_surface */
+        if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
         uint32_t p_idx;
-        Ray pray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), p_idx);
+        Ray pray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), p_idx, apx, apy);
         const uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u);
         float4 *const rec0 = B.view_rec, *const rec1 = B.view_rec + (size_t) G * n,
                       *const rec2 = B.view_rec + (size_t) 2 * G * n;
@@ -1099,7 +1168,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 bd.reuse = reuse;
                 VSF(F_BR, 0) = bsdf_val.r; VSF(F_BG, 0) = bsdf_val.g; VSF(F_BB, 0) = bsdf_val.b;
                 /* ---- camera_selection (mvpath_multi.h:371-464) ---- */
-                Surf p0 = persp_sample_surface(V[view_of(0)], si, p_hit);
+                Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
                 VSF(F_PDF, 0) = pdf0; VSF(F_PDFLK, 0) = pdf0; VSF(F_JP, 0) = Jp0;
                 VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
@@ -1111,7 +1180,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 float n_direct = 1.f, n_indir = 2.f;
 #pragma unroll 1
                 for (int k = 1; k < G; ++k) {
-                    Surf r = persp_sample_surface(V[view_of(k)], si, bd.reuse);
+                    Surf r = camera_sample_surface(V[view_of(k)], si, bd.reuse, apx, apy);
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
@@ -1191,7 +1260,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 vflags |= p_hit ? 1u : 0u;
 #pragma unroll 1
                 for (int k = 1; k < G; ++k) {
-                    Surf r = persp_sample_surface(V[view_of(k)], si, reuse);
+                    Surf r = camera_sample_surface(V[view_of(k)], si, reuse, apx, apy);
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
@@ -1494,9 +1563,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         return AMVPT_ERR_INVALID;
     }
     for (uint32_t v = 0; v < Pp.n_views; ++v)
-        if (views[v].type != AMVPT_CAMERA_PERSPECTIVE) {
-            set_error("amvpt_render: thinlens sub-sensors not implemented in this build");
-            return AMVPT_ERR_UNSUPPORTED;
+        if (views[v].type != AMVPT_CAMERA_PERSPECTIVE && views[v].type != AMVPT_CAMERA_THINLENS) {
+            set_error("amvpt_render: unknown camera type");
+            return AMVPT_ERR_INVALID;
         }
     if (lane_end > L) lane_end = L;
     if (lane_begin >= lane_end) {
@@ -1522,6 +1591,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.sa_mis = Pp.sa_mis; P.fast_mis = Pp.fast_mis; P.debug = Pp.debug; P.n_adapt = n_adapt;
     P.G = G;
     P.multisensor = Pp.multisensor; P.batch = Pp.batch; P.n_views = Pp.n_views;
+    /* grid: its first sub-sensor decides (grid.cpp:228); batch: any child (batch.cpp:127) */
+    P.needs_ap = 0;
+    for (uint32_t v = 0; v < (Pp.multisensor && Pp.batch ? Pp.n_views : 1u); ++v)
+        P.needs_ap |= views[v].type == AMVPT_CAMERA_THINLENS ? 1u : 0u;
     P.gx = Pp.grid_x ? Pp.grid_x : 1; P.gy = Pp.grid_y ? Pp.grid_y : 1;
     P.rev_x = Pp.reverse_x; P.rev_y = Pp.reverse_y;
     P.sres_x = P.W / P.gx; P.sres_y = P.H / P.gy;
@@ -1547,6 +1620,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         o.near_clip = d.near_clip; o.far_clip = d.far_clip; o.normalization = d.normalization; o.pad0 = 0.f;
         o.res[0] = d.resolution[0]; o.res[1] = d.resolution[1];
         o.pp[0] = d.pp_offset[0]; o.pp[1] = d.pp_offset[1];
+        o.type = d.type;
+        o.aperture_radius = d.aperture_radius;
+        o.focus_distance = d.focus_distance;
+        o.pad1 = 0.f;
     }
 
     /* lane arena: queues (2 x 6 x 16 B) + lane_out/lane_rec (32 B) + view records (48 B x G) */

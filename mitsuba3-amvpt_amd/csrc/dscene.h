@@ -75,6 +75,8 @@ struct DView {
     float camera_to_sample[16];
     float near_clip, far_clip, normalization, pad0;
     float res[2], pp[2];
+    uint32_t type;          /* AMVPT_CAMERA_PERSPECTIVE / _THINLENS */
+    float aperture_radius, focus_distance, pad1;
 };
 
 /* Small material/shape/emitter/view tables are copied to LDS by every kernel. */

@@ -193,6 +193,11 @@ static amvpt_view_desc make_perspective_view(const Properties &p, const Transfor
     v.pp_offset[1] = (float) h * ppy / (float) h;
     v.focus_distance = (float) p.get_float("focus_distance", far_clip);
     v.aperture_radius = (float) p.get_float("aperture_radius", 0.0);
+    if (v.type == AMVPT_CAMERA_THINLENS) {
+        /* thinlens.cpp:156-162 */
+        if (!p.has("aperture_radius")) Throw("Property \"aperture_radius\" has not been specified!");
+        if (v.aperture_radius == 0.f) v.aperture_radius = 5.9604645e-8f; /* dr::Epsilon<float> */
+    }
     return v;
 }
 

@@ -22,6 +22,7 @@
  *   tv_pdf / tv_pdf_fast / mis_weight / sensors_visible  mvpath.h:243-311
  *   GridSensor::sample_ray_idx                     src/sensors/grid.cpp:269-297
  *   BatchSensor::sample_ray_idx                    src/sensors/batch.cpp:163-181
+ *   ThinLensCamera::sample_ray / sample_surface    src/sensors/thinlens.cpp:220-257,358-418
  *   PerspectiveCamera::sample_ray / sample_surface src/sensors/perspective.cpp:205-241,327-385
  *   PCG32Sampler::seed / IndependentSampler        src/render/sampler.cpp:125-144, independent.cpp:77-97
  *   sample_tea_32                                  include/mitsuba/core/random.h:77-90
@@ -782,7 +783,67 @@ static Ray persp_sample_ray(const amvpt_view_desc &v, V2 pos) {
     return r;
 }
 
+/* ThinLensCamera::sample_ray (thinlens.cpp:220-257) */
+static Ray thin_sample_ray(const amvpt_view_desc &v, V2 pos, V2 ap) {
+    V3 near_p = xform_point(v.sample_to_camera, v3(pos.x, pos.y, 0.f));
+    V2 t = square_to_uniform_disk_concentric(ap);
+    V3 aperture_p = v3(v.aperture_radius * t.x, v.aperture_radius * t.y, 0.f);
+    V3 focus_p = near_p * (v.focus_distance / near_p.z);
+    V3 d = normalize(focus_p - aperture_p);
+    Ray r;
+    r.o = xform_point_affine(v.to_world, aperture_p);
+    r.d = xform_vector(v.to_world, d);
+    float inv_z = rcp(d.z);
+    float near_t = v.near_clip * inv_z, far_t = v.far_clip * inv_z;
+    r.o = r.o + r.d * near_t;
+    r.maxt = far_t - near_t;
+    return r;
+}
+
+static Ray camera_sample_ray(const amvpt_view_desc &v, V2 pos, V2 ap) {
+    return v.type == AMVPT_CAMERA_THINLENS ? thin_sample_ray(v, pos, ap) : persp_sample_ray(v, pos);
+}
+
 struct SurfSample { DS ds; float Jp; bool face; bool valid; };
+
+/* ThinLensCamera::sample_surface (thinlens.cpp:358-418), JIT semantics (none_or<false>
+ * early-outs never taken); `ap` = the primary lane's aperture sample, shared by all views. */
+static SurfSample thin_sample_surface(const amvpt_view_desc &v, const SI &it, bool active, V2 ap) {
+    SurfSample r;
+    r.Jp = 0.f; r.face = false; r.valid = false;
+    if (!active) return r;
+    V3 ref_p = xform_point_affine(v.to_world_inv, it.p);
+    DS ds;
+    bool a = ref_p.z >= v.near_clip && ref_p.z <= v.far_clip;
+    V2 t = square_to_uniform_disk_concentric(ap);
+    V3 aperture_p = v3(t.x * v.aperture_radius, t.y * v.aperture_radius, 0.f);
+    V3 local_d = ref_p - aperture_p;
+    float dist = norm(local_d), inv_dist = rcp(dist);
+    local_d = local_d * inv_dist;
+    float ctf = local_d.z, ictf = rcp(ctf), ictf3 = ictf * ictf * ictf;
+    float inv_f = 1.f / v.focus_distance;
+    /* aperture_p * (1 / f) + local_d / local_d.z: separate multiply and add (no contraction) */
+    V3 film_plane = v3(aperture_p.x * inv_f + local_d.x / local_d.z, aperture_p.y * inv_f + local_d.y / local_d.z,
+                       aperture_p.z * inv_f + local_d.z / local_d.z);
+    V3 scr = xform_point_affine(v.camera_to_sample, film_plane);
+    a = a && scr.x >= 0.f && scr.y >= 0.f && scr.x <= 1.f && scr.y <= 1.f;
+    float pdf_lens = rcp(sqr(v.aperture_radius) * Pi);
+    float pdf_film = v.normalization * ictf3;
+    ds.pdf = pdf_lens * pdf_film;
+    ds.uv = {scr.x * v.resolution[0], scr.y * v.resolution[1]};
+    ds.p = xform_point_affine(v.to_world, aperture_p);
+    ds.d = (ds.p - it.p) * inv_dist;
+    ds.dist = dist;
+    ds.n = xform_vector(v.to_world, v3(0.f, 0.f, 1.f));
+    float cts = dot(ds.d, it.n);
+    bool face = cts > 0.f;
+    cts = std::fabs(cts);
+    r.ds = ds;
+    r.Jp = (cts * inv_dist * inv_dist) * ds.pdf;
+    r.face = face;
+    r.valid = a;
+    return r;
+}
 
 /* PerspectiveCamera::sample_surface (perspective.cpp:327-385), JIT semantics;
  * reached through GridSensor::sample_surface's masked vcall (grid.cpp:331-336). */
@@ -815,6 +876,10 @@ static SurfSample persp_sample_surface(const amvpt_view_desc &v, const SI &it, b
     float Jp = (cts * inv_dist * inv_dist) * ds.pdf;
     r.ds = ds; r.Jp = Jp; r.face = face; r.valid = a;
     return r;
+}
+
+static SurfSample camera_sample_surface(const amvpt_view_desc &v, const SI &it, bool active, V2 ap) {
+    return v.type == AMVPT_CAMERA_THINLENS ? thin_sample_surface(v, it, active, ap) : persp_sample_surface(v, it, active);
 }
 
 /* --------------------------------------------------------------------- */
@@ -912,13 +977,20 @@ struct Renderer {
     uint32_t fw, fh;
     uint64_t stat_vertices = 0, stat_reuse = 0, stat_vis = 0, stat_splats = 0;
 
-    Renderer(const Scene &s, const amvpt_view_desc *v, const amvpt_params &p) : sc(s), views(v), P(p) {}
+    V2 ap{.5f, .5f};            /* aperture sample of the current lane */
+    bool needs_ap = false;      /* Sensor::needs_aperture_sample (thin-lens views) */
+
+    Renderer(const Scene &s, const amvpt_view_desc *v, const amvpt_params &p) : sc(s), views(v), P(p) {
+        /* grid: its first sub-sensor decides (grid.cpp:228); batch: any child (batch.cpp:127) */
+        uint32_t nv = p.multisensor ? (p.batch ? p.n_views : 1u) : 1u;
+        for (uint32_t i = 0; i < nv; ++i) needs_ap = needs_ap || v[i].type == AMVPT_CAMERA_THINLENS;
+    }
 
     /* GridSensor::sample_ray_idx (grid.cpp:269-297) / single camera */
     Ray sample_ray_idx(V2 pos01, uint32_t &index) const {
         if (!P.multisensor) {
             index = 0;
-            return persp_sample_ray(views[0], pos01);
+            return camera_sample_ray(views[0], pos01, ap);
         }
         if (P.batch) {
             /* BatchSensor::sample_ray_idx (batch.cpp:163-181): clamp, then reverse_x */
@@ -926,7 +998,7 @@ struct Renderer {
             uint32_t idx_u = (uint32_t) idx_f;
             index = std::min(idx_u, P.n_views - 1);
             if (P.reverse_x) index = (P.n_views - 1) - index;
-            return persp_sample_ray(views[index], V2{idx_f - (float) idx_u, pos01.y});
+            return camera_sample_ray(views[index], V2{idx_f - (float) idx_u, pos01.y}, ap);
         }
         float gx = (float) P.grid_x, gy = (float) P.grid_y;
         V2 idx_f{pos01.x * gx, pos01.y * gy};
@@ -937,7 +1009,7 @@ struct Renderer {
         index = ix + P.grid_x * iy;
         index = std::min(index, P.n_views - 1);
         V2 p2{idx_f.x - (float) ux, idx_f.y - (float) uy};
-        return persp_sample_ray(views[index], p2);
+        return camera_sample_ray(views[index], p2, ap);
     }
 
     /* sample_single (mvpath_single.h:82-278) == PathIntegrator::sample */
@@ -1076,7 +1148,7 @@ struct Renderer {
 
     /* sensors_visible<primary> (mvpath.h:243-256) */
     SurfSample sensors_visible(bool primary, const SI &si, bool prim_face, uint32_t idx, bool active, bool count) {
-        SurfSample r = persp_sample_surface(views[idx], si, active);
+        SurfSample r = camera_sample_surface(views[idx], si, active, ap);
         if (!primary) {
             r.valid = r.valid && (r.face == prim_face) && r.Jp > 0.f;
             if (r.valid) { /* ray_test result only matters where valid */
@@ -1430,7 +1502,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
         uint32_t seed_value = P.base_seed + (is_mv ? (spp_pp * pass + P.seed) : P.seed);
         uint64_t span = lane_end - lane_begin;
         std::vector<uint8_t> amask(n_adapt ? L : 0, 0);
-        std::vector<float> spos(n_adapt ? 2 * L : 0, 0.f);
+        std::vector<float> spos(n_adapt ? 2 * L : 0, 0.f), sap(n_adapt ? 2 * L : 0, .5f);
         auto worker = [&](int tid) {
             std::vector<float> &tf = films[tid];
             if (tf.empty()) tf.assign((size_t) W * H * C, 0.f);
@@ -1453,6 +1525,8 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
                 V2 jit{rng.next_1d(), 0.f};
                 jit.y = rng.next_1d();
                 V2 sample_pos{(float) px + jit.x, (float) py + jit.y};
+                R.ap = V2{.5f, .5f};
+                if (R.needs_ap) { R.ap.x = rng.next_1d(); R.ap.y = rng.next_1d(); }
                 V2 adj{fmadd(sample_pos.x, 1.f / (float) W, -0.f * (1.f / (float) W)),
                        fmadd(sample_pos.y, 1.f / (float) H, -0.f * (1.f / (float) H))};
                 float *rec = (records && pass == record_pass) ? records + (lane - lane_begin) * (size_t) G * 8 : nullptr;
@@ -1492,6 +1566,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
                     amask[lane] = adapt_mask;
                     spos[2 * lane] = sample_pos.x;
                     spos[2 * lane + 1] = sample_pos.y;
+                    if (R.needs_ap) { sap[2 * lane] = R.ap.x; sap[2 * lane + 1] = R.ap.y; }
                 }
                 for (uint32_t i = 0; i < G; ++i) {
                     SampleData &s = S[i];
@@ -1542,6 +1617,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
                         rng.seed(v0, v1);
                         uint32_t lane = idx[j];
                         V2 sample_pos{spos[2 * lane], spos[2 * lane + 1]};
+                        R.ap = V2{sap[2 * lane], sap[2 * lane + 1]};   /* nested_gather(aperture_sample, idx) */
                         V2 adj{fmadd(sample_pos.x, 1.f / (float) W, -0.f * (1.f / (float) W)),
                                fmadd(sample_pos.y, 1.f / (float) H, -0.f * (1.f / (float) H))};
                         uint32_t index;

@@ -195,3 +195,12 @@ def test_batch_sensor(gpu_ready, amvpt_mod, oracle, rev):
     """`batch` MultiSensor (batch.cpp:163-181): strip layout, clamp-then-reverse view index."""
     s = amvpt_mod.load_file(BATCH, res=24, width=96, spp=16, rev=rev)
     _check(amvpt_mod, oracle, s)
+
+
+@pytest.mark.parametrize("kw", [dict(res=32, spp=16), dict(res=32, spp=16, reuse=1), dict(res=24, spp=16, adaptive=1)],
+                         ids=["g4_mis", "g1", "adaptive"])
+def test_thinlens_views(gpu_ready, amvpt_mod, oracle, kw):
+    """Thin-lens sub-sensors (thinlens.cpp:220-257,358-418): aperture sample drawn after the jitter
+    and shared by every view's sample_surface; re-gathered by the adaptive fill."""
+    s = amvpt_mod.load_file(CBOX, cam="thinlens", aperture="0.05", **kw)
+    _check(amvpt_mod, oracle, s)
