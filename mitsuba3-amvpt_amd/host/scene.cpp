@@ -33,6 +33,7 @@
 #include "../../include/amvpt.h"
 #include "../../include/amvpt_host.h"
 #include "xml.h"
+#include "meshio.h"
 
 namespace mi {
 
@@ -550,6 +551,30 @@ static void build(amvpt_host_scene &S) {
                 d.faces = m->faces.data();
                 fill_xform(T, d.to_world, d.to_object);
                 S.meshes.push_back(std::move(m));
+            } else if (t == "obj" || t == "ply") {
+                /* OBJMesh / PLYMesh (obj.cpp:148-406, ply.cpp:150-450) */
+                d.type = AMVPT_SHAPE_MESH;
+                d.flip_normals = flip;
+                std::string fn = p.get_string("filename");
+                if (fn.empty()) Throw("\"" + t + "\": property \"filename\" has not been specified");
+                if (fn[0] != '/') fn = (S.root->base_dir.empty() ? std::string(".") : S.root->base_dir) + "/" + fn;
+                const bool fnorm = p.get_bool("face_normals", false);
+                MeshData md = t == "obj" ? load_obj(fn, T, fnorm, p.get_bool("flip_tex_coords", true))
+                                         : load_ply(fn, T, fnorm, p.get_bool("flip_tex_coords", false));
+                if (md.faces.empty()) Throw("\"" + fn + "\": mesh has no faces");
+                auto m = std::make_unique<MeshStore>();
+                m->pos = std::move(md.pos);
+                m->nrm = std::move(md.nrm);
+                m->uv = std::move(md.uv);
+                m->faces = std::move(md.faces);
+                d.vertex_count = (uint32_t) (m->pos.size() / 3);
+                d.face_count = (uint32_t) (m->faces.size() / 3);
+                d.positions = m->pos.data();
+                d.normals = m->nrm.empty() ? nullptr : m->nrm.data();
+                d.texcoords = m->uv.empty() ? nullptr : m->uv.data();
+                d.faces = m->faces.data();
+                fill_xform(T, d.to_world, d.to_object);
+                S.meshes.push_back(std::move(m));
             } else if (t == "sphere") {
                 d.type = AMVPT_SHAPE_SPHERE;
                 V3f c = p.get_vec3("center", {0, 0, 0});
@@ -562,7 +587,7 @@ static void build(amvpt_host_scene &S) {
                 d.flip_normals = flip;
                 fill_xform(W, d.to_world, d.to_object);
             } else {
-                Throw("Shape \"" + p.plugin + "\" is not implemented (rectangle, cube, sphere)");
+                Throw("Shape \"" + p.plugin + "\" is not implemented (rectangle, cube, sphere, obj, ply)");
             }
             if (emit) {
                 std::string et = lower(emit->props.plugin);

@@ -389,7 +389,10 @@ std::shared_ptr<Object> load_scene_file(const std::string &path, const std::map<
     if (!f) throw std::runtime_error("Unable to open scene file \"" + path + "\"");
     std::stringstream ss;
     ss << f.rdbuf();
-    return load_scene_string(ss.str(), defines);
+    auto root = load_scene_string(ss.str(), defines);
+    const size_t slash = path.find_last_of('/');
+    root->base_dir = slash == std::string::npos ? std::string(".") : path.substr(0, slash);
+    return root;
 }
 
 } // namespace mi

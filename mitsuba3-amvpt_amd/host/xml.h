@@ -86,6 +86,7 @@ struct Properties {
 struct Object {
     std::string tag;       /* object class: integrator, sensor, film, rfilter, sampler, bsdf, emitter, shape, wrap, scene */
     Properties props;
+    std::string base_dir;  /* root only: directory of the scene file (FileResolver for `filename`) */
     virtual ~Object() = default;
 };
 

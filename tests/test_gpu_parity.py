@@ -204,3 +204,16 @@ def test_thinlens_views(gpu_ready, amvpt_mod, oracle, kw):
     and shared by every view's sample_surface; re-gathered by the adaptive fill."""
     s = amvpt_mod.load_file(CBOX, cam="thinlens", aperture="0.05", **kw)
     _check(amvpt_mod, oracle, s)
+
+
+MESH = os.path.join(SCENES, "cbox_mesh.xml")
+
+
+def test_file_meshes_per_lane_bvh(gpu_ready, amvpt_mod, oracle):
+    """OBJ (vertex normals + uv) and PLY (recomputed normals, rough conductor) meshes: 3.6k triangles, a
+    BVH far above the wave-uniform limit, walked per lane from global memory."""
+    s = amvpt_mod.load_file(MESH, res=16, spp=16)
+    sd, vd, p = s.describe(0, 0, 0)
+    n_nodes, n_prims = amvpt_mod.DeviceScene(sd).stats()
+    assert n_nodes > 255 and n_prims == 6 + 1280 + 2304
+    _check(amvpt_mod, oracle, s)

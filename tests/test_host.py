@@ -142,3 +142,72 @@ def test_batch_sensor_loading(amvpt_mod):
     assert all(tuple(vd[i].resolution) == (32, 32) for i in range(4))
     with pytest.raises(RuntimeError, match="divisible"):
         amvpt_mod.load_file(os.path.join(SCENES, "cbox_batch.xml"), res=32, width=130, spp=16)
+
+
+def _mesh_scene(shape_xml):
+    return """<scene version="3.0.0">
+      <integrator type="path"/>
+      <sensor type="perspective"><float name="fov" value="45"/>
+        <transform name="to_world"><lookat origin="0, 0, 4" target="0, 0, 0" up="0, 1, 0"/></transform>
+        <film type="hdrfilm"><integer name="width" value="8"/><integer name="height" value="8"/></film></sensor>
+      %s
+      <shape type="rectangle"><transform name="to_world"><translate value="0, 3, 0"/></transform>
+        <emitter type="area"><rgb name="radiance" value="1, 1, 1"/></emitter></shape>
+    </scene>""" % shape_xml
+
+
+def _mesh(amvpt_mod, xml):
+    s = amvpt_mod.load_string(xml)
+    sd, _, _ = s.describe(0, 0, 0)
+    d = sd[0].shapes[0]
+    nv, nf = d.vertex_count, d.face_count
+    faces = np.ctypeslib.as_array(d.faces, shape=(nf * 3,)).reshape(nf, 3).copy()
+    pos = np.ctypeslib.as_array(d.positions, shape=(nv * 3,)).reshape(nv, 3).copy()
+    nrm = np.ctypeslib.as_array(d.normals, shape=(nv * 3,)).reshape(nv, 3).copy() if d.normals else None
+    return s, d, faces, pos, nrm
+
+
+def test_obj_fan_triangulation_and_dedup(amvpt_mod):
+    """obj.cpp:270-330: polygons fan out as (v0, v[k-1], v[k]); vertices shared by (v, vt, vn) key."""
+    path = os.path.join(SCENES, "meshes", "quad_fan.obj")
+    s, d, faces, pos, nrm = _mesh(amvpt_mod, _mesh_scene('<shape type="obj"><string name="filename" value="%s"/></shape>' % path))
+    assert d.vertex_count == 7 and d.face_count == 5
+    assert faces.tolist() == [[0, 1, 2], [0, 2, 3], [0, 3, 4], [1, 5, 6], [1, 6, 2]]
+    assert np.allclose(pos[5], [2, 0, 0])
+    assert nrm is not None and np.allclose(nrm, [0, 0, 1], atol=1e-6)   # recomputed (planar mesh)
+
+
+def test_obj_transform_and_normals(amvpt_mod):
+    path = os.path.join(SCENES, "meshes", "icosphere.obj")
+    xml = _mesh_scene('<shape type="obj"><string name="filename" value="%s"/><transform name="to_world">'
+                      '<scale x="2" y="1" z="1"/><translate x="1"/></transform></shape>' % path)
+    s, d, faces, pos, nrm = _mesh(amvpt_mod, xml)
+    assert d.vertex_count == 642 and d.face_count == 1280
+    assert np.allclose(pos[:, 0].min(), -1, atol=1e-5) and np.allclose(pos[:, 0].max(), 3, atol=1e-5)
+    assert np.allclose(np.linalg.norm(nrm, axis=1), 1, atol=1e-5)
+    # normals transform with the inverse transpose: on the unit sphere scaled by (2,1,1), n ~ (x/4, y, z)
+    p0 = (pos - [1, 0, 0]) / [2, 1, 1]
+    ref = p0 / [2, 1, 1]
+    ref /= np.linalg.norm(ref, axis=1, keepdims=True)
+    assert np.abs(nrm - ref).max() < 1e-4
+    _, d2, _, _, nrm2 = _mesh(amvpt_mod, xml.replace('<transform', '<boolean name="face_normals" value="true"/><transform'))
+    assert not d2.normals and nrm2 is None
+
+
+def test_ply_binary_with_recomputed_normals(amvpt_mod):
+    path = os.path.join(SCENES, "meshes", "torus.ply")
+    s, d, faces, pos, nrm = _mesh(amvpt_mod, _mesh_scene('<shape type="ply"><string name="filename" value="%s"/></shape>' % path))
+    assert d.vertex_count == 48 * 24 and d.face_count == 2304
+    assert np.allclose(np.linalg.norm(nrm, axis=1), 1, atol=1e-5)
+    # torus normal at a vertex points away from the tube centre ring
+    ring = pos.copy()
+    ring[:, 1] = 0
+    ring = ring / np.linalg.norm(ring, axis=1, keepdims=True)
+    radial = pos - ring
+    radial /= np.linalg.norm(radial, axis=1, keepdims=True)
+    assert (np.sum(radial * nrm, axis=1) > 0.99).all()
+
+
+def test_mesh_errors(amvpt_mod):
+    with pytest.raises(RuntimeError, match="not found"):
+        amvpt_mod.load_string(_mesh_scene('<shape type="obj"><string name="filename" value="/nope.obj"/></shape>'))
