@@ -34,6 +34,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CHUNK_LANES = 1 << 23  # amvpt_render's default lane chunk (g_chunk_lanes)
 
 
+# SURVEY 8 config table.  M = the metric's workload (bench line); C5 = the 32-view adaptive
+# scale configuration (grid 8x4 of 2048^2 views, groups of 4, one 16-spp pass, adaptive 3),
+# lane-sharded so that every GPU count renders the same frame.
+CONFIGS = {
+    "M": dict(res=1024, spp=64, gx=4, gy=2, reuse=8, adaptive=0, sharding="pass"),
+    "C5": dict(res=2048, spp=16, gx=8, gy=4, reuse=4, adaptive=3, sharding="lane"),
+}
+
+
 def group_size(p):
     """Views per group (mvpath.cpp:192-217)."""
     if not (p.sa_reuse and p.n_views > 1 and p.reuse_count != 1):
@@ -52,14 +61,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--res", type=int, default=1024)
-    ap.add_argument("--spp", type=int, default=64)
-    ap.add_argument("--gx", type=int, default=4)
-    ap.add_argument("--gy", type=int, default=2)
-    ap.add_argument("--reuse", type=int, default=8)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="M",
+                    help="M: the metric's workload (default); C5: 32-view 2048^2 adaptive, lane-sharded")
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--gx", type=int, default=None)
+    ap.add_argument("--gy", type=int, default=None)
+    ap.add_argument("--reuse", type=int, default=None)
+    ap.add_argument("--adaptive", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    for k in ("res", "spp", "gx", "gy", "reuse", "adaptive"):
+        if getattr(args, k) is not None:
+            cfg[k] = getattr(args, k)
+    headline = cfg == CONFIGS["M"]   # PMC traffic in profiles/ was collected on exactly this workload
+    lane_sharded = cfg.pop("sharding") == "lane"
 
     import torch
     import torch.distributed as dist
@@ -76,23 +94,29 @@ def main():
     hip = amvpt.hip_lib()
     hip.amvpt_set_device(local)
 
-    scene = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), res=args.res, spp=args.spp,
-                            gx=args.gx, gy=args.gy, reuse=args.reuse)
+    scene = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), **cfg)
     sd, vd, p = scene.describe(0, 0, 0)
     plan = amvpt.plan(p)
     spp, spp_pp, n_passes, lanes_per_pass = plan
-    # pass sharding: this rank's passes are [rank*n_passes, (rank+1)*n_passes) of a world*spp frame
-    p = adist.pass_shard(p, rank, world, plan)
+    if lane_sharded:
+        # strong scaling: this rank's lanes of every pass of ONE frame; the adaptive fill's
+        # prefix/total come from one all-gather per pass (amvpt.dist.count_exchange)
+        lane_begin, lane_end = adist.lane_shard(lanes_per_pass, rank, world)
+        amvpt.set_adaptive_exchange(adist.count_exchange(device="cuda"))
+    else:
+        # pass sharding: this rank's passes are [rank*n_passes, (rank+1)*n_passes) of a world*spp frame
+        lane_begin, lane_end = 0, 2 ** 64 - 1
+        p = adist.pass_shard(p, rank, world, plan)
     dev = amvpt.DeviceScene(sd)
     C = 5 if p.film_alpha else 4
     film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    samples_per_rank = lanes_per_pass * n_passes
+    samples_per_rank = (min(lane_end, lanes_per_pass) - lane_begin) * n_passes
     G = group_size(p)
 
     def step(counters=None):
         film.zero_()
-        c = dev.render(vd, p, film.data_ptr(), 0, 2 ** 64 - 1, stream, counters)
+        c = dev.render(vd, p, film.data_ptr(), lane_begin, lane_end, stream, counters)
         adist.reduce_film(film, dst=0)
         return c
 
@@ -142,16 +166,16 @@ def main():
     achieved = bytes_stage[dom] / (stage_ms[dom] * 1e-3) / 1e9
     kernel_name = {"primary": "k_mv_primary<%d>" % G if G > 1 else "k_raygen_single", "bounce": "k_bounce",
                    "splat": "k_splat_multi<%d, %d>" % (G, C) if G > 1 else "k_splat_single<%d>" % C}[dom]
-    chunks = n_passes * ((lanes_per_pass + CHUNK_LANES - 1) // CHUNK_LANES)
+    chunks = n_passes * ((samples_per_rank // n_passes + CHUNK_LANES - 1) // CHUNK_LANES)
     launches = {"primary": chunks, "splat": chunks, "bounce": None}[dom]
-    traffic, traffic_src = pmc_traffic(kernel_name, args.res == 1024)
+    traffic, traffic_src = pmc_traffic(kernel_name, headline)
     # SURVEY 8(d) whole-pipeline byte model
     P = p.film_width * p.film_height
     B_sample = 336.0 * vbar + 120.0 * (G - 1) * hbar + 32.0 * P / samples_per_rank
     pipeline_gbs = value / world * 1e6 * B_sample / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not p.adaptive:
         cpu = cpu_baseline(sd, vd, p, args.cpu_seconds)
 
     if rank == 0:
@@ -164,16 +188,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if lane_sharded else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (Cornell box of util.py:551-685 on a 4x2 grid sensor; no external assets)",
+            "data": "synthetic (Cornell box of util.py:551-685 on a %dx%d grid sensor; no external assets)"
+                    % (p.grid_x, p.grid_y),
             "config": {
-                "workload": "M: 8-view %dx%d per view (quilt %dx%d), %d spp/GPU (%d passes x %d), G=%d, sa_mis, "
-                            "max_depth 8, rr_depth 5, seed 0" % (args.res, args.res, p.film_width, p.film_height,
-                                                                 spp, n_passes, spp_pp, G),
+                "workload": "%s: %d-view %dx%d per view (quilt %dx%d), %d spp%s (%d passes x %d), G=%d, sa_mis, "
+                            "adaptive %d, max_depth 8, rr_depth 5, seed 0"
+                            % (args.config, p.n_views, cfg["res"], cfg["res"], p.film_width, p.film_height, spp,
+                               "" if lane_sharded else "/GPU", n_passes, spp_pp, G, p.adaptive),
                 "samples_per_gpu_per_step": samples_per_rank,
-                "parallelism": "pass-sharded x%d + RCCL reduce of the RGBW ImageBlock" % world,
+                "adaptive_lanes_per_gpu_per_step": c["adaptive_lanes"],
+                "parallelism": ("lane-sharded x%d (+ one count all-gather per pass) + RCCL reduce of the RGBW "
+                                "ImageBlock" if lane_sharded else
+                                "pass-sharded x%d + RCCL reduce of the RGBW ImageBlock") % world,
             },
             "roofline": {
                 "bound": "hbm",

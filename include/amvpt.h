@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 2
+#define AMVPT_ABI_VERSION 3
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -239,6 +239,22 @@ amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes);
 /* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane), 1 force wave-uniform,
  * 2 force per-lane.  Results are identical in every mode (closest hit = min (t, prim)). */
 amvpt_status amvpt_set_traversal(uint32_t mode);
+
+/*
+ * Adaptive fill over a lane range (adaptive > 0 with lane_begin/lane_end not the
+ * whole pass).  The fill re-traces the pass's flagged lanes in compressed order
+ * and seeds its sampler from the size of the WHOLE pass's compressed array
+ * (mvpath_multi.h:81-90: dr::compress, dr::repeat, sampler->seed(wavefront,
+ * wavefront)), so a rank rendering [lane_begin, lane_end) must learn, once per
+ * pass, how many flagged lanes lie in lower ranges (`prefix`) and in the whole
+ * pass (`total`).  The host supplies that exchange (an all-gather of one
+ * integer per rank: MPI, RCCL, torch.distributed, ...); it receives this
+ * range's flagged-lane count and returns 0 on success.  Every rank calls
+ * amvpt_render with the same params and disjoint ranges; NULL clears it, and
+ * without it a partial-range adaptive render is refused.
+ */
+typedef int (*amvpt_exchange_fn)(void *ctx, uint64_t local_count, uint64_t *prefix, uint64_t *total);
+amvpt_status amvpt_set_adaptive_exchange(amvpt_exchange_fn fn, void *ctx);
 
 #ifdef __cplusplus
 }

@@ -97,7 +97,8 @@ def hip_lib():
         L.amvpt_film_channels.restype = u32
         for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
                    "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
-                   "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal"):
+                   "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal",
+                   "amvpt_set_adaptive_exchange"):
             if hasattr(L, fn):   # older variant builds (AMVPT_LIB_DIR A/B runs) may lack the newest knobs
                 getattr(L, fn).restype = ctypes.c_int
         L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,
@@ -111,6 +112,8 @@ def hip_lib():
                                  ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.amvpt_develop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u32, u32, u32, ctypes.c_void_p]
         L.amvpt_set_chunk_lanes.argtypes = [u64]
+        if hasattr(L, "amvpt_set_adaptive_exchange"):
+            L.amvpt_set_adaptive_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.amvpt_set_device.argtypes = [ctypes.c_int]
         L.amvpt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         _hip = L
@@ -241,6 +244,34 @@ def set_traversal(mode):
 def set_chunk_lanes(n):
     L = hip_lib()
     _check(L.amvpt_set_chunk_lanes(u64(n)), L)
+
+
+# amvpt_exchange_fn: (ctx, local_count, *prefix, *total) -> 0 on success
+ExchangeFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, u64, ctypes.POINTER(u64), ctypes.POINTER(u64))
+_exchange_cb = None
+
+
+def wrap_exchange(fn):
+    """ctypes callback around `fn(local_count) -> (prefix, total)` (exceptions -> status 1)."""
+    def cb(_ctx, local, prefix, total):
+        try:
+            pre, tot = fn(int(local))
+            prefix[0], total[0] = int(pre), int(tot)
+            return 0
+        except Exception:   # noqa: BLE001 -- reported to the C side as a failed exchange
+            return 1
+    return ExchangeFn(cb)
+
+
+def set_adaptive_exchange(fn):
+    """Count exchange for adaptive renders over lane ranges (amvpt_set_adaptive_exchange).
+
+    `fn(local_count) -> (prefix, total)`: flagged lanes in lower ranges and in the
+    whole pass (see amvpt.dist.count_exchange); None clears it."""
+    global _exchange_cb
+    L = hip_lib()
+    _exchange_cb = wrap_exchange(fn) if fn is not None else None
+    _check(L.amvpt_set_adaptive_exchange(_exchange_cb if _exchange_cb else ExchangeFn(), None), L)
 
 
 def device_count():

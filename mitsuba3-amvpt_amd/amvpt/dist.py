@@ -12,7 +12,8 @@ Two partitions are provided:
     spp_per_pass * P * r -- exactly the seeds those passes get in a single
     (world * spp)-spp render (seed_value = spp_per_pass * pass + seed).
   * lane_shard  -- strong scaling: rank r renders lanes [begin, end) of every
-    pass of the same frame (amvpt_render's lane_begin/lane_end).
+    pass of the same frame (amvpt_render's lane_begin/lane_end).  With
+    adaptive > 0 the fill needs one tiny exchange per pass (count_exchange).
 """
 
 
@@ -21,8 +22,6 @@ def pass_shard(params, rank, world, plan):
     spp, spp_pp, n_passes, _ = plan
     if world < 1 or not 0 <= rank < world:
         raise ValueError("rank %d outside world %d" % (rank, world))
-    if params.adaptive and world > 1:
-        raise ValueError("adaptive passes compact the whole frame: pass sharding needs adaptive = 0")
     p = type(params).from_buffer_copy(params)
     p.seed = params.seed + spp_pp * n_passes * rank
     return p
@@ -35,6 +34,26 @@ def lane_shard(n_lanes, rank, world):
     q, r = divmod(n_lanes, world)
     begin = rank * q + min(rank, r)
     return begin, begin + q + (1 if rank < r else 0)
+
+
+def count_exchange(device=None):
+    """`fn(local) -> (prefix, total)` over torch.distributed (one all-gather of one
+    integer per rank and pass): the adaptive fill's index space is the whole pass's
+    compressed lane array (mvpath_multi.h:81-90), so a lane-sharded rank needs the
+    number of flagged lanes in the ranges of lower ranks (lane_shard orders ranges
+    by rank) and in the whole pass.  Install it with amvpt.set_adaptive_exchange."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(local):
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return 0, local
+        t = torch.tensor([local], dtype=torch.int64, device=device)
+        out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, t)
+        counts = [int(o.item()) for o in out]
+        return sum(counts[:dist.get_rank()]), sum(counts)
+    return fn
 
 
 def reduce_film(film, dst=0):

@@ -206,6 +206,12 @@ amvpt_status amvpt_set_traversal(uint32_t mode) {
     return AMVPT_OK;
 }
 
+amvpt_status amvpt_set_adaptive_exchange(amvpt_exchange_fn fn, void *ctx) {
+    g_exchange = fn;
+    g_exchange_ctx = fn ? ctx : nullptr;
+    return AMVPT_OK;
+}
+
 amvpt_status amvpt_plan(const amvpt_params *P, uint32_t *spp, uint32_t *spp_pp, uint32_t *n_passes,
                         uint64_t *lanes) {
     if (!P) { set_error("amvpt_plan: null params"); return AMVPT_ERR_INVALID; }

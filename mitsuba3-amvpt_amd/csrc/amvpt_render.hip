@@ -35,6 +35,8 @@ namespace amvpt {
 
 uint64_t g_chunk_lanes = 1ull << 23;
 uint32_t g_traversal = 0;
+amvpt_exchange_fn g_exchange = nullptr;
+void *g_exchange_ctx = nullptr;
 
 /* ------------------------------------------------------------------ */
 /* Parameters                                                         */
@@ -53,6 +55,8 @@ struct KParams {
     uint32_t trav_mode;     /* amvpt_set_traversal */
     uint32_t adapt_seed;    /* adaptive pass: seed of the forked sampler (base_seed + wavefront) */
     uint32_t pass_seed;     /* adaptive pass: seed_value of the pass whose lanes are refilled */
+    uint32_t adapt_base;    /* adaptive pass: index of this range's first entry in the pass's wavefront */
+    uint64_t range_begin;   /* lane_begin of the render (amask is indexed from it) */
     float inv_w, inv_h;
     float adapt_w;
     FilterCoeffs filt;
@@ -853,7 +857,7 @@ __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V,
         float sx, sy, apx, apy;
         lane_sample_pos(P, lane, sx, sy, apx, apy);
         uint32_t v0, v1;
-        tea4(P.adapt_seed, j, v0, v1);
+        tea4(P.adapt_seed, P.adapt_base + j, v0, v1);
         Pcg rng;
         rng.seed(v0, v1);
         uint32_t index;
@@ -1386,7 +1390,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
     if (ok) { lr = B.lane_rec[slot]; lo = B.lane_out[slot]; }
     uint32_t lflags = fbits(lr.y);
     float pdfW = lr.x;
-    if (ok && B.amask) B.amask[P.chunk_begin + i] = (lflags & LF_ADAPT) ? 1u : 0u;
+    if (ok && B.amask) B.amask[P.chunk_begin - P.range_begin + i] = (lflags & LF_ADAPT) ? 1u : 0u;
     bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
     bool mis = (lflags & LF_MIS) != 0;
     bool adapt_mask = (lflags & LF_ADAPT) != 0;
@@ -1542,6 +1546,7 @@ static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launc
 static const splat_fn kSplat[] = {nullptr, nullptr, launch_splat<2>, launch_splat<3>, launch_splat<4>,
                                   launch_splat<5>, launch_splat<6>, launch_splat<7>, launch_splat<8>};
 constexpr uint32_t kMaxG = 8;
+constexpr uint64_t kSelectChunk = 1ull << 30;
 
 amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
                          uint64_t lane_begin, uint64_t lane_end, float *film, void *stream,
@@ -1573,10 +1578,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         return AMVPT_OK;
     }
     /* the adaptive fill compacts the whole pass (its RNG seeds depend on the global
-     * wavefront), so it cannot be split by lane ranges (shard by passes instead) */
+     * wavefront): a lane range needs the host's count exchange (amvpt_set_adaptive_exchange) */
     const bool do_fill = n_adapt && !Pp.debug;
-    if (do_fill && (lane_begin != 0 || lane_end != L)) {
-        set_error("amvpt_render: adaptive > 0 needs the whole frame (lane_begin = 0, lane_end = all lanes)");
+    const bool partial = lane_begin != 0 || lane_end != L;
+    const amvpt_exchange_fn exchange = g_exchange;
+    void *const exchange_ctx = g_exchange_ctx;
+    if (do_fill && partial && !exchange) {
+        set_error("amvpt_render: adaptive > 0 over a lane range needs amvpt_set_adaptive_exchange "
+                  "(or the whole frame: lane_begin = 0, lane_end = all lanes)");
         return AMVPT_ERR_UNSUPPORTED;
     }
 
@@ -1606,6 +1615,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.inv_h = 1.f / (float) P.H;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = g_traversal;
+    P.range_begin = lane_begin;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
 
     /* views to device (tiny) */
@@ -1660,11 +1670,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     uint32_t *d_asel = nullptr, *d_anum = nullptr;
     void *d_cub = nullptr;
     size_t cub_bytes = 0;
+    const uint64_t span_all = lane_end - lane_begin;
+    const uint64_t sel_max = std::min<uint64_t>(span_all, kSelectChunk);
     if (do_fill) {
         HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, cub_bytes, hipcub::CountingInputIterator<uint32_t>(0),
                                              (const uint8_t *) nullptr, (uint32_t *) nullptr, (uint32_t *) nullptr,
-                                             (int) L, st));
-        const size_t abytes = ((L + 255) & ~(uint64_t) 255) + 4 * ((L + 63) & ~(uint64_t) 63) + 256 + cub_bytes + 256;
+                                             (int) sel_max, st));
+        const size_t abytes = ((span_all + 255) & ~(uint64_t) 255) + 4 * ((span_all + 63) & ~(uint64_t) 63) + 256 +
+                              cub_bytes + 256;
         if (g_adapt.bytes < abytes || g_adapt.device != dev) {
             if (g_adapt.base) (void) hipFree(g_adapt.base);
             g_adapt.base = nullptr;
@@ -1677,14 +1690,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             g_adapt.device = dev;
         }
         char *ap = (char *) g_adapt.base;
-        d_amask = (uint8_t *) ap; ap += (L + 255) & ~(uint64_t) 255;
-        d_asel = (uint32_t *) ap; ap += 4 * ((L + 63) & ~(uint64_t) 63);
+        d_amask = (uint8_t *) ap; ap += (span_all + 255) & ~(uint64_t) 255;
+        d_asel = (uint32_t *) ap; ap += 4 * ((span_all + 63) & ~(uint64_t) 63);
         d_anum = (uint32_t *) ap; ap += 256;
         d_cub = ap;
-    }
-    if (do_fill && L > 0x7fffffffull) {
-        set_error("amvpt_render: adaptive fill over more than 2^31 lanes per pass");
-        return AMVPT_ERR_UNSUPPORTED;
     }
 
     Bufs B{};
@@ -1780,17 +1789,33 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         }
         if (do_fill) {
             /* compact the pass's adapt_mask lanes in lane order, then n_adapt re-traces each */
-            HIPCHK(hipcub::DeviceSelect::Flagged(d_cub, cub_bytes, hipcub::CountingInputIterator<uint32_t>(0),
-                                                 d_amask, d_asel, d_anum, (int) L, st));
-            uint32_t n_sel = 0;
-            HIPCHK(hipMemcpyAsync(&n_sel, d_anum, 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            const uint64_t wf = (uint64_t) n_sel * n_adapt;
+            /* (hipcub counts in int: select in pieces of <= 2^30 lanes, appending) */
+            uint64_t n_sel = 0;
+            for (uint64_t s0 = 0; s0 < span_all; s0 += kSelectChunk) {
+                const uint64_t sn = std::min<uint64_t>(kSelectChunk, span_all - s0);
+                HIPCHK(hipcub::DeviceSelect::Flagged(d_cub, cub_bytes,
+                                                     hipcub::CountingInputIterator<uint32_t>((uint32_t) (lane_begin + s0)),
+                                                     d_amask + s0, d_asel + n_sel, d_anum, (int) sn, st));
+                uint32_t got = 0;
+                HIPCHK(hipMemcpyAsync(&got, d_anum, 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                n_sel += got;
+            }
+            /* this range's place in the pass's compressed array */
+            uint64_t prefix = 0, total = n_sel;
+            if (partial) {
+                if (exchange(exchange_ctx, n_sel, &prefix, &total) != 0 || prefix + n_sel > total) {
+                    set_error("amvpt_render: adaptive count exchange failed");
+                    return AMVPT_ERR_INVALID;
+                }
+            }
+            const uint64_t wf = n_sel * n_adapt;
             adaptive_lanes += wf;
-            if (wf > 0xffffffffull) { set_error("amvpt_render: adaptive wavefront over 2^32 lanes"); return AMVPT_ERR_UNSUPPORTED; }
+            if (total * n_adapt > 0xffffffffull) { set_error("amvpt_render: adaptive wavefront over 2^32 lanes"); return AMVPT_ERR_UNSUPPORTED; }
             KParams Ps = P;
             P.pass_seed = P.seed_value;
-            P.adapt_seed = Pp.base_seed + (uint32_t) wf;   /* sampler->fork(); seed(wavefront, wavefront) */
+            P.adapt_seed = Pp.base_seed + (uint32_t) (total * n_adapt);   /* sampler->fork(); seed(wavefront, wavefront) */
+            P.adapt_base = (uint32_t) (prefix * n_adapt);
             P.record = 0;
             for (uint64_t c0 = 0; c0 < wf; c0 += chunk) {
                 const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, wf - c0);

@@ -26,4 +26,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream);
 extern uint64_t g_chunk_lanes;
 extern uint32_t g_traversal;
+extern amvpt_exchange_fn g_exchange;
+extern void *g_exchange_ctx;
 } // namespace amvpt

@@ -1455,6 +1455,12 @@ static uint32_t group_size(const amvpt_params &P, bool reuse) {
 /* ====================================================================== */
 extern "C" {
 
+typedef int (*oracle_exchange_fn)(void *ctx, uint64_t local, uint64_t *prefix, uint64_t *total);
+static oracle_exchange_fn g_exchange = nullptr;
+static void *g_exchange_ctx = nullptr;
+/* adaptive fill over a lane range: per pass, (local flagged-lane count) -> (prefix, total) */
+void oracle_set_exchange(oracle_exchange_fn fn, void *ctx) { g_exchange = fn; g_exchange_ctx = ctx; }
+
 struct oracle_stats { uint64_t lanes, vertices, reuse_lanes, visibility_rays, adaptive_lanes; double seconds; };
 
 /*
@@ -1492,7 +1498,8 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
     uint32_t sres_x = W / gx, sres_y = H / gy;
     uint32_t n_adapt = std::min(P.adaptive, G - 1);
     if (!is_mv && n_passes > 1) return 4; /* stock path: RNG state carried across passes (unsupported) */
-    if (n_adapt && (lane_begin != 0 || lane_end != L)) return 4; /* adaptive needs the full frame */
+    const bool partial = lane_begin != 0 || lane_end != L;
+    if (n_adapt && partial && !g_exchange) return 4; /* adaptive needs the full frame or a count exchange */
     if (n_threads <= 0) n_threads = (int) std::max(1u, std::thread::hardware_concurrency());
 
     std::atomic<uint64_t> a_vert{0}, a_reuse{0}, a_vis{0}, a_adapt{0};
@@ -1596,12 +1603,17 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
         if (n_adapt) {
             /* adaptive fill (mvpath_multi.h:79-115): compress + repeat, new sampler seeded (W, W) */
             std::vector<uint32_t> idx;
-            for (uint64_t l = 0; l < L; ++l)
+            for (uint64_t l = lane_begin; l < lane_end; ++l)
                 if (amask[l]) for (uint32_t r = 0; r < n_adapt; ++r) idx.push_back((uint32_t) l);
             uint64_t wf = idx.size();
+            /* lane-sharded frame: the fill's index space is the whole pass's compressed
+             * array, so ask the other ranges how many flagged lanes precede this one */
+            uint64_t prefix = 0, total = wf / n_adapt;
+            if (partial && g_exchange(g_exchange_ctx, wf / n_adapt, &prefix, &total) != 0) return 5;
             a_adapt += wf;
             if (wf > 0) {
-                uint32_t sv = P.base_seed + (uint32_t) wf;
+                uint32_t sv = P.base_seed + (uint32_t) (total * n_adapt);
+                uint32_t jbase = (uint32_t) (prefix * n_adapt);
                 float adapt_w = 1.f / (float) (n_adapt + 1);
                 auto aworker = [&](int tid) {
                     Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, films[tid].data()};
@@ -1612,7 +1624,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
                     uint64_t b0 = wf * tid / n_threads, b1 = wf * (tid + 1) / n_threads;
                     for (uint64_t j = b0; j < b1; ++j) {
                         uint32_t v0, v1;
-                        tea(sv, (uint32_t) j, 4, v0, v1);
+                        tea(sv, jbase + (uint32_t) j, 4, v0, v1);
                         PCG32 rng;
                         rng.seed(v0, v1);
                         uint32_t lane = idx[j];

@@ -40,6 +40,7 @@ def lib():
                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_uint32, ctypes.POINTER(OracleStats)]
         L.oracle_plan.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
+        L.oracle_set_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.oracle_tea_float32.restype = ctypes.c_float
         L.oracle_tea_float64.restype = ctypes.c_double
         L.oracle_gaussian_eval.restype = ctypes.c_float
@@ -79,6 +80,30 @@ def plan(params):
     L.oracle_plan(ctypes.byref(params), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(lanes),
                   ctypes.byref(g))
     return dict(spp=a.value, spp_per_pass=b.value, passes=c.value, lanes=lanes.value, group=g.value)
+
+
+ExchangeFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                              ctypes.POINTER(ctypes.c_uint64))
+_exchange_cb = None
+
+
+def set_exchange(fn):
+    """Adaptive fill over a lane range: `fn(local_count) -> (prefix, total)` once per pass."""
+    global _exchange_cb
+    if fn is None:
+        _exchange_cb = None
+        lib().oracle_set_exchange(ExchangeFn(), None)
+        return
+
+    def cb(_ctx, local, prefix, total):
+        try:
+            pre, tot = fn(int(local))
+            prefix[0], total[0] = int(pre), int(tot)
+            return 0
+        except Exception:   # noqa: BLE001
+            return 1
+    _exchange_cb = ExchangeFn(cb)
+    lib().oracle_set_exchange(_exchange_cb, None)
 
 
 def render(scene_desc_ptr, views_ptr, params, lane_begin=0, lane_end=2 ** 64 - 1, threads=0,

@@ -178,13 +178,67 @@ def test_adaptive_fill(gpu_ready, amvpt_mod, oracle, adaptive, extra):
     assert cnt.adaptive_lanes == st["adaptive_lanes"] > 0
 
 
-def test_adaptive_refuses_lane_shards(gpu_ready, amvpt_mod):
+def test_adaptive_refuses_lane_shards_without_exchange(gpu_ready, amvpt_mod):
     s = amvpt_mod.load_file(CBOX, res=16, spp=16, adaptive=1)
     sd, vd, p = s.describe(0, 0, 0)
     torch = _torch()
     film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
-    with pytest.raises(RuntimeError, match="whole frame"):
+    amvpt_mod.set_adaptive_exchange(None)
+    with pytest.raises(RuntimeError, match="amvpt_set_adaptive_exchange"):
         amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), 0, 100)
+
+
+def _counts_per_pass(render_range, shards, set_exchange):
+    """Phase 1: each range's flagged-lane count per pass (the fill's output is discarded)."""
+    counts = []
+    for b, e in shards:
+        got = []
+        set_exchange(lambda local: (got.append(local), (0, local))[1])
+        render_range(b, e)
+        counts.append(got)
+    set_exchange(None)
+    return counts
+
+
+def _exchange_from(counts, r):
+    calls = iter(range(len(counts[0])))
+
+    def fn(local):
+        k = next(calls)
+        assert local == counts[r][k]
+        return sum(c[k] for c in counts[:r]), sum(c[k] for c in counts)
+    return fn
+
+
+def test_adaptive_lane_shards_with_exchange(gpu_ready, amvpt_mod, oracle):
+    """C5's partition: adaptive > 0 over lane ranges, the fill's prefix/total supplied per pass by
+    the host exchange (amvpt_set_adaptive_exchange); the ranges' films sum to the whole frame."""
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=24, spp=32, gx=4, gy=2, reuse=4, adaptive=2)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    assert plan["passes"] == 2
+    n = plan["lanes"]
+    shards = [(0, n // 3 + 5), (n // 3 + 5, 2 * n // 3 - 300), (2 * n // 3 - 300, n)]
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+
+    def render_range(b, e):
+        dev.render(vd, p, film.data_ptr(), b, e)
+        torch.cuda.synchronize()
+    counts = _counts_per_pass(render_range, shards, amvpt_mod.set_adaptive_exchange)
+    assert all(len(c) == 2 for c in counts) and sum(counts[1]) > 0
+    film.zero_()
+    try:
+        for r, (b, e) in enumerate(shards):
+            amvpt_mod.set_adaptive_exchange(_exchange_from(counts, r))
+            render_range(b, e)
+    finally:
+        amvpt_mod.set_adaptive_exchange(None)
+    got = film.cpu().numpy()
+    ref, _, st = oracle.render(sd, vd, p, threads=16)
+    assert st["adaptive_lanes"] == 2 * sum(sum(c) for c in counts)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
 BATCH = os.path.join(SCENES, "cbox_batch.xml")

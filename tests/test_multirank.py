@@ -23,7 +23,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, mode, out_dir):
+def _worker(rank, world, port, mode, out_dir, kw=None):
     import sys
     for p in (REPO, PKG):
         if p not in sys.path:
@@ -37,7 +37,7 @@ def _worker(rank, world, port, mode, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        s = amvpt.load_file(CBOX, res=16, spp=16, gx=2, gy=2, reuse=4)
+        s = amvpt.load_file(CBOX, **(kw or dict(res=16, spp=16, gx=2, gy=2, reuse=4)))
         sd, vd, p = s.describe(0, 0, 0)
         plan = amvpt.plan(p)
         if mode == "pass":
@@ -45,7 +45,9 @@ def _worker(rank, world, port, mode, out_dir):
             film, _, _ = O.render(sd, vd, pr, threads=2)
         else:
             b, e = adist.lane_shard(plan[3], rank, world)
+            O.set_exchange(adist.count_exchange())
             film, _, _ = O.render(sd, vd, p, lane_begin=b, lane_end=e, threads=2)
+            O.set_exchange(None)
         t = torch.from_numpy(film)
         adist.reduce_film(t, dst=0)
         if rank == 0:
@@ -54,10 +56,10 @@ def _worker(rank, world, port, mode, out_dir):
         dist.destroy_process_group()
 
 
-def _run(mode, world=2):
+def _run(mode, world=2, kw=None):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), mode, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), mode, d, kw), nprocs=world, join=True)
         return np.load(os.path.join(d, "film.npy"))
 
 
@@ -75,6 +77,28 @@ def test_pass_sharded_frame_equals_double_spp_frame(oracle, amvpt_mod):
     s = amvpt_mod.load_file(CBOX, res=16, spp=32, gx=2, gy=2, reuse=4)
     sd, vd, p = s.describe(0, 0, 0)
     assert amvpt_mod.plan(p)[2] == 2
+    ref, _, _ = oracle.render(sd, vd, p, threads=4)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_adaptive_lane_shards_exchange_counts(oracle, amvpt_mod):
+    """C5's partition: adaptive > 0 over lane ranges; the fill learns its prefix and the pass's
+    total from one all-gather per pass (amvpt.dist.count_exchange) and the sum is the frame."""
+    kw = dict(res=16, spp=32, gx=2, gy=2, reuse=4, adaptive=2)
+    got = _run("lane", world=3, kw=kw)
+    s = amvpt_mod.load_file(CBOX, **kw)
+    sd, vd, p = s.describe(0, 0, 0)
+    ref, _, st = oracle.render(sd, vd, p, threads=4)
+    assert st["adaptive_lanes"] > 0
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_adaptive_pass_shards(oracle, amvpt_mod):
+    """Pass sharding keeps the adaptive fill local: each pass compacts only its own lanes."""
+    kw = dict(res=16, spp=16, gx=2, gy=2, reuse=4, adaptive=1)
+    got = _run("pass", kw=kw)
+    s = amvpt_mod.load_file(CBOX, **dict(kw, spp=32))
+    sd, vd, p = s.describe(0, 0, 0)
     ref, _, _ = oracle.render(sd, vd, p, threads=4)
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
