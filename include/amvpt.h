@@ -239,6 +239,10 @@ amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes);
 /* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane), 1 force wave-uniform,
  * 2 force per-lane.  Results are identical in every mode (closest hit = min (t, prim)). */
 amvpt_status amvpt_set_traversal(uint32_t mode);
+/* BVH build of later amvpt_scene_create calls: leaves keep up to max_leaf_prims (1..15,
+ * default 4) primitives unless splitting is cheaper; a split costs traversal_cost
+ * primitive tests per unit area (default 0).  Hits are identical for every shape. */
+amvpt_status amvpt_set_bvh_build(uint32_t max_leaf_prims, float traversal_cost);
 
 /*
  * Adaptive fill over a lane range (adaptive > 0 with lane_begin/lane_end not the

@@ -98,7 +98,7 @@ def hip_lib():
         for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
                    "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
                    "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal",
-                   "amvpt_set_adaptive_exchange"):
+                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build"):
             if hasattr(L, fn):   # older variant builds (AMVPT_LIB_DIR A/B runs) may lack the newest knobs
                 getattr(L, fn).restype = ctypes.c_int
         L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,
@@ -112,6 +112,8 @@ def hip_lib():
                                  ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.amvpt_develop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u32, u32, u32, ctypes.c_void_p]
         L.amvpt_set_chunk_lanes.argtypes = [u64]
+        if hasattr(L, "amvpt_set_bvh_build"):
+            L.amvpt_set_bvh_build.argtypes = [u32, ctypes.c_float]
         if hasattr(L, "amvpt_set_adaptive_exchange"):
             L.amvpt_set_adaptive_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.amvpt_set_device.argtypes = [ctypes.c_int]
@@ -239,6 +241,12 @@ def set_traversal(mode):
     """BVH walk: 0 auto, 1 wave-uniform, 2 per-lane (amvpt_set_traversal)."""
     L = hip_lib()
     _check(L.amvpt_set_traversal(u32(mode)), L)
+
+
+def set_bvh_build(max_leaf_prims=4, traversal_cost=0.0):
+    """SAH shape of later DeviceScene builds (amvpt_set_bvh_build)."""
+    L = hip_lib()
+    _check(L.amvpt_set_bvh_build(u32(max_leaf_prims), ctypes.c_float(traversal_cost)), L)
 
 
 def set_chunk_lanes(n):

@@ -63,6 +63,12 @@ struct BuildPrim { Box box; float c[3]; uint32_t idx; };
 /* Binary SAH tree as built (children of inner node i at left, left + 1). */
 struct BNode { Box box; uint32_t left_or_first, count; };
 
+/* SAH shape: leaves of up to g_bvh_max_leaf primitives are kept when the split is
+ * not cheaper; a split costs g_bvh_trav_cost primitive tests per unit of area on top
+ * of the children's tests (amvpt_set_bvh_build). */
+static uint32_t g_bvh_max_leaf = 4;
+static float g_bvh_trav_cost = 0.f;
+
 struct Builder {
     std::vector<BuildPrim> &prims;
     std::vector<BNode> nodes;
@@ -114,10 +120,11 @@ struct Builder {
             }
         }
         float leaf_cost = b.area() * n;
-        if (best_axis < 0 || (n <= 4 && best_cost >= leaf_cost)) {
+        best_cost += g_bvh_trav_cost * b.area();
+        if (best_axis < 0 || (n <= g_bvh_max_leaf && best_cost >= leaf_cost)) {
             if (best_axis < 0) {
                 /* degenerate centroids: median split on the index */
-                if (n <= 4) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
+                if (n <= g_bvh_max_leaf) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
                 uint32_t mid = begin + n / 2;
                 uint32_t l = (uint32_t) nodes.size();
                 nodes.resize(nodes.size() + 2);
@@ -203,6 +210,16 @@ amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes) {
 amvpt_status amvpt_set_traversal(uint32_t mode) {
     if (mode > 2) { set_error("amvpt_set_traversal: mode must be 0 (auto), 1 (wave-uniform) or 2 (per-lane)"); return AMVPT_ERR_INVALID; }
     g_traversal = mode;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_set_bvh_build(uint32_t max_leaf_prims, float traversal_cost) {
+    if (max_leaf_prims < 1 || max_leaf_prims > kMaxLeafPrims || !(traversal_cost >= 0.f)) {
+        set_error("amvpt_set_bvh_build: max_leaf_prims in [1, 15], traversal_cost >= 0");
+        return AMVPT_ERR_INVALID;
+    }
+    g_bvh_max_leaf = max_leaf_prims;
+    g_bvh_trav_cost = traversal_cost;
     return AMVPT_OK;
 }
 

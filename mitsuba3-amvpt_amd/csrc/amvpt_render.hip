@@ -422,32 +422,33 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
  * the window is flushed once with global float atomics (skipping cells that
  * received nothing), so the film sees about one atomic per touched
  * pixel-channel per block instead of one per sample.  Footprints that do not
- * fit the window fall back to direct global atomics.  The per-cell weights are
- * exactly those of film_put (imageblock.cpp:174-559).
+ * fit the window fall back to direct global atomics.  The per-cell weights and
+ * the per-cell products value * weight are exactly those of film_put
+ * (imageblock.cpp:174-559); only the order of the additions differs.
  *
- * LDS float adds: gfx950's ds_add_f32 retires ~0.33 lanes/clk/CU
- * (tools/ubench_lds.hip) -- 40x slower than ds_add_u32 -- so the window holds
- * channel PAIRS (R,G), (B,W|A), (W,-) as 64-bit words updated with
- * ds_cmpst_rtn_b64 (compare-and-swap on the bit pattern): one read and one CAS
- * per pair, retried only when another lane changed the word in between.
- * Bit-pattern comparison keeps NaN contributions terminating and propagating.
+ * LDS adds on gfx950 (tools/ubench_lds.hip, lane-ops/clk/CU, distinct 8-byte
+ * words): ds_add_f32 0.33, a 64-bit compare-and-swap of a float pair 1.55 (3.1
+ * channel adds), ds_add_f64 7.4.  The window therefore holds one fp64 word per
+ * cell and channel and every contribution is one fire-and-forget ds_add_f64
+ * (no return value, no retry loop, NaN/Inf propagate as in fp32).  The f32
+ * products are exact in fp64 and the window sum is rounded once to f32 at the
+ * flush -- a block's sum is at least as accurate as the reference's sequential
+ * fp32 scatter_reduce.
  *
- * The window is double-buffered (view k uses buffer k & 1) and the flush
- * writes zeros back, so one put costs two block barriers and no zeroing pass.
+ * The flush writes zeros back, so one put costs two block barriers and no zeroing
+ * pass; the window is single-buffered (the next put's first barrier orders its
+ * adds after this flush), only the tiny bounding-box exchange alternates buffers.
  */
 constexpr int kWinW = 96, kWinH = 16, kMaxWaves = 16, kMaxFoot = 5;
 constexpr int kSplatBlock = 512;   /* threads per splat block (see slot_lane) */
 constexpr int kWinCells = kWinW * kWinH;
 template <int C> struct SplatLds {
-    static constexpr int NP = (C + 1) / 2;  /* channel pairs per cell */
-    uint64_t win[2][kWinCells * NP];        /* pair p of cell c at win[b][p * plane + c] */
-    uint64_t dummy[NP * kSplatBlock];       /* per-lane sink for clipped footprint cells */
+    double win[kWinCells * C];              /* channel k of cell c at win[k * plane + c] */
     alignas(16) int bb[2][kMaxWaves][4];
 };
 
 template <int C> AD void splat_lds_init(SplatLds<C> &L) {
-    uint64_t *w = &L.win[0][0];
-    for (int c = threadIdx.x; c < 2 * kWinCells * SplatLds<C>::NP; c += blockDim.x) w[c] = 0ull;
+    for (int c = threadIdx.x; c < kWinCells * C; c += blockDim.x) L.win[c] = 0.0;
     __syncthreads();
 }
 
@@ -503,15 +504,10 @@ AD int wave_max(int v) {
     return v;
 }
 
-AD uint64_t pair_add(uint64_t w, float a, float b) {
-    const float lo = __uint_as_float((uint32_t) w) + a, hi = __uint_as_float((uint32_t) (w >> 32)) + b;
-    return (uint64_t) __float_as_uint(lo) | ((uint64_t) __float_as_uint(hi) << 32);
+/* ds_add_f64, result unused (the backend emits the no-return form) */
+AD void lds_add64(double *p, double v) {
+    (void) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-AD bool lds_cas64(uint64_t *p, uint64_t &expect, uint64_t nw) {
-    return __hip_atomic_compare_exchange_strong(p, &expect, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-AD uint64_t lds_load64(uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
 /*
  * Block-cooperative put into window buffer `buf`.  Cells xs in [0, nx) x ys in
@@ -522,7 +518,6 @@ AD uint64_t lds_load64(uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAX
 template <int C>
 AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float px, float py, const float *vals,
                   bool valid, bool coalesce, unsigned long long *fallback = nullptr) {
-    constexpr int NP = SplatLds<C>::NP;
     Foot f;
     f.ok = false;
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
@@ -554,7 +549,7 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     const bool any = bx0 != 0x7fffffff && bx0 < bx1;
     const int ww = any ? min(bx1 - bx0, kWinW) : 0, wh = any ? min(by1 - by0, kWinH) : 0;
     const int plane = ww * wh;
-    uint64_t *win = L.win[buf];
+    double *win = L.win;
     if (act) {
         const bool in_win = cx0 >= bx0 && cy0 >= by0 && f.x0 + f.nx <= bx0 + ww && f.y0 + f.ny <= by0 + wh;
         float wx[kMaxFoot], wy[kMaxFoot];
@@ -566,64 +561,21 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
         /* cells per footprint side: uniform over the call (filter radius and method only) */
         const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
         if (in_win && cnt <= kMaxFoot) {
-            /* Straight-line columns: every lane runs cnt x cnt cells; clipped cells are
-             * redirected to the lane's private dummy words so no cell needs its own branch.
-             * One batch = one footprint COLUMN (all reads, then all CAS): the lanes of a wave
-             * hold neighbouring pixels of one film row, whose footprints overlap only at
-             * different column offsets, so a batch never reads a word that a neighbour's CAS
-             * of the same batch changes (batching a ROW would make every such CAS fail).
-             * The CAS that lost a race against another wave is retried below. */
-            uint64_t *const col0 = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
-            uint64_t *const dummy = L.dummy + threadIdx.x;   /* pair q at dummy + q * kSplatBlock */
-            uint32_t rowm = 0;
+            /* straight-line cnt x cnt cells; clipped cells are masked off (no retry, no branch body) */
+            double *const c0 = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
 #pragma unroll
-            for (int ys = 0; ys < kMaxFoot; ++ys) rowm |= (ys < f.ny && f.y0 + ys >= 0) ? 1u << ys : 0u;
+            for (int ys = 0; ys < kMaxFoot; ++ys) {
+                if (ys >= cnt) break;
+                const bool rok = ys < f.ny && f.y0 + ys >= 0;
 #pragma unroll
-            for (int xs = 0; xs < kMaxFoot; ++xs) {
-                if (xs >= cnt) break;
-                const bool cok = xs < f.nx && f.x0 + xs >= 0;
-                uint64_t *base[kMaxFoot];
-                int stride[kMaxFoot];
-                uint32_t okm = 0;   /* cells that are real (not redirected to the dummy) */
+                for (int xs = 0; xs < kMaxFoot; ++xs) {
+                    if (xs >= cnt) break;
+                    if (rok && xs < f.nx && f.x0 + xs >= 0) {
+                        const float w = wx[xs] * wy[ys];
+                        double *const cp = c0 + ys * ww + xs;
 #pragma unroll
-                for (int ys = 0; ys < kMaxFoot; ++ys) {
-                    const bool ok = cok && (rowm >> ys & 1u);
-                    okm |= ok ? 1u << ys : 0u;
-                    base[ys] = ok ? col0 + ys * ww + xs : dummy;
-                    stride[ys] = ok ? plane : kSplatBlock;
-                }
-                uint64_t o[kMaxFoot][NP];
-#pragma unroll
-                for (int ys = 0; ys < kMaxFoot; ++ys) {
-                    if (ys >= cnt) break;
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) o[ys][q] = lds_load64(base[ys] + q * stride[ys]);
-                }
-                uint32_t fail = 0;
-#pragma unroll
-                for (int ys = 0; ys < kMaxFoot; ++ys) {
-                    if (ys >= cnt) break;
-                    const float w = wx[xs] * wy[ys];
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) {
-                        const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
-                        const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
-                        /* several clipped cells share the dummy word: their CAS may "fail", ignore it */
-                        if (!lds_cas64(base[ys] + q * stride[ys], o[ys][q], pair_add(o[ys][q], a0, a1)) &&
-                            (okm >> ys & 1u))
-                            fail |= 1u << (ys * NP + q);
+                        for (int k = 0; k < C; ++k) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
                     }
-                }
-                while (fail) {
-                    const int bit = __builtin_ctz(fail);
-                    const int ys = bit / NP, q = bit - ys * NP;
-                    const float w = wx[xs] * wy[ys];
-                    const float a0 = P.box ? vals[2 * q] : vals[2 * q] * w;
-                    const float a1 = (2 * q + 1 < C) ? (P.box ? vals[2 * q + 1] : vals[2 * q + 1] * w) : 0.f;
-                    uint64_t *cp = col0 + ys * ww + xs + q * plane;
-                    uint64_t e = lds_load64(cp);
-                    while (!lds_cas64(cp, e, pair_add(e, a0, a1))) {}
-                    fail &= fail - 1u;
                 }
             }
         } else {
@@ -647,7 +599,6 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     }
     __syncthreads();
     /* flush + re-zero: consecutive threads take consecutive floats of the film row segment */
-    float *wf = reinterpret_cast<float *>(win);
     const int rowlen = ww * C;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     float *film0 = film + ((size_t) by0 * P.W + (size_t) bx0) * C;
@@ -656,11 +607,11 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
         cy -= (cy * rowlen > e) ? 1 : 0;
         cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
         const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
-        const int cell = cy * ww + cx;
-        float *src = wf + 2 * ((k >> 1) * plane + cell) + (k & 1);
-        const float v = *src;
-        if (__float_as_uint(v) != 0u) {
-            *src = 0.f;
+        double *src = win + k * plane + cy * ww + cx;
+        const double d = *src;
+        if (__double_as_longlong(d) != 0ll) {
+            *src = 0.0;
+            const float v = (float) d;
             if (v != 0.f || v != v) film_add(film0 + (size_t) cy * P.W * C + r, v);
         }
     }

@@ -38,6 +38,30 @@ __global__ __launch_bounds__(1024) void k(float* out, int stride) {
             unsigned old = *p;
             while (!__hip_atomic_compare_exchange_strong(p, &old, __float_as_uint(__uint_as_float(old) + v), __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {}
         }
+        else if (MODE == 11) atomicAdd((double*)&s[a & ~1], (double)v);
+        else if (MODE == 12) {   /* fixed-point (32 fractional bits) f32 -> u64, ds_add_u64 */
+            const float x = v * 4294967296.f;
+            const unsigned hi = (unsigned)(x * 2.3283064365386963e-10f);
+            const unsigned lo = (unsigned)__builtin_fmaf(-(float)hi, 4294967296.f, x);
+            atomicAdd((unsigned long long*)&s[a & ~1], ((unsigned long long)hi << 32) + lo);
+        }
+        else if (MODE == 13) {   /* 64-bit CAS of a float pair (the current splat window) */
+            unsigned long long* p = (unsigned long long*)&s[a & ~1];
+            unsigned long long old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            while (true) {
+                unsigned long long nw = (unsigned long long)__float_as_uint(__uint_as_float((unsigned)old) + v) |
+                                        ((unsigned long long)__float_as_uint(__uint_as_float((unsigned)(old >> 32)) + v) << 32);
+                if (__hip_atomic_compare_exchange_strong(p, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            }
+        }
+        else if (MODE == 14) atomicAdd((unsigned long long*)&s[(a * 2) & (kLds - 2)], (unsigned long long)(lane + 1));
+        else if (MODE == 15) atomicAdd((double*)&s[(a * 2) & (kLds - 2)], (double)v);
+        else if (MODE == 16) {
+            const float x = v * 4294967296.f;
+            const unsigned hi = (unsigned)(x * 2.3283064365386963e-10f);
+            const unsigned lo = (unsigned)__builtin_fmaf(-(float)hi, 4294967296.f, x);
+            atomicAdd((unsigned long long*)&s[(a * 2) & (kLds - 2)], ((unsigned long long)hi << 32) + lo);
+        }
         else if (MODE == 8) { float x = s[a]; __builtin_amdgcn_s_waitcnt(0); s[a] = x + v; }
     }
     __syncthreads();
@@ -63,6 +87,17 @@ void run(const char* name, int stride, int block) {
 }
 
 int main() {
+    for (int bs : {512}) {
+        run<5>("ds_add_u64 distinct", 1, bs);
+        run<14>("ds_add_u64 distinct 8B-stride", 1, bs);
+        run<11>("ds_add_f64 distinct", 1, bs);
+        run<15>("ds_add_f64 distinct 8B-stride", 1, bs);
+        run<16>("fixed-point cvt + u64 8B-stride", 1, bs);
+        run<12>("fixed-point cvt + ds_add_u64", 1, bs);
+        run<13>("CAS64 pair add distinct", 1, bs);
+        run<4>("ds_add_u32 distinct", 1, bs);
+        run<9>("CAS-loop f32 add distinct", 1, bs);
+    }
     for (int bs : {256, 1024}) {
         run<0>("ds_add_f32 distinct", 1, bs);
         run<0>("ds_add_f32 distinct", 3, bs);
