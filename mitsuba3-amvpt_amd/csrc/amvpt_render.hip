@@ -69,7 +69,8 @@ struct KParams {
 struct Bufs {
     float4 *q_in[6];
     float4 *q_out[6];
-    uint32_t *cnt_in, *cnt_out;
+    uint32_t *cnt_in, *cnt_out;  /* kQParts partition counters each, kCntStride words apart */
+    uint32_t qcap;               /* entries per queue partition */
     float4 *lane_out;     /* (indirect / result rgb, valid_ray) */
     float4 *lane_rec;     /* (pdfW, flags) */
     float4 *view_rec;     /* [3][G][n]: (pos, weight, flags), (result), (bsdf_val) */
@@ -78,6 +79,11 @@ struct Bufs {
     unsigned long long *stats; /* [0] vertices [1] reuse lanes [2] visibility rays [3] splats */
     uint8_t *amask;       /* adaptive: per-lane adapt_mask of the pass (lane order), or null */
     const uint32_t *asel; /* adaptive: compacted lanes with adapt_mask (ascending) */
+    float4 *hit;          /* k_extend / k_prim_hit -> shading: closest hit (t, u, v, prim) per entry */
+    float4 *nee[4];       /* k_bounce -> k_shadow: deferred emitter-sample shadow rays (NEE records) */
+    uint32_t *cnt_nee;
+    float4 *vreq[3];      /* k_prim_req -> k_vis: (p, bits), (n, ap.x), (emitter point, ap.y) per lane */
+    unsigned long long *occ; /* k_vis -> k_mv_primary: occlusion ballots, word (i >> 6) * G + slot */
 };
 
 /* ------------------------------------------------------------------ */
@@ -131,7 +137,7 @@ template <typename T> AD T *copy_to_lds(const T *src, uint32_t bytes, char *&dst
  * lane-divergent reads then hit LDS instead of L1/L2.  S is the kernel's local
  * copy of the scene header; its table pointers are redirected.
  */
-template <bool kTab>
+template <bool kTab, bool kBvh = true>
 AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0) {
     SceneRef sc;
     sc.g = &S;
@@ -143,7 +149,7 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.prims = S.prims;
     char *dst = lds;
     bool sync = false;
-    if (scene_staged(S.n_nodes, S.lds_bytes, mode)) {
+    if (kBvh && scene_staged(S.n_nodes, S.lds_bytes, mode)) {
         const uint32_t nn = S.n_nodes * (uint32_t) sizeof(DNode) / 16, np = S.n_prims * (uint32_t) sizeof(DPrim) / 16;
         float4 *d4 = (float4 *) lds;
         const float4 *sn = (const float4 *) S.nodes, *spr = (const float4 *) S.prims;
@@ -167,7 +173,8 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     return sc;
 }
 
-AD SI intersect(const SceneRef &sc, const Ray &r) { return compute_si(sc, r, trace_closest(sc, r)); }
+AD Hit hit_of(float4 h) { return Hit{h.x, h.y, h.z, (int32_t) fbits(h.w)}; }
+AD float4 hit_rec(const Hit &h) { return make_float4(h.t, h.u, h.v, bitsf((uint32_t) h.prim)); }
 
 /* ------------------------------------------------------------------ */
 /* Emitters at scene level                                            */
@@ -183,12 +190,19 @@ AD C3 emitter_eval(const SceneRef &sc, int32_t e, const SI &si, bool active) {
     return c3(sc.g->emitters[e].radiance);
 }
 
-AD void sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, float u2, bool active, DSamp &ds,
+/*
+ * Scene::sample_emitter_direction (scene.cpp:294-348) up to its ray_test: returns
+ * true when the reference would trace the shadow ray spawn_ray_to(ref.p, ref.n,
+ * ds.p).  The test itself runs in its own wavefront (k_vis slot 0 for primary
+ * vertices, k_shadow for suffix vertices); an occluded sample is then zeroed
+ * exactly as the reference does (spec = 0, ds.pdf = 0).
+ */
+AD bool sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, float u2, bool active, DSamp &ds,
                                  C3 &spec) {
     ds = ds_zero();
     spec = c3(0.f);
     uint32_t n = sc.g->n_emitters;
-    if (n == 0) return;
+    if (n == 0) return false;
     uint32_t index = 0;
     float weight = 1.f;
     if (n >= 2) {
@@ -197,7 +211,7 @@ AD void sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, fl
         weight = (float) n;
         u1 = scaled - (float) index;
     }
-    if (!active) return;
+    if (!active) return false;
     const DEmitter &em = sc.g->emitters[index];
     const DShape &s = sc.g->shapes[em.shape];
     ds = shape_sample_direction(s, ref.p, u1, u2);
@@ -206,11 +220,9 @@ AD void sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, fl
     ds.emitter = (int32_t) index;
     ds.pdf *= sc.g->emitter_pmf;
     spec = spec * weight;
-    if (ds.pdf != 0.f) {
-        Ray r = spawn_ray_to(ref.p, ref.n, ds.p);
-        if (trace_any(sc, r)) { spec = c3(0.f); ds.pdf = 0.f; }
-    }
+    return ds.pdf != 0.f;
 }
+AD void occlude_emitter_sample(DSamp &ds, C3 &spec) { spec = c3(0.f); ds.pdf = 0.f; }
 
 AD float pdf_emitter_direction(const SceneRef &sc, f3 refp, const DSamp &ds, bool active) {
     if (ds.emitter < 0 || !active) return 0.f;
@@ -355,6 +367,13 @@ AD Surf thin_sample_surface(const DView &v, const SI &it, bool active, float apx
 AD Surf camera_sample_surface(const DView &v, const SI &it, bool active, float apx, float apy) {
     return v.type == AMVPT_CAMERA_THINLENS ? thin_sample_surface(v, it, active, apx, apy)
                                            : persp_sample_surface(v, it, active);
+}
+/* Surf::p of camera_sample_surface (the visibility-ray target), bit for bit */
+AD f3 camera_point(const DView &v, float apx, float apy) {
+    if (v.type != AMVPT_CAMERA_THINLENS) return xf_point_affine(v.to_world, mk(0.f, 0.f, 0.f));
+    float tx, ty;
+    disk_concentric(apx, apy, tx, ty);
+    return xf_point_affine(v.to_world, mk(tx * v.aperture_radius, ty * v.aperture_radius, 0.f));
 }
 
 /* ------------------------------------------------------------------ */
@@ -672,10 +691,26 @@ AD unsigned long long wave_sum(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += (unsigned long long) __shfl_xor((long long) v, o);
     return v;
 }
-AD void stat_add(unsigned long long *ctr, unsigned long long v) {
+/* lane counters: stats[s * kStatShards + shard], one shard per block residue (summed on
+ * the host), so the per-wave adds never pile onto one word */
+constexpr uint32_t kStatShards = 256, kStats = 8;
+AD void stat_add(unsigned long long *stats, uint32_t which, unsigned long long v) {
     v = wave_sum(v);
-    if (__lane_id() == 0 && v) atomicAdd(ctr, v);
+    if (__lane_id() == 0 && v) atomicAdd(stats + which * kStatShards + blockIdx.x % kStatShards, v);
 }
+
+/*
+ * Partitioned queues.  A returning device-scope atomic on ONE word saturates at
+ * about 88 per microsecond on MI355X (MI355X_MICROARCH.md, "dequeue"), far below
+ * the tens of millions of wave-level pushes a frame makes, so every queue (path
+ * queues, NEE queue) is split into kQParts partitions with one counter each, on
+ * its own 64-B line.  Block b of a producer appends to partition b % kQParts; block
+ * b of a consumer grid (a multiple of kQParts blocks) reads partition b % kQParts,
+ * striding over it with the gridDim / kQParts blocks of that partition, and writes
+ * its survivors to the same partition of the next queue, so a partition never
+ * outgrows its initial fill (<= qcap entries, see render_impl).
+ */
+constexpr uint32_t kQParts = 256, kCntStride = 16;
 
 /* Wave-aggregated slot allocation: one atomic per wave (ballot + mbcnt). */
 AD uint32_t queue_slot(bool want, uint32_t *counter) {
@@ -688,6 +723,11 @@ AD uint32_t queue_slot(bool want, uint32_t *counter) {
     base = (uint32_t) __shfl((int) base, (int) leader);
     uint32_t rank = (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
     return base + rank;
+}
+/* global index of a new entry in this block's partition */
+AD uint32_t push_slot(bool want, uint32_t *counters, uint32_t qcap) {
+    const uint32_t p = blockIdx.x % kQParts;
+    return p * qcap + queue_slot(want, counters + p * kCntStride);
 }
 
 struct PathState {
@@ -774,7 +814,7 @@ __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V
             ok = false;
         }
     }
-    uint32_t qslot = queue_slot(ok, B.cnt_out);
+    uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
     if (ok) store_state(B.q_out, qslot, s);
 }
 
@@ -824,13 +864,74 @@ __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V,
             ok = false;
         }
     }
-    uint32_t qslot = queue_slot(ok, B.cnt_out);
+    uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
     if (ok) store_state(B.q_out, qslot, s);
 }
 
 /* ------------------------------------------------------------------ */
 /* k_bounce: one loop iteration (mvpath_multi.h:563-686 == mvpath_single.h:130-275) */
 /* ------------------------------------------------------------------ */
+
+/*
+ * The suffix loop body (mvpath_multi.h:563-686 == mvpath_single.h:130-275) runs as
+ * three wavefronts per depth, so that no kernel holds both a BVH walk and the
+ * shading state (each walk runs at high occupancy to hide its node-load latency):
+ *   k_extend   closest hit of every live path's ray        (Scene::ray_intersect)
+ *   k_bounce   emitter-hit MIS, emitter sample, BSDF eval/sample, Russian roulette,
+ *              compaction of the survivors; the emitter sample's shadow ray goes to
+ *              the NEE queue with the pre-bounce throughput and its contribution
+ *   k_shadow   the NEE ray_test (Scene::sample_emitter_direction's test); if the
+ *              light is visible, result = fma(throughput, contribution, result)
+ *              in the path's next state (or its final lane record)
+ * The accumulation order of a lane's result is the reference's: emitter hit of
+ * vertex d, then NEE of vertex d, then vertex d + 1.
+ */
+template <bool kUni>
+__global__ void __launch_bounds__(256) k_extend(KParams P, const DScene *Sp, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
+    const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
+    /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
+    if (blockIdx.x == 0) {
+        for (uint32_t q = threadIdx.x; q < kQParts; q += blockDim.x) { B.cnt_out[q * kCntStride] = 0u; B.cnt_nee[q * kCntStride] = 0u; }
+    }
+    for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
+        const uint32_t i = pbase + e0 + threadIdx.x;
+        if (e0 + threadIdx.x < count) {
+            const float4 a = B.q_in[0][i], b = B.q_in[1][i];
+            const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest};
+            B.hit[i] = hit_rec(trace_closest<kUni>(sc, r));
+        }
+    }
+}
+
+template <bool kUni>
+__global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
+    const uint32_t count = B.cnt_nee[part * kCntStride], pbase = part * B.qcap;
+    for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
+        const uint32_t i = pbase + e0 + threadIdx.x;
+        if (e0 + threadIdx.x < count) {
+            const float4 a = B.nee[0][i], b = B.nee[1][i];
+            const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z};
+            if (!trace_any<kUni>(sc, r)) {
+                const float4 t = B.nee[2][i], c = B.nee[3][i];
+                const uint32_t dest = fbits(b.w);
+                float4 *const dp = (dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest];
+                float4 v = *dp;
+                v.x = fmadd(t.x, c.x, v.x);
+                v.y = fmadd(t.y, c.y, v.y);
+                v.z = fmadd(t.z, c.z, v.z);
+                *dp = v;
+            }
+        }
+    }
+}
 
 #ifndef AMVPT_BOUNCE_WAVES
 #define AMVPT_BOUNCE_WAVES 4
@@ -839,21 +940,24 @@ template <bool kTab>
 __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<kTab>(S, lds, P.trav_mode);
-    const uint32_t count = *B.cnt_in;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode);
+    const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
+    const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     unsigned long long verts = 0;
-    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < count; i0 += gridDim.x * blockDim.x) {
-        uint32_t i = i0 + threadIdx.x;
-        bool ok = i < count;
+    for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
+        const uint32_t i = pbase + e0 + threadIdx.x;
+        bool ok = e0 + threadIdx.x < count;
         PathState s;
-        bool keep = false;
+        bool keep = false, nee = false;
+        Ray shr;
+        C3 nee_thr, nee_c;
         if (ok) {
             s = load_state(B.q_in, i);
             Pcg rng;
             rng.state = s.rng_state;
             rng.inc = (((uint64_t) s.rng_seq) << 1) | 1u;
             ++verts;
-            SI si = intersect(sc, s.ray);
+            SI si = compute_si(sc, s.ray, hit_of(B.hit[i]));
             int32_t em = si_emitter(sc, si);
             {
                 DSamp ds = ds_zero();
@@ -873,7 +977,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             DSamp ds;
             C3 em_w;
             sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
-            active_em = active_em && ds.pdf != 0.f;
+            active_em = active_em && ds.pdf != 0.f;   /* ds.pdf != 0 <=> the reference traces the ray */
             f3 wo = si.sh.to_local(ds.d);
             float s1 = rng.next_1d();
             float s2a = rng.next_1d(), s2b = rng.next_1d();
@@ -884,9 +988,12 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             BSample bs;
             C3 bw;
             bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
-            {
+            if (active_em) {
                 float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
-                if (active_em) s.res = cfma(s.thr, bval * em_w * mis_em, s.res);
+                nee = true;
+                nee_thr = s.thr;
+                nee_c = bval * em_w * mis_em;
+                shr = spawn_ray_to(si.p, si.n, ds.p);
             }
             s.ray = spawn_ray(si.p, si.n, si.sh.to_world(bs.wo));
             s.thr = s.thr * bw;
@@ -905,10 +1012,18 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             s.rng_state = rng.state;
             if (!keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
         }
-        uint32_t slot = queue_slot(keep, B.cnt_out);
+        const uint32_t slot = push_slot(keep, B.cnt_out, B.qcap);
         if (keep) store_state(B.q_out, slot, s);
+        const uint32_t ns = push_slot(nee, B.cnt_nee, B.qcap);
+        if (nee) {
+            const uint32_t dest = keep ? slot : (0x80000000u | s.idx);
+            B.nee[0][ns] = make_float4(shr.o.x, shr.o.y, shr.o.z, shr.d.x);
+            B.nee[1][ns] = make_float4(shr.d.y, shr.d.z, shr.maxt, bitsf(dest));
+            B.nee[2][ns] = make_float4(nee_thr.r, nee_thr.g, nee_thr.b, 0.f);
+            B.nee[3][ns] = make_float4(nee_c.r, nee_c.g, nee_c.b, 0.f);
+        }
     }
-    if (B.stats) stat_add(&B.stats[0], verts);
+    if (B.stats) stat_add(B.stats, 0, verts);
 }
 
 /* ------------------------------------------------------------------ */
@@ -963,6 +1078,130 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_adapt(KParams P, Bufs B) 
         pack_vals(P, C3{w * lo.x, w * lo.y, w * lo.z}, 1.f, w, vals);
     }
     block_put<C>(P, B.film, L, 0, sx, sy, vals, ok, false);
+}
+
+/* ------------------------------------------------------------------ */
+/* Primary vertex of render_multisample (mvpath_multi.h:8-38)          */
+/* ------------------------------------------------------------------ */
+
+/* jitter, [aperture], sample_ray_idx of lane-order thread i of the chunk */
+struct PrimRay {
+    Pcg rng;
+    uint32_t v1, p_idx;
+    float sx, sy, apx, apy;
+    Ray ray;
+};
+AD PrimRay primary_raygen(const KParams &P, const DView *V, uint32_t i) {
+    PrimRay r;
+    const uint32_t lane = (uint32_t) (P.chunk_begin + i);
+    int px, py;
+    lane_pixel(P, lane, px, py);
+    uint32_t v0;
+    tea4(P.seed_value, lane, v0, r.v1);
+    r.rng.seed(v0, r.v1);
+    const float jx = r.rng.next_1d(), jy = r.rng.next_1d();
+    r.sx = (float) px + jx;
+    r.sy = (float) py + jy;
+    r.apx = r.apy = .5f;   /* aperture sample: raygen and every view's sample_surface */
+    if (P.needs_ap) { r.apx = r.rng.next_1d(); r.apy = r.rng.next_1d(); }
+    r.ray = sample_ray_idx(P, V, fmadd(r.sx, P.inv_w, -0.f), fmadd(r.sy, P.inv_h, -0.f), r.p_idx, r.apx, r.apy);
+    return r;
+}
+/* view index of group slot k of a lane whose primary view is p_idx (mvpath_multi.h:31-38) */
+template <int G> AD uint32_t group_view(uint32_t p_idx, int k) {
+    const uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u), id = p_idx + (uint32_t) k;
+    return id < max_idx ? id : id - (uint32_t) G;
+}
+/* k_vis's verdict for slot k of lane-order thread i (0: emitter shadow ray, k >= 1: view k) */
+template <int G> AD bool occluded(const Bufs &B, uint32_t i, int k) {
+    return (B.occ[(size_t) (i >> 6) * G + (uint32_t) k] >> (i & 63u)) & 1ull;
+}
+
+/*
+ * The primary vertex runs as four wavefronts (the BVH walks get their own launches):
+ *   k_prim_hit   raygen + closest hit                         -> hit
+ *   k_prim_req   the rays the reference traces at this vertex: the emitter sample's
+ *                shadow ray (scene.cpp:338) and one visibility ray per view of the
+ *                group that passes sensors_visible's geometric tests (mvpath.h:243-256)
+ *   k_vis        those rays, one wave per (64 lanes, slot): any-hit -> occlusion ballots
+ *   k_mv_primary the whole vertex (camera_selection, mis_weights, direct light,
+ *                mixture pdf) with the ray tests read from the ballots
+ * k_prim_req and k_mv_primary evaluate the same functions on the same inputs, so the
+ * traced rays are exactly the reference's.
+ */
+template <bool kUni>
+__global__ void __launch_bounds__(256) k_prim_hit(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < P.chunk_n && P.max_depth != 0) {
+        const PrimRay pr = primary_raygen(P, V, i);
+        B.hit[i] = hit_rec(trace_closest<kUni>(sc, pr.ray));
+    }
+}
+
+template <int G, bool kTab>
+__global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.chunk_n) return;
+    PrimRay pr = primary_raygen(P, V, i);
+    uint32_t bits = 0;
+    f3 p = mk(0.f, 0.f, 0.f), n = p, dsp = p;
+    if (P.max_depth != 0) {
+        const SI si = compute_si(sc, pr.ray, hit_of(B.hit[i]));
+        const bool p_hit = si.valid();
+        const bool direct_em = si_emitter(sc, si) >= 0;
+        const int32_t b = p_hit ? S.shapes[si.shape].bsdf : -1;
+        const bool bsdf_smooth = (bsdf_flags(S.bsdfs, b) & BF_Smooth) != 0;
+        const float e1 = pr.rng.next_1d(), e2 = pr.rng.next_1d();
+        DSamp ds;
+        C3 em_w;
+        if (sample_emitter_direction(sc, si, e1, e2, p_hit && bsdf_smooth, ds, em_w)) bits |= 1u;
+        (void) pr.rng.next_1d();   /* rand_1 */
+        const float r2a = pr.rng.next_1d(), r2b = pr.rng.next_1d();
+        BSample bsmp;
+        C3 bsdf_weight;
+        bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, r2a, r2b, true, bsmp, bsdf_weight);
+        const bool delta = (bsmp.type & BF_Delta) != 0 || (bsmp.type & BF_Null) != 0;
+        const bool reuse = !direct_em && !delta && p_hit && bsdf_smooth;
+        const bool p_face = si.wi.z > 0.f;
+#pragma unroll 1
+        for (int k = 1; k < G; ++k) {
+            const Surf r = camera_sample_surface(V[group_view<G>(pr.p_idx, k)], si, reuse, pr.apx, pr.apy);
+            if (r.valid && (r.face == p_face) && r.Jp > 0.f) bits |= 1u << k;
+        }
+        p = si.p; n = si.n; dsp = ds.p;
+    }
+    bits |= pr.p_idx << 16;
+    B.vreq[0][i] = make_float4(p.x, p.y, p.z, bitsf(bits));
+    B.vreq[1][i] = make_float4(n.x, n.y, n.z, pr.apx);
+    B.vreq[2][i] = make_float4(dsp.x, dsp.y, dsp.z, pr.apy);
+}
+
+/* one block = 64 lanes x G slots, wave k traces slot k of the block's 64 lanes */
+template <int G, bool kUni>
+__global__ void __launch_bounds__(64 * G) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    const int k = (int) (threadIdx.x >> 6);
+    const uint32_t i = blockIdx.x * 64u + (threadIdx.x & 63u);
+    bool occ = false;
+    if (i < P.chunk_n) {
+        const float4 a = B.vreq[0][i];
+        const uint32_t bits = fbits(a.w);
+        if ((bits >> k) & 1u) {
+            const float4 nn = B.vreq[1][i], d = B.vreq[2][i];
+            const f3 target = k == 0 ? mk(d.x, d.y, d.z) : camera_point(V[group_view<G>(bits >> 16, k)], nn.w, d.w);
+            occ = trace_any<kUni>(sc, spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target));
+        }
+    }
+    const unsigned long long m = __ballot(occ);
+    if ((threadIdx.x & 63u) == 0u) B.occ[(size_t) blockIdx.x * G + (uint32_t) k] = m;
 }
 
 /* ------------------------------------------------------------------ */
@@ -1025,8 +1264,8 @@ template <int G, bool kTab>
 __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    const uint32_t vs_off = scene_lds_bytes(S, P.trav_mode) + (kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u);
-    SceneRef sc = stage_scene<kTab>(S, lds, P.trav_mode, &V, P.n_views);
+    const uint32_t vs_off = kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
     float *const vs = reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
 #define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
@@ -1040,27 +1279,15 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
     unsigned long long st_reuse = 0, st_vis = 0;
     if (ok) {
         const uint32_t n = P.chunk_n;
-        uint32_t lane = (uint32_t) (P.chunk_begin + i);
-        int px, py;
-        lane_pixel(P, lane, px, py);
-        uint32_t v0, v1;
-        tea4(P.seed_value, lane, v0, v1);
-        Pcg rng;
-        rng.seed(v0, v1);
-        float jx = rng.next_1d(), jy = rng.next_1d();
-        float sx = (float) px + jx, sy = (float) py + jy;
-        float apx = .5f, apy = .5f;   /* aperture sample: raygen and every view's sample_surface */
-        if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
-        uint32_t p_idx;
-        Ray pray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), p_idx, apx, apy);
-        const uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u);
+        const PrimRay pr = primary_raygen(P, V, i);
+        Pcg rng = pr.rng;
+        const uint32_t v1 = pr.v1, p_idx = pr.p_idx;
+        const float sx = pr.sx, sy = pr.sy, apx = pr.apx, apy = pr.apy;
+        const Ray pray = pr.ray;
         float4 *const rec0 = B.view_rec, *const rec1 = B.view_rec + (size_t) G * n,
                       *const rec2 = B.view_rec + (size_t) 2 * G * n;
         /* view index of slot k and its film position (quilt offset for k >= 1) */
-        auto view_of = [&](int k) -> uint32_t {
-            uint32_t id = p_idx + (uint32_t) k;
-            return id < max_idx ? id : id - (uint32_t) G;
-        };
+        auto view_of = [&](int k) -> uint32_t { return group_view<G>(p_idx, k); };
         auto put_pos = [&](int k, float x, float y) {
             if (k > 0) {
                 uint32_t id = view_of(k);
@@ -1084,7 +1311,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         float pdfW = 1.f;
         bool should_mis = P.sa_mis != 0;
         if (P.max_depth != 0) {
-            SI si = intersect(sc, pray);
+            SI si = compute_si(sc, pray, hit_of(B.hit[i]));
             bool p_hit = si.valid();
             int32_t em = si_emitter(sc, si);
             bool direct_em = em >= 0;
@@ -1095,7 +1322,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             float e1 = rng.next_1d(), e2 = rng.next_1d();
             DSamp ds;
             C3 em_w;
-            sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
+            if (sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w) && occluded<G>(B, i, 0))
+                occlude_emitter_sample(ds, em_w);
             active_em = active_em && ds.pdf != 0.f;
             f3 wo = si.sh.to_local(ds.d);
             float rand_1 = rng.next_1d();
@@ -1139,8 +1367,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
-                        Ray vr = spawn_ray_to(si.p, si.n, r.p);
-                        valid = !trace_any(sc, vr);
+                        valid = !occluded<G>(B, i, k);
                     }
                     f3 wik = si.sh.to_local(r.d);
                     VSF(F_WX, k) = wik.x; VSF(F_WY, k) = wik.y; VSF(F_WZ, k) = wik.z;
@@ -1219,8 +1446,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
-                        Ray vr = spawn_ray_to(si.p, si.n, r.p);
-                        valid = !trace_any(sc, vr);
+                        valid = !occluded<G>(B, i, k);
                     }
                     put_pos(k, r.uvx, r.uvy);
                     vflags |= valid ? (1u << k) : 0u;
@@ -1315,12 +1541,12 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             }
         }
     }
-    const uint32_t qslot = queue_slot(push, B.cnt_out);
+    const uint32_t qslot = push_slot(push, B.cnt_out, B.qcap);
     if (push) store_state(B.q_out, qslot, ps);
     if (B.stats) {
-        stat_add(&B.stats[1], st_reuse);
-        stat_add(&B.stats[2], st_vis);
-        stat_add(&B.stats[0], (ok && P.max_depth != 0) ? 1ull : 0ull);
+        stat_add(B.stats, 1, st_reuse);
+        stat_add(B.stats, 2, st_vis);
+        stat_add(B.stats, 0, (ok && P.max_depth != 0) ? 1ull : 0ull);
     }
 }
 #undef VSF
@@ -1388,7 +1614,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
             rr[7] = valid ? 1.f : 0.f;
         }
     }
-    if (B.stats) { stat_add(&B.stats[3], splats); stat_add(&B.stats[4], fallback); }
+    if (B.stats) { stat_add(B.stats, 3, splats); stat_add(B.stats, 4, fallback); }
 }
 
 /* develop: rgb / W (hdrfilm.cpp:400) */
@@ -1477,12 +1703,20 @@ struct Arena {
 };
 static Arena g_arena;
 
+/* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
 template <int G>
-static void launch_primary(dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *S, const DView *V,
-                           const Bufs &B, bool tab) {
+static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
+                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni) {
+    const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPrimBlock - 1) / kPrimBlock);
     const size_t lds_view = (size_t) VS_FIELDS * G * kPrimBlock * sizeof(float);
-    if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true>), grid, dim3(kPrimBlock), lds + lds_view, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false>), grid, dim3(kPrimBlock), lds + lds_view, st, P, S, V, B);
+    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
+    if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
+    if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
@@ -1490,7 +1724,8 @@ static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4>), grid, dim3(kSplatBlock), 0, st, P, B);
 }
 
-typedef void (*primary_fn)(dim3, size_t, hipStream_t, const KParams &, const DScene *, const DView *, const Bufs &, bool);
+typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
+                           const Bufs &, bool, bool);
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
 static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>};
@@ -1587,12 +1822,17 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         o.pad1 = 0.f;
     }
 
-    /* lane arena: queues (2 x 6 x 16 B) + lane_out/lane_rec (32 B) + view records (48 B x G) */
+    /* lane arena: queues (2 x 6 x 16 B), lane_out/lane_rec/hit (48 B), NEE queue (64 B), visibility
+     * requests (48 B), view records (48 B x G), occlusion ballots (G / 8 B) */
     const uint64_t span = lane_end - lane_begin;
     const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
-    const size_t per_lane = 12 * 16 + 32 + (size_t) 48 * G + (records ? 0 : 0);
+    const size_t per_lane = 12 * 16 + 48 + 64 + 48 + (size_t) 48 * G + (G + 7) / 8;
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
-    const size_t need = views_bytes + 256 + 64 + per_lane * chunk + 4096;
+    /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
+    const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
+    const uint64_t qlen = (uint64_t) qcap * kQParts;
+    const size_t stats_bytes = (size_t) kStats * kStatShards * 8, cnt_bytes = (size_t) 3 * kQParts * kCntStride * 4;
+    const size_t need = views_bytes + stats_bytes + cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     if (g_arena.bytes < need || g_arena.device != dev) {
@@ -1609,11 +1849,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     char *base = (char *) g_arena.base;
     DView *dviews = (DView *) base;
     unsigned long long *dstats = (unsigned long long *) (base + views_bytes);
-    uint32_t *dcnt = (uint32_t *) (base + views_bytes + 64);
-    char *p = base + views_bytes + 256 + 64;
+    uint32_t *dcnt = (uint32_t *) (base + views_bytes + stats_bytes);   /* [3][kQParts * kCntStride] */
+    uint32_t *const cntA = dcnt, *const cntB = dcnt + kQParts * kCntStride, *const cntN = dcnt + 2 * kQParts * kCntStride;
+    char *p = base + views_bytes + stats_bytes + cnt_bytes;
     auto carve = [&](size_t bytes) { char *r = p; p += (bytes + 255) & ~(size_t) 255; return r; };
     HIPCHK(hipMemcpyAsync(dviews, hv.data(), hv.size() * sizeof(DView), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(dstats, 0, 64, st));
+    HIPCHK(hipMemsetAsync(dstats, 0, stats_bytes, st));
 
     /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
     static struct AdaptArena { void *base = nullptr; size_t bytes = 0; int device = -1; } g_adapt;
@@ -1649,10 +1890,16 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     Bufs B{};
     float4 *qa[6], *qb[6];
-    for (int k = 0; k < 6; ++k) qa[k] = (float4 *) carve(16 * chunk);
-    for (int k = 0; k < 6; ++k) qb[k] = (float4 *) carve(16 * chunk);
+    for (int k = 0; k < 6; ++k) qa[k] = (float4 *) carve(16 * qlen);
+    for (int k = 0; k < 6; ++k) qb[k] = (float4 *) carve(16 * qlen);
     B.lane_out = (float4 *) carve(16 * chunk);
     B.lane_rec = (float4 *) carve(16 * chunk);
+    B.hit = (float4 *) carve(16 * std::max<uint64_t>(chunk, qlen));
+    for (int k = 0; k < 4; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
+    for (int k = 0; k < 3; ++k) B.vreq[k] = (float4 *) carve(16 * chunk);
+    B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
+    B.cnt_nee = cntN;
+    B.qcap = qcap;
     B.view_rec = (float4 *) carve((size_t) 48 * G * chunk);
     B.film = film;
     B.records = records;
@@ -1662,9 +1909,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
     const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
-    const size_t lds = scene_lds_bytes(scene->dev, g_traversal) + (tab_b ? scene->dev.tab_bytes : 0u);   /* k_bounce */
-    const size_t lds_prim = scene_lds_bytes(scene->dev, g_traversal) +
-                            (tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u);          /* k_mv_primary */
+    const bool uni = scene_uniform(scene->dev.n_nodes, g_traversal);
+    const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
+    const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
+    const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
     hipEvent_t ev[4];
     for (auto &e : ev) HIPCHK(hipEventCreate(&e));
     float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;
@@ -1674,24 +1922,31 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* the shared suffix (sample_suffix / sample_single loop) over the queue the raygen
      * or primary kernel filled: one k_bounce launch per depth, ping-pong A <-> B */
     auto run_suffix = [&](uint32_t cn) -> amvpt_status {
-        const uint32_t bgrid = std::min<uint32_t>((cn + 255) / 256, 256 * 16);
+        /* a multiple of kQParts blocks: 1..16 per partition */
+        const uint32_t bgrid = kQParts * std::max<uint32_t>(1, std::min<uint32_t>(16, (cn + 256 * kQParts - 1) / (256 * kQParts)));
         bool a_is_in = true;
         for (uint32_t bnc = 0; bnc < max_bounces; ++bnc) {
             for (int k = 0; k < 6; ++k) {
                 B.q_in[k] = a_is_in ? qa[k] : qb[k];
                 B.q_out[k] = a_is_in ? qb[k] : qa[k];
             }
-            B.cnt_in = a_is_in ? dcnt : dcnt + 1;
-            B.cnt_out = a_is_in ? dcnt + 1 : dcnt;
-            HIPCHK(hipMemsetAsync(B.cnt_out, 0, sizeof(uint32_t), st));
+            B.cnt_in = a_is_in ? cntA : cntB;
+            B.cnt_out = a_is_in ? cntB : cntA;
+            /* k_extend zeroes cnt_out and cnt_nee */
+            if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<true>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<false>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             if (tab_b) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
             else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<true>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<false>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             HIPCHK(hipGetLastError());
             a_is_in = !a_is_in;
             if (bnc >= 15 && (bnc & 7) == 7) { /* unbounded depth: poll the live count */
-                uint32_t live = 0;
-                HIPCHK(hipMemcpyAsync(&live, B.cnt_out, 4, hipMemcpyDeviceToHost, st));
+                std::vector<uint32_t> hc((size_t) kQParts * kCntStride);
+                HIPCHK(hipMemcpyAsync(hc.data(), B.cnt_out, hc.size() * 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
+                uint64_t live = 0;
+                for (uint32_t q = 0; q < kQParts; ++q) live += hc[(size_t) q * kCntStride];
                 if (live == 0) break;
             }
         }
@@ -1709,14 +1964,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.records = P.record ? records + (size_t) (c0 - lane_begin) * G * 8 : records;
             const dim3 grid((cn + 255) / 256);
             /* counters: [0] = queue A, [1] = queue B */
-            HIPCHK(hipMemsetAsync(dcnt, 0, 2 * sizeof(uint32_t), st));
+            HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
             for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
-            B.cnt_out = dcnt; B.cnt_in = dcnt + 1;
+            B.cnt_out = cntA; B.cnt_in = cntB;
             HIPCHK(hipEventRecord(ev[0], st));
             if (G == 1) {
                 hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
             } else {
-                kPrimary[G](dim3((cn + kPrimBlock - 1) / kPrimBlock), lds_prim, st, P, dS, dviews, B, tab_p);
+                kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni);
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[1], st));
@@ -1772,9 +2027,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, wf - c0);
                 P.chunk_begin = c0;
                 P.chunk_n = cn;
-                HIPCHK(hipMemsetAsync(dcnt, 0, 2 * sizeof(uint32_t), st));
+                HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
                 for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
-                B.cnt_out = dcnt; B.cnt_in = dcnt + 1;
+                B.cnt_out = cntA; B.cnt_in = cntB;
                 hipLaunchKernelGGL(k_raygen_adapt, dim3((cn + 255) / 256), dim3(256), 0, st, P, dviews, B);
                 HIPCHK(hipGetLastError());
                 { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
@@ -1787,9 +2042,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         }
     }
     if (counters) {
-        unsigned long long hs[8] = {0};
-        HIPCHK(hipMemcpyAsync(hs, dstats, 64, hipMemcpyDeviceToHost, st));
+        std::vector<unsigned long long> hsh((size_t) kStats * kStatShards);
+        HIPCHK(hipMemcpyAsync(hsh.data(), dstats, stats_bytes, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        unsigned long long hs[kStats] = {0};
+        for (uint32_t k = 0; k < kStats; ++k)
+            for (uint32_t q = 0; q < kStatShards; ++q) hs[k] += hsh[(size_t) k * kStatShards + q];
         amvpt_counters &c = *counters;
         c = amvpt_counters{};
         c.lanes = span * n_passes;

@@ -31,7 +31,7 @@ struct SceneRef {
     const DPrim *gprims;
     const DScene *g;
     uint32_t n_nodes;
-    bool uniform;             /* small BVH: wave-uniform traversal (see trace_closest) */
+    bool uniform;             /* small BVH: the kernels run their kUni = true instance (see trace_closest) */
 };
 
 /* BVHs up to this many nodes are traversed wave-uniformly. */
@@ -160,19 +160,19 @@ AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float 
  * spilled to scratch).  Ties resolve toward the lower scene-order primitive
  * index, so the hit equals a brute-force scan whatever the traversal visits.
  *
- * Small BVHs (sc.uniform) are walked wave-uniformly: the wave enters a node if
+ * Small BVHs (kUni, chosen per scene by the host) are walked wave-uniformly: the wave enters a node if
  * any active lane's ray hits its box and every active lane tests the leaf's
  * primitives.  Node and primitive records are then wave-uniform scalar loads,
  * the primitive type is a uniform branch, and there is no per-lane divergence.
  * Testing a primitive for a lane whose own box test failed cannot change that
  * lane's result (its box is padded and inclusive), so both walks are exact.
  */
-AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
+template <bool kUni> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
     const f3 inv_d = safe_inv(ray.d);
     float tmax_box = ray.maxt;
-    if (sc.uniform) {
+    if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
         uint32_t node = 0;
         while (node < nn) {
@@ -227,9 +227,9 @@ AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
 }
 
 /* Any hit in [0, maxt] (Scene::ray_test); same two walks as trace_closest. */
-AD bool trace_any(const SceneRef &sc, const Ray &ray) {
+template <bool kUni> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
     const f3 inv_d = safe_inv(ray.d);
-    if (sc.uniform) {
+    if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
         bool found = false;
         uint32_t node = 0;
