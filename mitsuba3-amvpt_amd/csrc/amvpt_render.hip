@@ -92,7 +92,7 @@ struct Bufs {
 
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;
 constexpr int kPrimBlock = 128;
-enum { F_PDF, F_PDFLK, F_JP, F_PDFM, F_WX, F_WY, F_WZ, F_BR, F_BG, F_BB, F_W, VS_FIELDS };
+enum { F_PDF, F_JP, F_PDFM, F_WX, F_WY, F_WZ, VS_FIELDS };   /* k_mv_primary's per-view LDS state */
 
 /* Small BVHs are walked wave-uniformly from global memory (scalar loads) and not
  * staged; mid-size ones are staged in LDS; large ones stay in global memory. */
@@ -1269,8 +1269,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
     float *const vs = reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
 #define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
-    /* threads run in lane order (a wave = 4 pixels x 16 samples: coherent rays for the
-     * wave-uniform traversal); records go to the lane's slot (see slot_lane) */
+    /* threads run in lane order (a wave = 4 pixels x 16 samples); records go to the
+     * lane's slot (see slot_lane) */
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = i < P.chunk_n;
     const uint32_t slot = ok ? lane_slot(P, i) : 0u;
@@ -1278,6 +1278,12 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
     bool push = false;
     unsigned long long st_reuse = 0, st_vis = 0;
     if (ok) {
+        /* every global load first: a load issued after the record stores would wait
+         * for them (vmcnt counts loads and stores in issue order) */
+        const float4 hitv = B.hit[i];
+        uint32_t occm = 0;   /* bit k: k_vis found slot k occluded */
+#pragma unroll
+        for (int k = 0; k < G; ++k) occm |= occluded<G>(B, i, k) ? (1u << k) : 0u;
         const uint32_t n = P.chunk_n;
         const PrimRay pr = primary_raygen(P, V, i);
         Pcg rng = pr.rng;
@@ -1299,9 +1305,12 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             }
             reinterpret_cast<float2 *>(&rec0[(size_t) k * n + slot])[0] = make_float2(x, y);
         };
-#pragma unroll 1
-        for (int f = 0; f < VS_FIELDS * G; ++f) vs[f * kPrimBlock] = 0.f;
+        auto put_wf = [&](int k, float w, uint32_t vflags) {
+            const uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
+            reinterpret_cast<float2 *>(&rec0[(size_t) k * n + slot])[1] = make_float2(w, bitsf(vf));
+        };
         uint32_t vflags = 0;   /* bit k: valid, bit 16 + k: indirect */
+        float w0 = 1.f;        /* slot 0's splat weight */
         C3 result0 = c3(0.f);  /* slot-0 emission + direct, for the non-MIS path */
         bool records_done = false;
         put_pos(0, sx, sy);
@@ -1311,7 +1320,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         float pdfW = 1.f;
         bool should_mis = P.sa_mis != 0;
         if (P.max_depth != 0) {
-            SI si = compute_si(sc, pray, hit_of(B.hit[i]));
+            SI si = compute_si(sc, pray, hit_of(hitv));
             bool p_hit = si.valid();
             int32_t em = si_emitter(sc, si);
             bool direct_em = em >= 0;
@@ -1322,7 +1331,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             float e1 = rng.next_1d(), e2 = rng.next_1d();
             DSamp ds;
             C3 em_w;
-            if (sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w) && occluded<G>(B, i, 0))
+            if (sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w) && (occm & 1u))
                 occlude_emitter_sample(ds, em_w);
             active_em = active_em && ds.pdf != 0.f;
             f3 wo = si.sh.to_local(ds.d);
@@ -1349,17 +1358,21 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 bd.rsqrt_a = rsqrt_(bd.alpha);
                 bd.diffuse = flag_diff;
                 bd.reuse = reuse;
-                VSF(F_BR, 0) = bsdf_val.r; VSF(F_BG, 0) = bsdf_val.g; VSF(F_BB, 0) = bsdf_val.b;
                 /* ---- camera_selection (mvpath_multi.h:371-464) ---- */
                 Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
-                VSF(F_PDF, 0) = pdf0; VSF(F_PDFLK, 0) = pdf0; VSF(F_JP, 0) = Jp0;
+                VSF(F_PDF, 0) = pdf0; VSF(F_JP, 0) = Jp0;
                 VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
                 vflags |= p_hit ? (1u | (1u << 16)) : 0u;
                 const f3 wo_r0 = reflect_l(si.wi);
-                VSF(F_PDFM, 0) = P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
-                                       : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit);
-                if (bd.diffuse) VSF(F_PDFM, 0) = 1.f;
+                VSF(F_PDFM, 0) = bd.diffuse ? 1.f : (P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
+                                                               : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit));
+                /* pdf_Mat of view k toward view 0 (tv_pdf, camera_selection) */
+                auto mat_pdf = [&](f3 wik, float pdfM, bool active) -> float {
+                    if (bd.diffuse) return 1.f;
+                    return P.fast_mis ? tv_pdf_fast(wo_r0, wik, pdfM, bd, active)
+                                      : tv_pdf(S.bsdfs, wo_r0, wik, pdfM, bd, active);
+                };
                 float n_direct = 1.f, n_indir = 2.f;
 #pragma unroll 1
                 for (int k = 1; k < G; ++k) {
@@ -1367,7 +1380,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
-                        valid = !occluded<G>(B, i, k);
+                        valid = !((occm >> k) & 1u);
                     }
                     f3 wik = si.sh.to_local(r.d);
                     VSF(F_WX, k) = wik.x; VSF(F_WY, k) = wik.y; VSF(F_WZ, k) = wik.z;
@@ -1375,9 +1388,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     float pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
                                             : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
                     VSF(F_PDFM, k) = pdfM;
-                    float pdf_Mat = P.fast_mis ? tv_pdf_fast(wo_r0, wik, pdfM, bd, valid)
-                                               : tv_pdf(S.bsdfs, wo_r0, wik, pdfM, bd, valid);
-                    if (bd.diffuse) pdf_Mat = 1.f;
+                    float pdf_Mat = mat_pdf(wik, pdfM, valid);
                     float J = r.Jp * iJp0;
                     float pdf_J = J > 1.f ? rcp(J) : J;
                     float pdf_Sel = pdf_Mat * pdf_J;
@@ -1385,7 +1396,6 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     VSF(F_JP, k) = r.Jp;
                     put_pos(k, r.uvx, r.uvy);
                     VSF(F_PDF, k) = valid ? r.pdf : 0.f;
-                    VSF(F_PDFLK, k) = valid ? pdf0 * J * pdf_Sel : 0.f;
                     bool indirect = valid, direct = valid;
                     bool replace = n_indir * rng.next_1d() < 1.f;
                     C3 bvk;
@@ -1395,7 +1405,6 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
                     bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
                     direct = direct && bpk > 0.f;
-                    VSF(F_BR, k) = bvk.r; VSF(F_BG, k) = bvk.g; VSF(F_BB, k) = bvk.b;
                     direct_pdf += direct ? bpk : 0.f;
                     n_direct += (float) direct;
                     indirect = indirect && bsk.type == bsmp.type;
@@ -1404,14 +1413,25 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     vflags |= (valid ? (1u << k) : 0u) | (indirect ? (1u << (16 + k)) : 0u);
                 }
                 direct_pdf /= n_direct;
-                /* ---- mis_weights (mvpath_multi.h:466-523) ---- */
+                const float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
+                const C3 emis_mis = em_w * mis_em;
+                /* ---- per view: mis_weights (mvpath_multi.h:466-523), direct light and
+                 *      the multi-view mixture pdf (mvpath_multi.h:245-317) ---- */
+                float n_ind = 0.f, pdf = 0.f;
 #pragma unroll 1
                 for (int k = 0; k < G; ++k) {
                     const bool vk = (vflags >> k) & 1u;
-                    const float iJpk = k == 0 ? iJp0 : (vk ? rcp(VSF(F_JP, k)) : 0.f);
+                    const float Jpk = VSF(F_JP, k);
+                    const float iJpk = k == 0 ? iJp0 : (vk ? rcp(Jpk) : 0.f);
                     const f3 wik = mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
                     const float pdfMk = VSF(F_PDFM, k);
-                    float pdfSum = VSF(F_PDFLK, k);
+                    /* pdf_lk of camera_selection, re-derived: valid_k implies it was active */
+                    float pdf_lk = pdf0;
+                    if (k > 0) {
+                        const float J = Jpk * iJp0, pdf_J = J > 1.f ? rcp(J) : J;
+                        pdf_lk = vk ? pdf0 * J * (mat_pdf(wik, pdfMk, true) * pdf_J) : 0.f;
+                    }
+                    float pdfSum = pdf_lk;
                     if (k > 0) pdfSum += VSF(F_PDF, k);
                     bool cond = k > 0 ? vk : bd.reuse;
                     float acc = 0.f;
@@ -1436,40 +1456,23 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                         acc = cond ? acc : 0.f;
                     }
                     pdfSum += acc;
-                    VSF(F_W, k) = VSF(F_PDFLK, k) / pdfSum;
-                }
-            } else {
-                vflags |= p_hit ? 1u : 0u;
-#pragma unroll 1
-                for (int k = 1; k < G; ++k) {
-                    Surf r = camera_sample_surface(V[view_of(k)], si, reuse, apx, apy);
-                    bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
-                    if (valid) {
-                        ++st_vis;
-                        valid = !occluded<G>(B, i, k);
-                    }
-                    put_pos(k, r.uvx, r.uvy);
-                    vflags |= valid ? (1u << k) : 0u;
-                }
-            }
-            /* ---- emitter sampling contribution ---- */
-            float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
-            C3 emis_mis = em_w * mis_em;
-            /* ---- BSDF sampling / multi-view mixture pdf ---- */
-            Ray pd_ray = spawn_ray(si.p, si.n, si.sh.to_world(bsmp.wo));
-            if (should_mis) {
-                float n_indir = 0.f, pdf = 0.f;
-#pragma unroll 1
-                for (int k = 0; k < G; ++k) {
+                    const float wk = pdf_lk / pdfSum;
                     const size_t o = (size_t) k * n + slot;
                     /* result: emission (slot 0) + direct light through this view's BSDF value */
                     C3 res = k == 0 ? emitted : c3(0.f);
-                    if (active_em && ((vflags >> k) & 1u)) res = cfma(C3{VSF(F_BR, k), VSF(F_BG, k), VSF(F_BB, k)}, emis_mis, res);
+                    if (active_em && vk) {
+                        C3 bvk = bsdf_val;
+                        if (k > 0) {   /* the value camera_selection evaluated for view k */
+                            float bpk;
+                            bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, true, bvk, bpk);
+                        }
+                        res = cfma(bvk, emis_mis, res);
+                    }
                     rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
                     bool valid = (vflags >> (16 + k)) & 1u;
                     C3 bv;
                     float bp;
-                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k)), bsmp.wo, valid, bv, bp);
+                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, bsmp.wo, valid, bv, bp);
                     if (k == 0) {
                         bv = p_not_delta ? bv : bsdf_weight;
                         bp = p_not_delta ? bp : bsmp.pdf;
@@ -1481,16 +1484,33 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bv = valid ? bv : c3(0.f);
                     rec2[o] = make_float4(bv.r, bv.g, bv.b, 0.f);
                     pdf += bp;
-                    n_indir += (float) valid;
+                    n_ind += (float) valid;
                     if (!valid) vflags &= ~(1u << (16 + k));
+                    if (k == 0) w0 = wk;
+                    else put_wf(k, wk, vflags);
                 }
-                bsmp.pdf = p_not_delta ? pdf / n_indir : bsmp.pdf;
-                adapt_mask = p_hit && !flag_null && (n_indir <= 1.f);
+                bsmp.pdf = p_not_delta ? pdf / n_ind : bsmp.pdf;
+                adapt_mask = p_hit && !flag_null && (n_ind <= 1.f);
                 records_done = true;
             } else {
+                vflags |= p_hit ? 1u : 0u;
+#pragma unroll 1
+                for (int k = 1; k < G; ++k) {
+                    Surf r = camera_sample_surface(V[view_of(k)], si, reuse, apx, apy);
+                    bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
+                    if (valid) {
+                        ++st_vis;
+                        valid = !((occm >> k) & 1u);
+                    }
+                    put_pos(k, r.uvx, r.uvy);
+                    vflags |= valid ? (1u << k) : 0u;
+                }
+                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
                 result0 = emitted;
-                if (active_em) result0 = cfma(bsdf_val, emis_mis, result0);
+                if (active_em) result0 = cfma(bsdf_val, em_w * mis_em, result0);
             }
+            /* ---- BSDF sampling continuation ---- */
+            Ray pd_ray = spawn_ray(si.p, si.n, si.sh.to_world(bsmp.wo));
             C3 thr = should_mis ? c3(1.f) : bsdf_weight;
             valid_ray = valid_ray || (p_hit && !flag_null);
             bool pd_active = p_hit;
@@ -1513,11 +1533,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 push = true;
             }
             /* p_sample.weight/valid finalisation happens after the suffix */
-            if (!should_mis) {
-#pragma unroll
-                for (int k = 0; k < G; ++k) VSF(F_W, k) = 1.f;
-            }
-            VSF(F_W, 0) = p_hit ? VSF(F_W, 0) : 1.f;
+            if (!p_hit) w0 = 1.f;
             vflags |= 1u;
         }
         if (!push) B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1528,13 +1544,14 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
 #pragma unroll 1
             for (int k = 1; k < G; ++k) put_pos(k, 0.f, 0.f);
             vflags = 0;
+            w0 = 0.f;   /* no vertex: every slot keeps weight 0 */
         }
+        put_wf(0, w0, vflags);
+        if (!records_done) {
 #pragma unroll 1
-        for (int k = 0; k < G; ++k) {
-            const size_t o = (size_t) k * n + slot;
-            uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
-            reinterpret_cast<float2 *>(&rec0[o])[1] = make_float2(VSF(F_W, k), bitsf(vf));
-            if (!records_done) {
+            for (int k = 0; k < G; ++k) {
+                const size_t o = (size_t) k * n + slot;
+                if (k > 0) put_wf(k, P.max_depth != 0 ? 1.f : 0.f, vflags);
                 C3 res = k == 0 ? result0 : c3(0.f);
                 rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
                 rec2[o] = make_float4(0.f, 0.f, 0.f, 0.f);
