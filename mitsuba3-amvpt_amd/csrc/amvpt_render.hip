@@ -458,8 +458,18 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
  * pass; the window is single-buffered (the next put's first barrier orders its
  * adds after this flush), only the tiny bounding-box exchange alternates buffers.
  */
-constexpr int kWinW = 96, kWinH = 16, kMaxWaves = 16, kMaxFoot = 5;
-constexpr int kSplatBlock = 512;   /* threads per splat block (see slot_lane) */
+#ifndef AMVPT_WIN_H
+#define AMVPT_WIN_H 8
+#endif
+#ifndef AMVPT_SPLAT_BLOCK
+#define AMVPT_SPLAT_BLOCK 256
+#endif
+#ifndef AMVPT_WIN_W
+#define AMVPT_WIN_W 96
+#endif
+constexpr int kWinW = AMVPT_WIN_W, kWinH = AMVPT_WIN_H, kMaxWaves = 16, kMaxFoot = 5;
+constexpr int kSplatSuper = 1024;   /* lanes per splat super-block (see slot_lane) */
+constexpr int kSplatBlock = AMVPT_SPLAT_BLOCK;   /* threads per splat block (see slot_lane) */
 constexpr int kWinCells = kWinW * kWinH;
 template <int C> struct SplatLds {
     double win[kWinCells * C];              /* channel k of cell c at win[k * plane + c] */
@@ -528,23 +538,12 @@ AD void lds_add64(double *p, double v) {
     (void) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-/*
- * Block-cooperative put into window buffer `buf`.  Cells xs in [0, nx) x ys in
- * [0, ny) of the footprint with x0 + xs >= 0 and y0 + ys >= 0 are accumulated (the
- * coalesced footprint may start left/above the film).  Weight of a cell =
- * eval(rx + xs) * eval(ry + ys).  `coalesce` is uniform over the block.
- */
+/* The block's window: union of the active footprints, clamped to kWinW x kWinH. */
+struct Win { int bx0, by0, ww, wh; };
 template <int C>
-AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float px, float py, const float *vals,
-                  bool valid, bool coalesce, unsigned long long *fallback = nullptr) {
-    Foot f;
-    f.ok = false;
-    f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
-    if (valid) f = footprint(P, px, py, coalesce);
-    const bool act = valid && f.ok;
-    const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
+AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, int y1) {
     int lx = act ? cx0 : 0x7fffffff, ly = act ? cy0 : 0x7fffffff;
-    int hx = act ? f.x0 + f.nx : (int) 0x80000000, hy = act ? f.y0 + f.ny : (int) 0x80000000;
+    int hx = act ? x1 : (int) 0x80000000, hy = act ? y1 : (int) 0x80000000;
     lx = wave_min(lx); ly = wave_min(ly); hx = wave_max(hx); hy = wave_max(hy);
     const int wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -566,67 +565,29 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
         bx0 = __shfl(bx0, 0); by0 = __shfl(by0, 0); bx1 = __shfl(bx1, 0); by1 = __shfl(by1, 0);
     }
     const bool any = bx0 != 0x7fffffff && bx0 < bx1;
-    const int ww = any ? min(bx1 - bx0, kWinW) : 0, wh = any ? min(by1 - by0, kWinH) : 0;
-    const int plane = ww * wh;
-    double *win = L.win;
-    if (act) {
-        const bool in_win = cx0 >= bx0 && cy0 >= by0 && f.x0 + f.nx <= bx0 + ww && f.y0 + f.ny <= by0 + wh;
-        float wx[kMaxFoot], wy[kMaxFoot];
-#pragma unroll
-        for (int t = 0; t < kMaxFoot; ++t) {
-            wx[t] = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
-            wy[t] = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
-        }
-        /* cells per footprint side: uniform over the call (filter radius and method only) */
-        const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
-        if (in_win && cnt <= kMaxFoot) {
-            /* straight-line cnt x cnt cells; clipped cells are masked off (no retry, no branch body) */
-            double *const c0 = win + ((f.y0 - by0) * ww + (f.x0 - bx0));
-#pragma unroll
-            for (int ys = 0; ys < kMaxFoot; ++ys) {
-                if (ys >= cnt) break;
-                const bool rok = ys < f.ny && f.y0 + ys >= 0;
-#pragma unroll
-                for (int xs = 0; xs < kMaxFoot; ++xs) {
-                    if (xs >= cnt) break;
-                    if (rok && xs < f.nx && f.x0 + xs >= 0) {
-                        const float w = wx[xs] * wy[ys];
-                        double *const cp = c0 + ys * ww + xs;
-#pragma unroll
-                        for (int k = 0; k < C; ++k) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
-                    }
-                }
-            }
-        } else {
-            /* window miss (or a filter wider than kMaxFoot): direct global atomics */
-            if (fallback && !in_win) ++*fallback;
-            for (int ys = 0; ys < f.ny; ++ys) {
-                const int y = f.y0 + ys;
-                if (y < 0) continue;
-                const float wyv = ys < kMaxFoot ? wy[ys] : (P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) ys));
-                for (int xs = 0; xs < f.nx; ++xs) {
-                    const int x = f.x0 + xs;
-                    if (x < 0) continue;
-                    const float wxv = xs < kMaxFoot ? wx[xs] : (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs));
-                    const float w = wxv * wyv;
-                    float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
-#pragma unroll
-                    for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
-                }
-            }
-        }
-    }
+    Win w;
+    w.bx0 = bx0; w.by0 = by0;
+    w.ww = any ? min(bx1 - bx0, kWinW) : 0;
+    w.wh = any ? min(by1 - by0, kWinH) : 0;
+    return w;
+}
+
+/* barrier, then one global float atomic per touched film float of the window; the window
+ * is re-zeroed on the way (consecutive threads take consecutive floats of a film row) */
+template <int C>
+AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w) {
     __syncthreads();
-    /* flush + re-zero: consecutive threads take consecutive floats of the film row segment */
-    const int rowlen = ww * C;
+    const int plane = w.ww * w.wh;
+    const int rowlen = w.ww * C;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
-    float *film0 = film + ((size_t) by0 * P.W + (size_t) bx0) * C;
+    float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
+    double *win = L.win;
     for (int e = threadIdx.x; e < plane * C; e += blockDim.x) {
         int cy = (int) ((float) e * inv_rowlen);            /* e < 2^24: off by at most one */
         cy -= (cy * rowlen > e) ? 1 : 0;
         cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
         const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
-        double *src = win + k * plane + cy * ww + cx;
+        double *src = win + k * plane + cy * w.ww + cx;
         const double d = *src;
         if (__double_as_longlong(d) != 0ll) {
             *src = 0.0;
@@ -634,6 +595,84 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
             if (v != 0.f || v != v) film_add(film0 + (size_t) cy * P.W * C + r, v);
         }
     }
+}
+
+/* one footprint's cells straight into the window (or the film when it does not fit) */
+template <int C>
+AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, const Foot &f, const float *wx,
+                 const float *wy, const float *vals, bool coalesce, unsigned long long *fallback) {
+    const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
+    const int plane = wn.ww * wn.wh;
+    const bool in_win = cx0 >= wn.bx0 && cy0 >= wn.by0 && f.x0 + f.nx <= wn.bx0 + wn.ww && f.y0 + f.ny <= wn.by0 + wn.wh;
+    /* cells per footprint side: uniform over the call (filter radius and method only) */
+    const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
+    if (in_win && cnt <= kMaxFoot) {
+        /* straight-line cnt x cnt cells; clipped cells are masked off (no retry, no branch body) */
+        double *const c0 = L.win + ((f.y0 - wn.by0) * wn.ww + (f.x0 - wn.bx0));
+#pragma unroll
+        for (int ys = 0; ys < kMaxFoot; ++ys) {
+            if (ys >= cnt) break;
+            const bool rok = ys < f.ny && f.y0 + ys >= 0;
+#pragma unroll
+            for (int xs = 0; xs < kMaxFoot; ++xs) {
+                if (xs >= cnt) break;
+                if (rok && xs < f.nx && f.x0 + xs >= 0) {
+                    const float w = wx[xs] * wy[ys];
+                    double *const cp = c0 + ys * wn.ww + xs;
+#pragma unroll
+                    for (int k = 0; k < C; ++k) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
+                }
+            }
+        }
+    } else {
+        /* window miss (or a filter wider than kMaxFoot): direct global atomics */
+        if (fallback && !in_win) ++*fallback;
+        for (int ys = 0; ys < f.ny; ++ys) {
+            const int y = f.y0 + ys;
+            if (y < 0) continue;
+            const float wyv = ys < kMaxFoot ? wy[ys] : (P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) ys));
+            for (int xs = 0; xs < f.nx; ++xs) {
+                const int x = f.x0 + xs;
+                if (x < 0) continue;
+                const float wxv = xs < kMaxFoot ? wx[xs] : (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs));
+                const float w = wxv * wyv;
+                float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
+#pragma unroll
+                for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
+            }
+        }
+    }
+}
+
+AD void foot_weights(const KParams &P, const Foot &f, float *wx, float *wy) {
+#pragma unroll
+    for (int t = 0; t < kMaxFoot; ++t) {
+        wx[t] = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
+        wy[t] = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
+    }
+}
+
+/*
+ * Block-cooperative put into window buffer `buf`.  Cells xs in [0, nx) x ys in
+ * [0, ny) of the footprint with x0 + xs >= 0 and y0 + ys >= 0 are accumulated (the
+ * coalesced footprint may start left/above the film).  Weight of a cell =
+ * eval(rx + xs) * eval(ry + ys).  `coalesce` is uniform over the block.
+ */
+template <int C>
+AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float px, float py, const float *vals,
+                  bool valid, bool coalesce, unsigned long long *fallback = nullptr) {
+    Foot f;
+    f.ok = false;
+    f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
+    if (valid) f = footprint(P, px, py, coalesce);
+    const bool act = valid && f.ok;
+    const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny);
+    if (act) {
+        float wx[kMaxFoot], wy[kMaxFoot];
+        foot_weights(P, f, wx, wy);
+        foot_add<C>(P, film, L, wn, f, wx, wy, vals, coalesce, fallback);
+    }
+    window_flush<C>(P, film, L, wn);
 }
 
 /*
@@ -648,7 +687,7 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
  * the same small film window.  Partial super-blocks and non power-of-two spp
  * use the identity map.  The map is a bijection on [0, chunk_n).
  */
-constexpr int kSplatSuper = 1024, kSplatSplit = kSplatSuper / kSplatBlock;
+constexpr int kSplatSplit = kSplatSuper / kSplatBlock;
 AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
     const uint32_t super = slot / (uint32_t) kSplatSuper, within = slot % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
