@@ -486,6 +486,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.lds_bytes = (uint32_t) (nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim));
     sc->n_nodes = D.n_nodes;
     sc->n_prims = (uint32_t) bprims.size();
+    sc->all_diffuse = d->bsdf_count > 0;
+    for (uint32_t i = 0; i < d->bsdf_count; ++i) sc->all_diffuse = sc->all_diffuse && d->bsdfs[i].type == AMVPT_BSDF_DIFFUSE;
     std::vector<DScene> one(1, D);
     if ((st = upload(one.data(), sizeof(DScene), &sc->dev_scene_struct)) != AMVPT_OK) {
         amvpt_scene_destroy(sc);

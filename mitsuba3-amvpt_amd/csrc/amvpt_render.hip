@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "dbsdf.h"
@@ -35,6 +36,7 @@ namespace amvpt {
 
 uint64_t g_chunk_lanes = 1ull << 23;
 uint32_t g_traversal = 0;
+bool g_diffuse_spec = true;   /* all-diffuse kernel specialisation (AMVPT_NO_DIFFUSE_SPEC=1 turns it off) */
 amvpt_exchange_fn g_exchange = nullptr;
 void *g_exchange_ctx = nullptr;
 
@@ -93,6 +95,7 @@ struct Bufs {
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;
 constexpr int kPrimBlock = 128;
 enum { F_PDF, F_JP, F_PDFM, F_WX, F_WY, F_WZ, VS_FIELDS };   /* k_mv_primary's per-view LDS state */
+constexpr int kVsFieldsDiff = 2;   /* all-diffuse scenes keep only F_PDF and F_JP in LDS */
 
 /* Small BVHs are walked wave-uniformly from global memory (scalar loads) and not
  * staged; mid-size ones are staged in LDS; large ones stay in global memory. */
@@ -1299,7 +1302,13 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #ifndef AMVPT_PRIM_WAVES
 #define AMVPT_PRIM_WAVES 1
 #endif
-template <int G, bool kTab>
+/*
+ * kDiff (every BSDF of the scene is plain `diffuse`): pdf_Mat is 1 and eval/pdf depend
+ * on a direction only through the sign of its z, a view's BSDF sample is the primary's
+ * own (cosine_hemisphere(rand_2) whatever wi), so the per-view state reduces to F_PDF,
+ * F_JP and one sign bit per view -- same values, a third of the LDS per thread.
+ */
+template <int G, bool kTab, bool kDiff>
 __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -1379,10 +1388,10 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             (void) rand_1;
             C3 bsdf_val;
             float direct_pdf;
-            bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bsdf_val, direct_pdf);
+            bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bsdf_val, direct_pdf);
             BSample bsmp;
             C3 bsdf_weight;
-            bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, r2a, r2b, true, bsmp, bsdf_weight);
+            bsdf_sample<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, r2a, r2b, true, bsmp, bsdf_weight);
             bool flag_delta = (bsmp.type & BF_Delta) != 0, flag_null = (bsmp.type & BF_Null) != 0;
             bool flag_diff = (bsmp.type & BF_Diffuse) != 0;
             bool delta = flag_delta || flag_null, p_not_delta = !delta && p_hit;
@@ -1392,7 +1401,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             if (should_mis) {
                 BD bd;
                 bd.bsdf = b;
-                bd.alpha = bsdf_roughness(S.bsdfs, b, si.wi);
+                bd.alpha = bsdf_roughness<kDiff>(S.bsdfs, b, si.wi);
                 bd.sqr_a = fmsub(bd.alpha, bd.alpha, 1.f);
                 bd.rsqrt_a = rsqrt_(bd.alpha);
                 bd.diffuse = flag_diff;
@@ -1401,11 +1410,19 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
                 VSF(F_PDF, 0) = pdf0; VSF(F_JP, 0) = Jp0;
-                VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
                 vflags |= p_hit ? (1u | (1u << 16)) : 0u;
                 const f3 wo_r0 = reflect_l(si.wi);
-                VSF(F_PDFM, 0) = bd.diffuse ? 1.f : (P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
-                                                               : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit));
+                uint32_t wpos = 0;   /* kDiff: bit k = (wi_k.z > 0) */
+                if (!kDiff) {
+                    VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
+                    VSF(F_PDFM, 0) = bd.diffuse ? 1.f : (P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
+                                                                   : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit));
+                }
+                /* view k's wi (kDiff: only the sign of z matters to diffuse.cpp) */
+                auto wi_of = [&](int k) -> f3 {
+                    if (kDiff) return k == 0 ? si.wi : mk(0.f, 0.f, ((wpos >> k) & 1u) ? 1.f : -1.f);
+                    return mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
+                };
                 /* pdf_Mat of view k toward view 0 (tv_pdf, camera_selection) */
                 auto mat_pdf = [&](f3 wik, float pdfM, bool active) -> float {
                     if (bd.diffuse) return 1.f;
@@ -1422,12 +1439,17 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                         valid = !((occm >> k) & 1u);
                     }
                     f3 wik = si.sh.to_local(r.d);
-                    VSF(F_WX, k) = wik.x; VSF(F_WY, k) = wik.y; VSF(F_WZ, k) = wik.z;
-                    f3 wor = reflect_l(wik);
-                    float pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
-                                            : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
-                    VSF(F_PDFM, k) = pdfM;
-                    float pdf_Mat = mat_pdf(wik, pdfM, valid);
+                    float pdf_Mat = 1.f;   /* kDiff: valid implies a diffuse hit (mat_pdf = 1) */
+                    if (!kDiff) {
+                        VSF(F_WX, k) = wik.x; VSF(F_WY, k) = wik.y; VSF(F_WZ, k) = wik.z;
+                        f3 wor = reflect_l(wik);
+                        float pdfM = P.fast_mis ? sqr(normalize(wik + wor).z)
+                                                : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
+                        VSF(F_PDFM, k) = pdfM;
+                        pdf_Mat = mat_pdf(wik, pdfM, valid);
+                    } else {
+                        wpos |= wik.z > 0.f ? (1u << k) : 0u;
+                    }
                     float J = r.Jp * iJp0;
                     float pdf_J = J > 1.f ? rcp(J) : J;
                     float pdf_Sel = pdf_Mat * pdf_J;
@@ -1441,13 +1463,17 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     float bpk;
                     BSample bsk;
                     C3 bwk;
-                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
-                    bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
+                    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, wo, valid, bvk, bpk);
                     direct = direct && bpk > 0.f;
                     direct_pdf += direct ? bpk : 0.f;
                     n_direct += (float) direct;
-                    indirect = indirect && bsk.type == bsmp.type;
-                    if (indirect && replace) bsmp.wo = bsk.wo;
+                    if (!kDiff) {
+                        bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
+                        indirect = indirect && bsk.type == bsmp.type;
+                        if (indirect && replace) bsmp.wo = bsk.wo;
+                    }
+                    /* kDiff: a valid view's sample is the primary's (same type, same wo) */
+                    (void) replace;
                     n_indir += (float) indirect;
                     vflags |= (valid ? (1u << k) : 0u) | (indirect ? (1u << (16 + k)) : 0u);
                 }
@@ -1462,19 +1488,19 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     const bool vk = (vflags >> k) & 1u;
                     const float Jpk = VSF(F_JP, k);
                     const float iJpk = k == 0 ? iJp0 : (vk ? rcp(Jpk) : 0.f);
-                    const f3 wik = mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
-                    const float pdfMk = VSF(F_PDFM, k);
+                    const f3 wik = wi_of(k);
+                    const float pdfMk = kDiff ? 1.f : VSF(F_PDFM, k);
                     /* pdf_lk of camera_selection, re-derived: valid_k implies it was active */
                     float pdf_lk = pdf0;
                     if (k > 0) {
                         const float J = Jpk * iJp0, pdf_J = J > 1.f ? rcp(J) : J;
-                        pdf_lk = vk ? pdf0 * J * (mat_pdf(wik, pdfMk, true) * pdf_J) : 0.f;
+                        pdf_lk = vk ? pdf0 * J * ((kDiff ? 1.f : mat_pdf(wik, pdfMk, true)) * pdf_J) : 0.f;
                     }
                     float pdfSum = pdf_lk;
                     if (k > 0) pdfSum += VSF(F_PDF, k);
                     bool cond = k > 0 ? vk : bd.reuse;
                     float acc = 0.f;
-                    if (cond && !bd.diffuse) {
+                    if (!kDiff && cond && !bd.diffuse) {
 #pragma unroll 1
                         for (int j = 1; j < G; ++j) {
                             if (j == k) continue;
@@ -1503,7 +1529,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                         C3 bvk = bsdf_val;
                         if (k > 0) {   /* the value camera_selection evaluated for view k */
                             float bpk;
-                            bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, wo, true, bvk, bpk);
+                            bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, wo, true, bvk, bpk);
                         }
                         res = cfma(bvk, emis_mis, res);
                     }
@@ -1511,7 +1537,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bool valid = (vflags >> (16 + k)) & 1u;
                     C3 bv;
                     float bp;
-                    bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, wik, bsmp.wo, valid, bv, bp);
+                    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, bsmp.wo, valid, bv, bp);
                     if (k == 0) {
                         bv = p_not_delta ? bv : bsdf_weight;
                         bp = p_not_delta ? bp : bsmp.pdf;
@@ -1762,17 +1788,19 @@ static Arena g_arena;
 /* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
 template <int G>
 static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
-                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni) {
+                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff) {
     const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPrimBlock - 1) / kPrimBlock);
-    const size_t lds_view = (size_t) VS_FIELDS * G * kPrimBlock * sizeof(float);
+    const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * G * kPrimBlock * sizeof(float);
     if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
     if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
     if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
-    if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
@@ -1781,7 +1809,7 @@ static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs
 }
 
 typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
-                           const Bufs &, bool, bool);
+                           const Bufs &, bool, bool, bool);
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
 static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>};
@@ -1796,6 +1824,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     if (!scene || !views || !params || !film) { set_error("amvpt_render: null argument"); return AMVPT_ERR_INVALID; }
     const amvpt_params &Pp = *params;
     hipStream_t st = (hipStream_t) stream;
+    { const char *e = std::getenv("AMVPT_NO_DIFFUSE_SPEC"); g_diffuse_spec = !(e && e[0] == '1'); }
     uint32_t spp, spp_pp, n_passes;
     uint64_t L;
     plan(Pp, spp, spp_pp, n_passes, L);
@@ -2027,7 +2056,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             if (G == 1) {
                 hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
             } else {
-                kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni);
+                kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, scene->all_diffuse && g_diffuse_spec);
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[1], st));

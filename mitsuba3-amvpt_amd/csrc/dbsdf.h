@@ -108,16 +108,32 @@ AD C3 fresnel3(const DBsdf &b, float ci) {
 }
 
 /* ---------------- leaf BSDFs ---------------- */
+/* diffuse.cpp:100-188 */
+AD void diffuse_eval_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo, C3 &val, float &pdf) {
+    if (!ctx_on(ctx, BF_DiffuseReflection)) { val = c3(0.f); pdf = 0.f; return; }
+    bool a = wi.z > 0.f && wo.z > 0.f;
+    C3 v = c3(d.refl) * kInvPi * wo.z;
+    float p = kInvPi * wo.z;
+    val = a ? v : c3(0.f);
+    pdf = a ? p : 0.f;
+}
+AD float diffuse_pdf(uint32_t ctx, f3 wi, f3 wo) {
+    if (!ctx_on(ctx, BF_DiffuseReflection)) return 0.f;
+    float p = kInvPi * wo.z;
+    return (wi.z > 0.f && wo.z > 0.f) ? p : 0.f;
+}
+AD void diffuse_sample(const DBsdf &d, uint32_t ctx, f3 wi, float u1, float u2, BSample &bs, C3 &w) {
+    bool a = wi.z > 0.f;
+    if (!ctx_on(ctx, BF_DiffuseReflection)) { w = c3(0.f); return; }
+    bs.wo = cosine_hemisphere(u1, u2);
+    bs.pdf = kInvPi * bs.wo.z;
+    bs.eta = 1.f;
+    bs.type = BF_DiffuseReflection;
+    w = (a && bs.pdf > 0.f) ? c3(d.refl) : c3(0.f);
+}
+
 AD void leaf_eval_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo, C3 &val, float &pdf) {
-    if (d.type == BSDF_DIFFUSE) {
-        if (!ctx_on(ctx, BF_DiffuseReflection)) { val = c3(0.f); pdf = 0.f; return; }
-        bool a = wi.z > 0.f && wo.z > 0.f;
-        C3 v = c3(d.refl) * kInvPi * wo.z;
-        float p = kInvPi * wo.z;
-        val = a ? v : c3(0.f);
-        pdf = a ? p : 0.f;
-        return;
-    }
+    if (d.type == BSDF_DIFFUSE) { diffuse_eval_pdf(d, ctx, wi, wo, val, pdf); return; }
     f3 H = normalize(wo + wi);
     bool a = wi.z > 0.f && wo.z > 0.f && dot(wi, H) > 0.f && dot(wo, H) > 0.f;
     if (!ctx_on(ctx, BF_GlossyReflection)) { val = c3(0.f); pdf = 0.f; return; }
@@ -135,11 +151,7 @@ AD void leaf_eval_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo, C3 &val, float
 }
 
 AD float leaf_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo) {
-    if (d.type == BSDF_DIFFUSE) {
-        if (!ctx_on(ctx, BF_DiffuseReflection)) return 0.f;
-        float p = kInvPi * wo.z;
-        return (wi.z > 0.f && wo.z > 0.f) ? p : 0.f;
-    }
+    if (d.type == BSDF_DIFFUSE) return diffuse_pdf(ctx, wi, wo);
     f3 m = normalize(wo + wi);
     bool a = wi.z > 0.f && wo.z > 0.f && dot(wi, m) > 0.f && dot(wo, m) > 0.f;
     if (!ctx_on(ctx, BF_GlossyReflection)) return 0.f;
@@ -150,16 +162,7 @@ AD float leaf_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo) {
 
 AD void leaf_sample(const DBsdf &d, uint32_t ctx, f3 wi, float u1, float u2, BSample &bs, C3 &w) {
     bs = bs_zero();
-    if (d.type == BSDF_DIFFUSE) {
-        bool a = wi.z > 0.f;
-        if (!ctx_on(ctx, BF_DiffuseReflection)) { w = c3(0.f); return; }
-        bs.wo = cosine_hemisphere(u1, u2);
-        bs.pdf = kInvPi * bs.wo.z;
-        bs.eta = 1.f;
-        bs.type = BF_DiffuseReflection;
-        w = (a && bs.pdf > 0.f) ? c3(d.refl) : c3(0.f);
-        return;
-    }
+    if (d.type == BSDF_DIFFUSE) { diffuse_sample(d, ctx, wi, u1, u2, bs, w); return; }
     bool a = wi.z > 0.f;
     if (!ctx_on(ctx, BF_GlossyReflection)) { w = c3(0.f); return; }
     Mf mf(d);
@@ -203,25 +206,36 @@ AD f3 ts_wo(const TwoSided &r, f3 wi, f3 wo) {
     return r.flip == 1u ? mk(wo.x, wo.y, -wo.z) : (r.flip == 2u ? mk(wo.x, wo.y, mulsign(wo.z, wi.z)) : wo);
 }
 
+/*
+ * Dispatch.  kDiff: the scene's BSDFs are all plain `diffuse` (the host checks), so
+ * the call is diffuse.cpp alone -- no twosided resolve, no microfacet code in the
+ * kernel (fewer registers), same arithmetic.
+ */
+template <bool kDiff = false>
 AD void bsdf_eval_pdf(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, f3 wo, bool active, C3 &val, float &pdf) {
     val = c3(0.f); pdf = 0.f;
     if (b < 0 || !active) return;
+    if (kDiff) { diffuse_eval_pdf(T[b], ctx, wi, wo, val, pdf); return; }
     const TwoSided r = resolve_twosided(T, b, wi);
     if (r.leaf < 0) return;
     leaf_eval_pdf(T[r.leaf], ctx, ts_wi(r, wi), ts_wo(r, wi, wo), val, pdf);
 }
 
+template <bool kDiff = false>
 AD float bsdf_pdf(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, f3 wo, bool active) {
     if (b < 0 || !active) return 0.f;
+    if (kDiff) return diffuse_pdf(ctx, wi, wo);
     const TwoSided r = resolve_twosided(T, b, wi);
     if (r.leaf < 0) return 0.f;
     return leaf_pdf(T[r.leaf], ctx, ts_wi(r, wi), ts_wo(r, wi, wo));
 }
 
+template <bool kDiff = false>
 AD void bsdf_sample(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, float u1, float u2, bool active, BSample &bs,
                     C3 &w) {
     bs = bs_zero(); w = c3(0.f);
     if (b < 0 || !active) return;
+    if (kDiff) { diffuse_sample(T[b], ctx, wi, u1, u2, bs, w); return; }
     const TwoSided r = resolve_twosided(T, b, wi);
     if (r.leaf < 0) return;
     leaf_sample(T[r.leaf], ctx, ts_wi(r, wi), u1, u2, bs, w);
@@ -232,8 +246,10 @@ AD void bsdf_sample(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, float u1, fl
 AD float leaf_roughness(const DBsdf &d) {
     return d.type == BSDF_DIFFUSE ? 1.f : dsqrt(0.5f * (sqr(d.alpha_u) + sqr(d.alpha_v)));
 }
+template <bool kDiff = false>
 AD float bsdf_roughness(const DBsdf *T, int32_t b, f3 wi) {
     if (b < 0) return 0.f;
+    if (kDiff) return 1.f;
     const DBsdf &d = T[b];
     if (d.type != BSDF_TWOSIDED) return leaf_roughness(d);
     if (d.nested0 == d.nested1) return leaf_roughness(T[d.nested0]);

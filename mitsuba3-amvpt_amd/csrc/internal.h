@@ -14,6 +14,7 @@ struct amvpt_scene {
     void *dev_scene_struct = nullptr; /* device copy of `dev` */
     std::vector<void *> allocations;
     uint32_t n_nodes = 0, n_prims = 0;
+    bool all_diffuse = false;   /* every BSDF is plain `diffuse`: kernels take their kDiff instances */
     int device = 0;
 };
 
@@ -26,6 +27,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream);
 extern uint64_t g_chunk_lanes;
 extern uint32_t g_traversal;
+extern bool g_diffuse_spec;
 extern amvpt_exchange_fn g_exchange;
 extern void *g_exchange_ctx;
 } // namespace amvpt
