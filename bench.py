@@ -153,21 +153,16 @@ def main():
     vbar = verts / max(1, lanes)
     hbar = c["reuse_lanes"] / max(1, lanes)
     stage_ms = {"primary": c["kernel_ms_primary"], "bounce": c["kernel_ms_bounce"], "splat": c["kernel_ms_splat"]}
-    # algorithmic bytes per stage (DESIGN.md "Byte model")
-    suffix_verts = max(0, verts - lanes)
-    live_after_primary = suffix_verts  # upper bound proxy: every suffix vertex was pushed once
-    atomics = c["view_splats"]
-    bytes_stage = {
-        "primary": lanes * (48 * G + 32) + 96 * min(lanes, live_after_primary),
-        "bounce": suffix_verts * 192,
-        "splat": lanes * (48 * G + 32),
-    }
-    dom = max(stage_ms, key=lambda k: stage_ms[k])
-    achieved = bytes_stage[dom] / (stage_ms[dom] * 1e-3) / 1e9
-    kernel_name = {"primary": "k_mv_primary<%d>" % G if G > 1 else "k_raygen_single", "bounce": "k_bounce",
-                   "splat": "k_splat_multi<%d, %d>" % (G, C) if G > 1 else "k_splat_single<%d>" % C}[dom]
-    chunks = n_passes * ((samples_per_rank // n_passes + CHUNK_LANES - 1) // CHUNK_LANES)
-    launches = {"primary": chunks, "splat": chunks, "bounce": None}[dom]
+    kms, kl = c["kernel_ms"], c["kernel_launches"]
+    bytes_kernel = kernel_bytes(c, G, C)
+    # the dominant single kernel (HIP events around each launch on the render stream)
+    dom = max((k for k in kms if kl[k]), key=lambda k: kms[k])
+    launches = kl[dom]
+    per_launch_bytes = bytes_kernel[dom] / launches
+    achieved = per_launch_bytes / (kms[dom] / launches * 1e-3) / 1e9
+    kernel_name = {"k_splat": ("k_splat_multi<%d, %d>" % (G, C)) if G > 1 else "k_splat_single<%d>" % C,
+                   "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
+                   "k_prim_req": "k_prim_req<%d," % G}.get(dom, dom + "<")
     traffic, traffic_src = pmc_traffic(kernel_name, headline)
     # SURVEY 8(d) whole-pipeline byte model
     P = p.film_width * p.film_height
@@ -206,17 +201,21 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": kernel_name,
+                "kernel": dom,
+                "kernel_symbol": kernel_name,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": (bytes_stage[dom] // launches) if launches else None,
+                "algorithmic_bytes_per_launch": int(per_launch_bytes),
+                "avg_launch_ms": round(kms[dom] / launches, 4),
                 "launches_per_step": launches,
                 "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
-                "stage_bytes": bytes_stage,
+                "kernel_ms": {k: round(v, 3) for k, v in kms.items() if kl[k]},
+                "kernel_launches": {k: v for k, v in kl.items() if v},
+                "kernel_bytes": {k: int(v) for k, v in bytes_kernel.items() if kl[k]},
                 "pipeline_model": {"B_sample": round(B_sample, 1), "vbar": round(vbar, 4), "hbar": round(hbar, 4),
                                    "achieved_GBs": round(pipeline_gbs, 2),
                                    "frac": round(pipeline_gbs / HBM_PEAK_GBS, 5)},
@@ -228,6 +227,27 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_bytes(c, G, C):
+    """Algorithmic HBM bytes per frame of each kernel: every SoA
+    stream element is written once by its producer and read once by its consumer."""
+    lanes, verts, shadow = c["lanes"], c["vertices"], c["shadow_rays"]
+    suffix = max(0, verts - lanes)        # suffix vertices (k_extend / k_bounce entries)
+    pushed = min(lanes, suffix)           # paths that left the primary vertex (= paths that terminate)
+    rec = 48 * G + 32                     # view records (3 x 16 B x G) + lane_rec + lane_out
+    adapt = c["adaptive_lanes"]
+    return {
+        "k_prim_hit": 16 * lanes,                                   # hit record out
+        "k_prim_req": (16 + 48) * lanes,                            # hit in, visibility requests out
+        "k_vis": (48 + G / 8.0) * lanes,                            # requests in (once), ballots out
+        "k_mv_primary": (16 + G / 8.0 + rec) * lanes + 96 * pushed,  # hit + ballots in, records + paths out
+        "k_raygen": 96 * (lanes if G == 1 else adapt),              # path state out
+        "k_extend": 48 * suffix,                                    # ray in, hit out
+        "k_bounce": 112 * suffix + 96 * (suffix - pushed) + 64 * shadow + 16 * pushed,
+        "k_shadow": 96 * shadow,                                    # NEE record in, result read-modify-write
+        "k_splat": rec * lanes + 16 * adapt,                        # records in (film: PMC WRITE_SIZE)
+    }
 
 
 def pmc_traffic(kernel_name, full_size):

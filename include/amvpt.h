@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 3
+#define AMVPT_ABI_VERSION 4
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -176,12 +176,30 @@ typedef struct amvpt_counters {
     uint64_t visibility_rays;  /* camera-visibility rays traced in camera_selection */
     uint64_t view_splats;      /* valid view samples splatted */
     uint64_t adaptive_lanes;   /* lanes re-traced by the adaptive pass */
-    double kernel_ms_primary;  /* HIP-event time of the dominant kernels (summed) */
-    double kernel_ms_bounce;
-    double kernel_ms_splat;
+    double kernel_ms_primary;  /* HIP-event time per stage: primary wavefronts (or raygen), */
+    double kernel_ms_bounce;   /* the suffix (extend + bounce + shadow, all depths), */
+    double kernel_ms_splat;    /* the splat */
     double total_ms;
     uint64_t splat_fallback;   /* view samples splatted with direct global atomics (LDS window miss) */
+    /* ABI 4: per-kernel HIP-event time and launch count, indexed by amvpt_kernel_id */
+    uint64_t shadow_rays;      /* suffix NEE rays traced by k_shadow */
+    double kernel_ms[12];
+    uint64_t kernel_launches[12];
 } amvpt_counters;
+
+/* kernels of the pipeline, for amvpt_counters.kernel_ms */
+typedef enum amvpt_kernel_id {
+    AMVPT_K_PRIM_HIT = 0,      /* raygen + primary closest hit            */
+    AMVPT_K_PRIM_REQ = 1,      /* shadow / visibility ray requests        */
+    AMVPT_K_VIS = 2,           /* visibility + primary shadow any-hit     */
+    AMVPT_K_MV_PRIMARY = 3,    /* camera selection, MIS, direct light     */
+    AMVPT_K_RAYGEN = 4,        /* G = 1 / adaptive raygen                 */
+    AMVPT_K_EXTEND = 5,        /* suffix closest hit                      */
+    AMVPT_K_BOUNCE = 6,        /* suffix shading                          */
+    AMVPT_K_SHADOW = 7,        /* suffix NEE any-hit                      */
+    AMVPT_K_SPLAT = 8,         /* ImageBlock::put                         */
+    AMVPT_K_COUNT = 9
+} amvpt_kernel_id;
 
 typedef struct amvpt_scene amvpt_scene; /* opaque device-resident scene */
 
@@ -236,8 +254,9 @@ amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t
 
 /* Tuning knobs (0 keeps the default). chunk_lanes bounds the lane arena per launch. */
 amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes);
-/* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane), 1 force wave-uniform,
- * 2 force per-lane.  Results are identical in every mode (closest hit = min (t, prim)). */
+/* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane; scenes of <= 48
+ * primitives test every primitive in the suffix walks instead), 1 force the wave-uniform
+ * BVH walk, 2 force per-lane.  Results are identical in every mode (closest hit = min (t, prim)). */
 amvpt_status amvpt_set_traversal(uint32_t mode);
 /* BVH build of later amvpt_scene_create calls: leaves keep up to max_leaf_prims (1..15,
  * default 4) primitives unless splitting is cheaper; a split costs traversal_cost

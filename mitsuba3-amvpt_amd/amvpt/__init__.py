@@ -73,10 +73,19 @@ class Counters(ctypes.Structure):
     _fields_ = [("lanes", u64), ("passes", u64), ("vertices", u64), ("reuse_lanes", u64),
                 ("visibility_rays", u64), ("view_splats", u64), ("adaptive_lanes", u64),
                 ("kernel_ms_primary", f64), ("kernel_ms_bounce", f64), ("kernel_ms_splat", f64),
-                ("total_ms", f64), ("splat_fallback", u64)]
+                ("total_ms", f64), ("splat_fallback", u64),
+                ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        for k in ("kernel_ms", "kernel_launches"):
+            d[k] = {name: d[k][i] for i, name in enumerate(KERNELS)}
+        return d
+
+
+# amvpt_kernel_id (include/amvpt.h): index -> name of Counters.kernel_ms / kernel_launches
+KERNELS = ("k_prim_hit", "k_prim_req", "k_vis", "k_mv_primary", "k_raygen", "k_extend", "k_bounce", "k_shadow",
+           "k_splat")
 
 
 INTEGRATOR_MVPATH, INTEGRATOR_PATH = 0, 1
@@ -238,7 +247,7 @@ def plan(params):
 
 
 def set_traversal(mode):
-    """BVH walk: 0 auto, 1 wave-uniform, 2 per-lane (amvpt_set_traversal)."""
+    """BVH walk: 0 auto (brute force for tiny scenes), 1 wave-uniform, 2 per-lane (amvpt_set_traversal)."""
     L = hip_lib()
     _check(L.amvpt_set_traversal(u32(mode)), L)
 

@@ -260,6 +260,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     *out = nullptr;
     if (!device_ok()) { set_error("amvpt_scene_create: no HIP device visible (the product path has no CPU fallback)"); return AMVPT_ERR_NO_DEVICE; }
     if (d->has_environment) { set_error("environment emitters are outside the implemented path"); return AMVPT_ERR_UNSUPPORTED; }
+    bool has_spheres = false;
     /* validate */
     for (uint32_t i = 0; i < d->bsdf_count; ++i) {
         const amvpt_bsdf_desc &b = d->bsdfs[i];
@@ -351,7 +352,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
                 DPrim p{};
                 const float *P0 = s.positions + 3 * s.faces[3 * f], *P1 = s.positions + 3 * s.faces[3 * f + 1],
                             *P2 = s.positions + 3 * s.faces[3 * f + 2];
-                for (int k = 0; k < 3; ++k) { p.a[k] = P0[k]; p.b[k] = P1[k]; p.c[k] = P2[k]; }
+                /* p0 and the two edges (the f32 differences tri_hit would form: same bits) */
+                for (int k = 0; k < 3; ++k) { p.a[k] = P0[k]; p.b[k] = P1[k] - P0[k]; p.c[k] = P2[k] - P0[k]; }
                 p.type = PRIM_TRI; p.shape = i; p.face = f;
                 p.pad = (uint32_t) scene_prims.size();
                 BuildPrim bp;
@@ -368,6 +370,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
             DPrim p{};
             p.a[0] = s.center[0]; p.a[1] = s.center[1]; p.a[2] = s.center[2]; p.a[3] = s.radius;
             p.type = PRIM_SPHERE; p.shape = i; p.face = 0;
+            has_spheres = true;
             p.pad = (uint32_t) scene_prims.size();
             BuildPrim bp;
             for (int k = 0; k < 3; ++k) { bp.box.lo[k] = s.center[k] - s.radius; bp.box.hi[k] = s.center[k] + s.radius; }
@@ -442,6 +445,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (faces.empty()) faces.resize(3, 0);
 
     amvpt_scene *sc = new amvpt_scene();
+    sc->has_spheres = has_spheres;
     (void) hipGetDevice(&sc->device);
     auto upload = [&](const void *src, size_t bytes, void **dst) -> amvpt_status {
         hipError_t e = hipMalloc(dst, bytes);

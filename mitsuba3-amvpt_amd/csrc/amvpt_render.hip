@@ -44,6 +44,21 @@ void *g_exchange_ctx = nullptr;
 /* Parameters                                                         */
 /* ------------------------------------------------------------------ */
 
+/* Walk of the suffix kernels (k_extend, k_shadow), a compile-time choice per scene:
+ * per-lane threaded BVH, wave-uniform BVH, or brute force over every primitive
+ * (tiny scenes; measured on the Cornell box: k_extend 114 -> 100 ms, k_shadow 103 -> 81 ms
+ * per config-M frame; brute force in the coherent primary / visibility walks was slower:
+ * k_vis 90 -> 248 ms, k_prim_hit 12 -> 30 ms). */
+enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */ };
+template <int kWalk> AD Hit walk_closest(const SceneRef &sc, const Ray &r) {
+    if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_closest<kWalk == WALK_BRUTE>(sc, r);
+    return trace_closest<kWalk == WALK_UNI>(sc, r);
+}
+template <int kWalk> AD bool walk_any(const SceneRef &sc, const Ray &r) {
+    if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_any<kWalk == WALK_BRUTE>(sc, r);
+    return trace_any<kWalk == WALK_UNI>(sc, r);
+}
+
 struct KParams {
     uint32_t W, H, C;
     uint32_t spp_pp, log_spp, pow2;
@@ -928,7 +943,7 @@ __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V,
  * The accumulation order of a lane's result is the reference's: emitter hit of
  * vertex d, then NEE of vertex d, then vertex d + 1.
  */
-template <bool kUni>
+template <int kWalk>
 __global__ void __launch_bounds__(256) k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -944,12 +959,12 @@ __global__ void __launch_bounds__(256) k_extend(KParams P, const DScene *Sp, Buf
         if (e0 + threadIdx.x < count) {
             const float4 a = B.q_in[0][i], b = B.q_in[1][i];
             const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest};
-            B.hit[i] = hit_rec(trace_closest<kUni>(sc, r));
+            B.hit[i] = hit_rec(walk_closest<kWalk>(sc, r));
         }
     }
 }
 
-template <bool kUni>
+template <int kWalk>
 __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -961,7 +976,7 @@ __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Buf
         if (e0 + threadIdx.x < count) {
             const float4 a = B.nee[0][i], b = B.nee[1][i];
             const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z};
-            if (!trace_any<kUni>(sc, r)) {
+            if (!walk_any<kWalk>(sc, r)) {
                 const float4 t = B.nee[2][i], c = B.nee[3][i];
                 const uint32_t dest = fbits(b.w);
                 float4 *const dp = (dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest];
@@ -978,14 +993,14 @@ __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Buf
 #ifndef AMVPT_BOUNCE_WAVES
 #define AMVPT_BOUNCE_WAVES 4
 #endif
-template <bool kTab>
+template <bool kTab, bool kDiff>
 __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
-    unsigned long long verts = 0;
+    unsigned long long verts = 0, shadows = 0;
     for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
         const uint32_t i = pbase + e0 + threadIdx.x;
         bool ok = e0 + threadIdx.x < count;
@@ -1026,10 +1041,10 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             (void) s1;
             C3 bval;
             float bpdf;
-            bsdf_eval_pdf(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
+            bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
             BSample bs;
             C3 bw;
-            bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
+            bsdf_sample<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
             if (active_em) {
                 float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
                 nee = true;
@@ -1057,6 +1072,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
         const uint32_t slot = push_slot(keep, B.cnt_out, B.qcap);
         if (keep) store_state(B.q_out, slot, s);
         const uint32_t ns = push_slot(nee, B.cnt_nee, B.qcap);
+        shadows += nee ? 1 : 0;
         if (nee) {
             const uint32_t dest = keep ? slot : (0x80000000u | s.idx);
             B.nee[0][ns] = make_float4(shr.o.x, shr.o.y, shr.o.z, shr.d.x);
@@ -1065,7 +1081,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             B.nee[3][ns] = make_float4(nee_c.r, nee_c.g, nee_c.b, 0.f);
         }
     }
-    if (B.stats) stat_add(B.stats, 0, verts);
+    if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
 }
 
 /* ------------------------------------------------------------------ */
@@ -1183,7 +1199,7 @@ __global__ void __launch_bounds__(256) k_prim_hit(KParams P, const DScene *Sp, c
     }
 }
 
-template <int G, bool kTab>
+template <int G, bool kTab, bool kDiff>
 __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -1207,7 +1223,7 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
         const float r2a = pr.rng.next_1d(), r2b = pr.rng.next_1d();
         BSample bsmp;
         C3 bsdf_weight;
-        bsdf_sample(S.bsdfs, b, CTX_ALL, si.wi, r2a, r2b, true, bsmp, bsdf_weight);
+        bsdf_sample<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, r2a, r2b, true, bsmp, bsdf_weight);
         const bool delta = (bsmp.type & BF_Delta) != 0 || (bsmp.type & BF_Null) != 0;
         const bool reuse = !direct_em && !delta && p_hit && bsdf_smooth;
         const bool p_face = si.wi.z > 0.f;
@@ -1785,22 +1801,90 @@ struct Arena {
 };
 static Arena g_arena;
 
+/* Per-kernel HIP-event timing of an instrumented render (amvpt_counters given): an
+ * event pair around every launch on the render stream, resolved in batches. */
+#ifndef AMVPT_FLUSH_MARKS
+#define AMVPT_FLUSH_MARKS 1
+#endif
+struct KTimer {
+    static constexpr size_t kPairs = 128;
+    bool on = false;
+    hipError_t err = hipSuccess;
+    hipEvent_t ev[2 * kPairs] = {};
+    int kid[kPairs] = {};
+    size_t n = 0;
+    double ms[AMVPT_K_COUNT] = {};
+    uint64_t launches[AMVPT_K_COUNT] = {};
+    void init(bool enable) {
+        on = enable;
+        if (!on) return;
+        for (auto &e : ev)
+            if (err == hipSuccess) err = hipEventCreate(&e);
+    }
+    void flush() {
+        if (!on || n == 0 || err != hipSuccess) return;
+        err = hipEventSynchronize(ev[2 * n - 1]);
+        for (size_t i = 0; i < n && err == hipSuccess; ++i) {
+            float t = 0.f;
+            err = hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
+            ms[kid[i]] += t;
+            launches[kid[i]] += 1;
+        }
+        n = 0;
+    }
+    void begin(int k, hipStream_t st) {
+        if (!on || err != hipSuccess) return;
+        if (n == kPairs) flush();
+        kid[n] = k;
+        err = hipEventRecord(ev[2 * n], st);
+    }
+    void end(hipStream_t st) {
+        if (!on || err != hipSuccess) return;
+        err = hipEventRecord(ev[2 * n + 1], st);
+        ++n;
+    }
+    /* stage markers when not timing: a timing-enabled event record after each stage
+     * (measured: a frame without them, or with hipEventDisableTiming markers, ran ~2 %
+     * slower; AMVPT_FLUSH_MARKS A/B) */
+    hipEvent_t mark_ev = nullptr;
+    void mark(hipStream_t st) {
+        if (on || !AMVPT_FLUSH_MARKS) return;
+        if (!mark_ev && hipEventCreate(&mark_ev) != hipSuccess) return;
+        (void) hipEventRecord(mark_ev, st);
+    }
+    ~KTimer() {
+        for (auto &e : ev)
+            if (e) (void) hipEventDestroy(e);
+        if (mark_ev) (void) hipEventDestroy(mark_ev);
+    }
+};
+
 /* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
 template <int G>
 static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
-                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff) {
+                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T) {
     const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPrimBlock - 1) / kPrimBlock);
     const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * G * kPrimBlock * sizeof(float);
+    T.begin(AMVPT_K_PRIM_HIT, st);
     if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
-    if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    T.end(st);
+    T.begin(AMVPT_K_PRIM_REQ, st);
+    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+    T.end(st);
+    T.begin(AMVPT_K_VIS, st);
     if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
+    T.end(st);
+    T.begin(AMVPT_K_MV_PRIMARY, st);
     if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
     else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
     else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    T.end(st);
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
@@ -1809,7 +1893,7 @@ static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs
 }
 
 typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
-                           const Bufs &, bool, bool, bool);
+                           const Bufs &, bool, bool, bool, KTimer &);
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
 static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>};
@@ -1995,12 +2079,20 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
     const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
     const bool uni = scene_uniform(scene->dev.n_nodes, g_traversal);
+    /* suffix walk: brute force for tiny scenes in auto mode (AMVPT_BRUTE=0 turns it off, A/B) */
+    int walk = uni ? WALK_UNI : WALK_LANE;
+    {
+        const char *e = std::getenv("AMVPT_BRUTE");
+        const bool brute_on = !(e && e[0] == '0');
+        if (uni && g_traversal == 0u && brute_on && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
+    }
+    const bool diff = scene->all_diffuse && g_diffuse_spec;                                        /* kDiff instances */
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
-    hipEvent_t ev[4];
-    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
-    float ms_primary = 0.f, ms_bounce = 0.f, ms_splat = 0.f;
+    KTimer T;
+    T.init(counters != nullptr);
+    HIPCHK(T.err);
     auto t0 = std::chrono::steady_clock::now();
     const uint32_t max_bounces = P.max_depth == 0xffffffffu ? 0xffffffffu : P.max_depth + 1;
 
@@ -2018,13 +2110,26 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.cnt_in = a_is_in ? cntA : cntB;
             B.cnt_out = a_is_in ? cntB : cntA;
             /* k_extend zeroes cnt_out and cnt_nee */
-            if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<true>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<false>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            if (tab_b) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
-            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
-            if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<true>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<false>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            T.begin(AMVPT_K_EXTEND, st);
+            if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            T.end(st);
+            T.begin(AMVPT_K_BOUNCE, st);
+            if (tab_b && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true, true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            else if (tab_b) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true, false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false, true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false, false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            T.end(st);
+            T.begin(AMVPT_K_SHADOW, st);
+            if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            T.end(st);
             HIPCHK(hipGetLastError());
+            HIPCHK(T.err);
             a_is_in = !a_is_in;
             if (bnc >= 15 && (bnc & 7) == 7) { /* unbounded depth: poll the live count */
                 std::vector<uint32_t> hc((size_t) kQParts * kCntStride);
@@ -2052,31 +2157,30 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
             for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
             B.cnt_out = cntA; B.cnt_in = cntB;
-            HIPCHK(hipEventRecord(ev[0], st));
+            T.mark(st);
             if (G == 1) {
+                T.begin(AMVPT_K_RAYGEN, st);
                 hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
+                T.end(st);
             } else {
-                kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, scene->all_diffuse && g_diffuse_spec);
+                kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, diff, T);
             }
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev[1], st));
+            HIPCHK(T.err);
+            T.mark(st);
             /* suffix bounces: ping-pong A <-> B */
             { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
-            HIPCHK(hipEventRecord(ev[2], st));
+            T.mark(st);
             const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
+            T.begin(AMVPT_K_SPLAT, st);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else if (G == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else kSplat[G](sgrid, st, P, B);
+            T.end(st);
+            T.mark(st);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev[3], st));
-            if (counters) {
-                HIPCHK(hipEventSynchronize(ev[3]));
-                float a = 0, b = 0, c = 0;
-                HIPCHK(hipEventElapsedTime(&a, ev[0], ev[1]));
-                HIPCHK(hipEventElapsedTime(&b, ev[1], ev[2]));
-                HIPCHK(hipEventElapsedTime(&c, ev[2], ev[3]));
-                ms_primary += a; ms_bounce += b; ms_splat += c;
-            }
+            T.flush();
+            HIPCHK(T.err);
         }
         if (do_fill) {
             /* compact the pass's adapt_mask lanes in lane order, then n_adapt re-traces each */
@@ -2115,13 +2219,19 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
                 for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
                 B.cnt_out = cntA; B.cnt_in = cntB;
+                T.begin(AMVPT_K_RAYGEN, st);
                 hipLaunchKernelGGL(k_raygen_adapt, dim3((cn + 255) / 256), dim3(256), 0, st, P, dviews, B);
+                T.end(st);
                 HIPCHK(hipGetLastError());
                 { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
                 const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
+                T.begin(AMVPT_K_SPLAT, st);
                 if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_adapt<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
                 else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_adapt<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
+                T.end(st);
                 HIPCHK(hipGetLastError());
+                T.flush();
+                HIPCHK(T.err);
             }
             P = Ps;
         }
@@ -2143,12 +2253,16 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.view_splats = hs[3];
         c.splat_fallback = hs[4];
         c.adaptive_lanes = adaptive_lanes;
-        c.kernel_ms_primary = ms_primary;
-        c.kernel_ms_bounce = ms_bounce;
-        c.kernel_ms_splat = ms_splat;
+        c.shadow_rays = hs[5];
+        T.flush();
+        HIPCHK(T.err);
+        for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }
+        c.kernel_ms_primary = T.ms[AMVPT_K_PRIM_HIT] + T.ms[AMVPT_K_PRIM_REQ] + T.ms[AMVPT_K_VIS] +
+                              T.ms[AMVPT_K_MV_PRIMARY] + T.ms[AMVPT_K_RAYGEN];
+        c.kernel_ms_bounce = T.ms[AMVPT_K_EXTEND] + T.ms[AMVPT_K_BOUNCE] + T.ms[AMVPT_K_SHADOW];
+        c.kernel_ms_splat = T.ms[AMVPT_K_SPLAT];
         c.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    for (auto &e : ev) (void) hipEventDestroy(e);
     return AMVPT_OK;
 }
 

@@ -54,8 +54,7 @@ AD bool rect_hit(const DPrim &p, const Ray &r, float &t, float &lx, float &ly) {
 }
 
 AD bool tri_hit(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
-    f3 p0 = ld3(p.a), p1 = ld3(p.b), p2 = ld3(p.c);
-    f3 e1 = p1 - p0, e2 = p2 - p0;
+    const f3 p0 = ld3(p.a), e1 = ld3(p.b), e2 = ld3(p.c);   /* edges precomputed by the host */
     f3 pvec = cross(r.d, e2);
     float inv_det = rcp(dot(e1, pvec));
     f3 tvec = r.o - p0;
@@ -269,6 +268,59 @@ template <bool kUni> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
         node = (hit && !count) ? node + 1 : skip;
     }
     return false;
+}
+
+/*
+ * Brute-force walks for tiny scenes (n_prims <= kBrutePrims, wave-uniform kernels only):
+ * every primitive is tested in BVH order with the next record's scalar load issued
+ * before the current test, so there are no dependent node loads and no box tests.
+ * For incoherent rays (suffix extension / NEE) a wave enters nearly every node of a
+ * Cornell-sized BVH anyway.  Same (t, scene-order index) rule -> the same hit.
+ */
+constexpr uint32_t kBrutePrims = 48;
+/* kSph = false: the scene has no sphere (no f64 sphere code, fewer registers) */
+template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
+    if (!kSph || type != PRIM_SPHERE) {
+        if (type == PRIM_RECT) return rect_hit(p, r, t, u, v);
+        return tri_hit(p, r, t, u, v);
+    }
+    u = v = 0.f;
+    return sphere_hit(p, r, t);
+}
+
+template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
+    Hit best{kInf, 0.f, 0.f, -1};
+    uint32_t best_orig = 0xffffffffu;
+    const uint32_t np = ufirst(sc.g->n_prims);
+    DPrim nxt = load_uniform(sc.gprims, 0);
+    for (uint32_t pi = 0; pi < np; ++pi) {
+        const DPrim p = nxt;
+        if (pi + 1 < np) nxt = load_uniform(sc.gprims, pi + 1);
+        float t, u, v;
+        if (prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v)) {
+            const uint32_t orig = ufirst(p.pad);
+            if (t < best.t || (t == best.t && orig < best_orig)) {
+                best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                best_orig = orig;
+            }
+        }
+    }
+    return best;
+}
+
+template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray) {
+    const uint32_t np = ufirst(sc.g->n_prims);
+    bool found = false;
+    DPrim nxt = load_uniform(sc.gprims, 0);
+    for (uint32_t pi = 0; pi < np; ++pi) {
+        const DPrim p = nxt;
+        if (pi + 1 < np) nxt = load_uniform(sc.gprims, pi + 1);
+        float t, u, v;
+        const bool h = !found && prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v);
+        found = found || h;
+        if (!wave_any(!found)) break;
+    }
+    return found;
 }
 
 /* SurfaceInteraction3f restricted to what the path reads. */

@@ -83,6 +83,15 @@ def test_mvpath_amvpt_mis_g8_two_passes(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
+@pytest.mark.parametrize("res,spp,kw", [(48, 16, dict()), (24, 32, dict(gx=4, gy=2, reuse=8))])
+def test_generic_kernels_on_diffuse_scene(gpu_ready, amvpt_mod, oracle, monkeypatch, res, spp, kw):
+    """The Cornell box is all-diffuse, so it normally runs the kDiff kernel instances;
+    AMVPT_NO_DIFFUSE_SPEC=1 forces the generic ones, which must agree just as well."""
+    monkeypatch.setenv("AMVPT_NO_DIFFUSE_SPEC", "1")
+    s = amvpt_mod.load_file(CBOX, res=res, spp=spp, **kw)
+    _check(amvpt_mod, oracle, s)
+
+
 def test_mvpath_reuse_without_mis(gpu_ready, amvpt_mod, oracle):
     s = amvpt_mod.load_file(CBOX, res=48, spp=16, sa_mis="false")
     _check(amvpt_mod, oracle, s)
@@ -149,10 +158,12 @@ def test_veach_single_view_g1(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["wave_uniform_bvh", "per_lane_bvh"])
 @pytest.mark.parametrize("scene", ["cbox", "veach"])
-def test_per_lane_traversal_matches(gpu_ready, amvpt_mod, oracle, scene):
-    """The per-lane threaded-BVH walk (large scenes) gives the same records as the oracle."""
-    amvpt_mod.set_traversal(2)
+def test_bvh_walks_match(gpu_ready, amvpt_mod, oracle, scene, mode):
+    """Auto mode brute-forces the suffix walks of these tiny scenes; the wave-uniform (mode 1) and
+    per-lane (mode 2, large scenes) threaded-BVH walks must give the same records as the oracle."""
+    amvpt_mod.set_traversal(mode)
     try:
         s = amvpt_mod.load_file(CBOX if scene == "cbox" else VEACH, res=24, spp=16, gx=4, gy=2, reuse=8)
         _check(amvpt_mod, oracle, s)

@@ -1,0 +1,69 @@
+"""Timed Msamples/s of config M for each variant: a library dir or an environment setting.
+
+    python tools/ab_value.py <libdir> [<libdir> ...]    (dirs relative to mitsuba3-amvpt_amd/)
+    python tools/ab_value.py --env AMVPT_BRUTE=0 --env AMVPT_BRUTE=1 ...   (current lib/)
+Each variant runs in its own child process (one ctypes load per process).  With --kernels
+the child also reports one instrumented frame's per-kernel HIP-event ms (ABI >= 4 only).
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(steps=3, kernels=False):
+    sys.path[:0] = [REPO, os.path.join(REPO, "mitsuba3-amvpt_amd")]
+    import torch
+    import amvpt
+    s = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), res=1024, spp=64, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    dev = amvpt.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    lanes = p.film_width * p.film_height * 64
+    dev.render(vd, p, film.data_ptr())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dev.render(vd, p, film.data_ptr())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"variant": os.environ.get("AB_VARIANT", "lib"), "msamples_s": round(lanes * steps / dt / 1e6, 2),
+           "ms_per_frame": round(dt * 1e3 / steps, 2)}
+    if kernels:
+        c = amvpt.Counters()
+        dev.render(vd, p, film.data_ptr(), counters=c)
+        torch.cuda.synchronize()
+        d = c.as_dict()
+        out["kernel_ms"] = {k: round(v, 2) for k, v in d["kernel_ms"].items() if v}
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    args = sys.argv[1:]
+    kernels = "--kernels" in args
+    args = [a for a in args if a != "--kernels"]
+    if args[:1] == ["--child"]:
+        child(kernels=kernels)
+        return
+    variants = []
+    while args:
+        a = args.pop(0)
+        if a == "--env":
+            kv = args.pop(0)
+            env = dict(os.environ, AB_VARIANT=kv)
+            for item in kv.split(","):
+                k, v = item.split("=", 1)
+                env[k] = v
+            variants.append(env)
+        else:
+            variants.append(dict(os.environ, AB_VARIANT=a, AMVPT_LIB_DIR=os.path.join(REPO, "mitsuba3-amvpt_amd", a)))
+    for env in variants:
+        cmd = [sys.executable, os.path.abspath(__file__), "--child"] + (["--kernels"] if kernels else [])
+        subprocess.run(cmd, env=env, check=True, timeout=300)
+
+
+if __name__ == "__main__":
+    main()
