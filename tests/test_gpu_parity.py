@@ -282,3 +282,18 @@ def test_file_meshes_per_lane_bvh(gpu_ready, amvpt_mod, oracle):
     n_nodes, n_prims = amvpt_mod.DeviceScene(sd).stats()
     assert n_nodes > 255 and n_prims == 6 + 1280 + 2304
     _check(amvpt_mod, oracle, s)
+
+
+@pytest.mark.parametrize("chunk", [8192, 5000])
+def test_many_chunks_per_pass(gpu_ready, amvpt_mod, oracle, chunk):
+    """Many lane chunks per pass (the arena bound at full size): records stay bit-identical, the film
+    equal up to atomic order.  5000 is not a multiple of the 1024-lane splat super-block (identity
+    slot map at the seams)."""
+    amvpt_mod.set_chunk_lanes(chunk)
+    try:
+        s = amvpt_mod.load_file(CBOX, res=24, spp=32, gx=4, gy=2, reuse=8)
+        sd, vd, p = s.describe(0, 0, 0)
+        assert oracle.plan(p)["lanes"] > 4 * chunk
+        _check(amvpt_mod, oracle, s)
+    finally:
+        amvpt_mod.set_chunk_lanes(1 << 23)
