@@ -90,7 +90,7 @@ struct Bufs {
     uint32_t qcap;               /* entries per queue partition */
     float4 *lane_out;     /* (indirect / result rgb, valid_ray) */
     float4 *lane_rec;     /* (pdfW, flags) */
-    float4 *view_rec;     /* [3][G][n]: (pos, weight, flags), (result), (bsdf_val) */
+    float4 *view_rec;     /* [3][G][n]: (pos | weight, flags) as two float2 planes, (result), (bsdf_val) */
     float *film;
     float *records;       /* optional [n][G][8] */
     unsigned long long *stats; /* [0] vertices [1] reuse lanes [2] visibility rays [3] splats */
@@ -1315,6 +1315,9 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #ifndef AMVPT_PRIM_TAB
 #define AMVPT_PRIM_TAB 1
 #endif
+#ifndef AMVPT_PRIM_SLOT_ORDER
+#define AMVPT_PRIM_SLOT_ORDER 1
+#endif
 #ifndef AMVPT_PRIM_WAVES
 #define AMVPT_PRIM_WAVES 1
 #endif
@@ -1333,11 +1336,20 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
     float *const vs = reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
 #define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
+#if AMVPT_PRIM_SLOT_ORDER
+    /* threads run in slot order (a wave = 64 pixels of one sample, see slot_lane), so every
+     * record store of a wave is 64 contiguous slots; the hit and the ballots are read at the
+     * lane (16-B loads 256 B apart) */
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = slot < P.chunk_n;
+    const uint32_t i = ok ? slot_lane(P, slot) : 0u;
+#else
     /* threads run in lane order (a wave = 4 pixels x 16 samples); records go to the
      * lane's slot (see slot_lane) */
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = i < P.chunk_n;
     const uint32_t slot = ok ? lane_slot(P, i) : 0u;
+#endif
     PathState ps;
     bool push = false;
     unsigned long long st_reuse = 0, st_vis = 0;
@@ -1354,7 +1366,10 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         const uint32_t v1 = pr.v1, p_idx = pr.p_idx;
         const float sx = pr.sx, sy = pr.sy, apx = pr.apx, apy = pr.apy;
         const Ray pray = pr.ray;
-        float4 *const rec0 = B.view_rec, *const rec1 = B.view_rec + (size_t) G * n,
+        /* rec0 = two float2 planes, [G][n] positions then [G][n] (weight, flags): each
+         * half is written whole by one wave (512 contiguous bytes), never as a partial line */
+        float2 *const rec0 = reinterpret_cast<float2 *>(B.view_rec);
+        float4 *const rec1 = B.view_rec + (size_t) G * n,
                       *const rec2 = B.view_rec + (size_t) 2 * G * n;
         /* view index of slot k and its film position (quilt offset for k >= 1) */
         auto view_of = [&](int k) -> uint32_t { return group_view<G>(p_idx, k); };
@@ -1367,11 +1382,11 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 x += (float) (xx * P.sres_x);
                 y += (float) (yy * P.sres_y);
             }
-            reinterpret_cast<float2 *>(&rec0[(size_t) k * n + slot])[0] = make_float2(x, y);
+            rec0[(size_t) k * n + slot] = make_float2(x, y);
         };
         auto put_wf = [&](int k, float w, uint32_t vflags) {
             const uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
-            reinterpret_cast<float2 *>(&rec0[(size_t) k * n + slot])[1] = make_float2(w, bitsf(vf));
+            rec0[(size_t) (G + k) * n + slot] = make_float2(w, bitsf(vf));
         };
         uint32_t vflags = 0;   /* bit k: valid, bit 16 + k: indirect */
         float w0 = 1.f;        /* slot 0's splat weight */
@@ -1680,7 +1695,11 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
     for (int k = 0; k < G; ++k) {
         size_t o = (size_t) k * n + slot;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) a = B.view_rec[o];
+        if (ok) {
+            const float2 *const r0 = reinterpret_cast<const float2 *>(B.view_rec);
+            const float2 pos = r0[o], wf = r0[(size_t) G * n + o];
+            a = make_float4(pos.x, pos.y, wf.x, wf.y);
+        }
         uint32_t vf = fbits(a.w);
         bool valid = ok && (vf & VF_VALID) != 0;
         float weight = a.z;
@@ -1895,11 +1914,17 @@ static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs
 typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
                            const Bufs &, bool, bool, bool, KTimer &);
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
+/* group sizes 2..16: the per-view bit masks (k_prim_req's request bits below the view index at
+ * bit 16, k_mv_primary's valid / indirect flags at bits k and 16 + k) hold 16 views */
 static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
-                                      launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>};
+                                      launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>,
+                                      launch_primary<9>, launch_primary<10>, launch_primary<11>, launch_primary<12>,
+                                      launch_primary<13>, launch_primary<14>, launch_primary<15>, launch_primary<16>};
 static const splat_fn kSplat[] = {nullptr, nullptr, launch_splat<2>, launch_splat<3>, launch_splat<4>,
-                                  launch_splat<5>, launch_splat<6>, launch_splat<7>, launch_splat<8>};
-constexpr uint32_t kMaxG = 8;
+                                  launch_splat<5>, launch_splat<6>, launch_splat<7>, launch_splat<8>,
+                                  launch_splat<9>, launch_splat<10>, launch_splat<11>, launch_splat<12>,
+                                  launch_splat<13>, launch_splat<14>, launch_splat<15>, launch_splat<16>};
+constexpr uint32_t kMaxG = 16;
 constexpr uint64_t kSelectChunk = 1ull << 30;
 
 amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
@@ -1915,7 +1940,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool is_mv = Pp.integrator == AMVPT_INTEGRATOR_MVPATH;
     const bool reuse = is_mv && Pp.sa_reuse && Pp.n_views > 1 && Pp.reuse_count != 1;
     const uint32_t G = reuse ? group_size(Pp) : 1;
-    if (G > kMaxG) { set_error("amvpt_render: group size > 8 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+    if (G > kMaxG) { set_error("amvpt_render: group size > 16 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
     if (!is_mv && n_passes > 1) { set_error("path: more than 2^32 lanes per frame"); return AMVPT_ERR_UNSUPPORTED; }
     if (Pp.multisensor && (Pp.grid_x == 0 || Pp.grid_y == 0 || Pp.film_width % Pp.grid_x || Pp.film_height % Pp.grid_y)) {

@@ -297,3 +297,13 @@ def test_many_chunks_per_pass(gpu_ready, amvpt_mod, oracle, chunk):
         _check(amvpt_mod, oracle, s)
     finally:
         amvpt_mod.set_chunk_lanes(1 << 23)
+
+
+@pytest.mark.parametrize("gx,gy,reuse", [(4, 4, 16), (4, 3, 12)], ids=["g16", "g12"])
+def test_large_view_groups(gpu_ready, amvpt_mod, oracle, gx, gy, reuse):
+    """Group sizes above 8 (reuse_count = n_views = 12 or 16): camera selection over up to 15
+    other views, G x (G-1) MIS pair terms, G splats per lane."""
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16, gx=gx, gy=gy, reuse=reuse)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert oracle.plan(p)["group"] == reuse
+    _check(amvpt_mod, oracle, s)
