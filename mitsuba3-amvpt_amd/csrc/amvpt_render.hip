@@ -70,6 +70,7 @@ struct KParams {
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
     uint32_t trav_mode;     /* amvpt_set_traversal */
+    uint32_t win_rs;        /* splat window row stride residue mod 32 (0: stride = width) */
     uint32_t adapt_seed;    /* adaptive pass: seed of the forked sampler (base_seed + wavefront) */
     uint32_t pass_seed;     /* adaptive pass: seed_value of the pass whose lanes are refilled */
     uint32_t adapt_base;    /* adaptive pass: index of this range's first entry in the pass's wavefront */
@@ -482,8 +483,16 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
 #ifndef AMVPT_SPLAT_BLOCK
 #define AMVPT_SPLAT_BLOCK 256
 #endif
+/* Row stride of the window: rows of ww cells are laid out rs cells apart with rs % 32 == 16,
+ * so consecutive rows start 32 banks apart for the 64-bit cells (2 * rs mod 64 = 32): lanes
+ * whose reprojected footprints straddle a row boundary stop colliding on banks
+ * (measured: splat 206 -> 187 ms at config M; rs = ww, or % 32 in {1, 8, 17, 24}: 200-207 ms).
+ * The 112-cell width leaves room for the padding (5 blocks per CU either way). */
+#ifndef AMVPT_WIN_RS
+#define AMVPT_WIN_RS 16
+#endif
 #ifndef AMVPT_WIN_W
-#define AMVPT_WIN_W 96
+#define AMVPT_WIN_W 112
 #endif
 constexpr int kWinW = AMVPT_WIN_W, kWinH = AMVPT_WIN_H, kMaxWaves = 16, kMaxFoot = 5;
 constexpr int kSplatSuper = 1024;   /* lanes per splat super-block (see slot_lane) */
@@ -557,9 +566,9 @@ AD void lds_add64(double *p, double v) {
 }
 
 /* The block's window: union of the active footprints, clamped to kWinW x kWinH. */
-struct Win { int bx0, by0, ww, wh; };
+struct Win { int bx0, by0, ww, wh, rs; };   /* rs: LDS row stride (cells) >= ww */
 template <int C>
-AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, int y1) {
+AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, int y1, int win_rs) {
     int lx = act ? cx0 : 0x7fffffff, ly = act ? cy0 : 0x7fffffff;
     int hx = act ? x1 : (int) 0x80000000, hy = act ? y1 : (int) 0x80000000;
     lx = wave_min(lx); ly = wave_min(ly); hx = wave_max(hx); hy = wave_max(hy);
@@ -587,6 +596,13 @@ AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, 
     w.bx0 = bx0; w.by0 = by0;
     w.ww = any ? min(bx1 - bx0, kWinW) : 0;
     w.wh = any ? min(by1 - by0, kWinH) : 0;
+    /* row stride: ww rounded up to rs % 32 == win_rs (2 * rs mod 64 = the bank shift between
+     * rows of a 64-bit cell), when that still fits the buffer */
+    w.rs = w.ww;
+    if (win_rs) {
+        const int r = (w.ww & ~31) + win_rs, r2 = r >= w.ww ? r : r + 32;
+        w.rs = r2 <= kWinW ? r2 : w.ww;
+    }
     return w;
 }
 
@@ -595,17 +611,18 @@ AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, 
 template <int C>
 AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w) {
     __syncthreads();
-    const int plane = w.ww * w.wh;
+    const int plane = w.rs * w.wh;
     const int rowlen = w.ww * C;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
     double *win = L.win;
-    for (int e = threadIdx.x; e < plane * C; e += blockDim.x) {
+    const int n_elems = w.ww * w.wh * C;                    /* touched film floats (rows of ww cells) */
+    for (int e = threadIdx.x; e < n_elems; e += blockDim.x) {
         int cy = (int) ((float) e * inv_rowlen);            /* e < 2^24: off by at most one */
         cy -= (cy * rowlen > e) ? 1 : 0;
         cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
         const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
-        double *src = win + k * plane + cy * w.ww + cx;
+        double *src = win + k * plane + cy * w.rs + cx;
         const double d = *src;
         if (__double_as_longlong(d) != 0ll) {
             *src = 0.0;
@@ -620,13 +637,13 @@ template <int C>
 AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, const Foot &f, const float *wx,
                  const float *wy, const float *vals, bool coalesce, unsigned long long *fallback) {
     const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
-    const int plane = wn.ww * wn.wh;
+    const int plane = wn.rs * wn.wh;
     const bool in_win = cx0 >= wn.bx0 && cy0 >= wn.by0 && f.x0 + f.nx <= wn.bx0 + wn.ww && f.y0 + f.ny <= wn.by0 + wn.wh;
     /* cells per footprint side: uniform over the call (filter radius and method only) */
     const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
     if (in_win && cnt <= kMaxFoot) {
         /* straight-line cnt x cnt cells; clipped cells are masked off (no retry, no branch body) */
-        double *const c0 = L.win + ((f.y0 - wn.by0) * wn.ww + (f.x0 - wn.bx0));
+        double *const c0 = L.win + ((f.y0 - wn.by0) * wn.rs + (f.x0 - wn.bx0));
 #pragma unroll
         for (int ys = 0; ys < kMaxFoot; ++ys) {
             if (ys >= cnt) break;
@@ -636,7 +653,7 @@ AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, c
                 if (xs >= cnt) break;
                 if (rok && xs < f.nx && f.x0 + xs >= 0) {
                     const float w = wx[xs] * wy[ys];
-                    double *const cp = c0 + ys * wn.ww + xs;
+                    double *const cp = c0 + ys * wn.rs + xs;
 #pragma unroll
                     for (int k = 0; k < C; ++k) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
                 }
@@ -684,7 +701,7 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
     if (valid) f = footprint(P, px, py, coalesce);
     const bool act = valid && f.ok;
-    const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny);
+    const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny, (int) P.win_rs);
     if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
@@ -1995,6 +2012,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.inv_h = 1.f / (float) P.H;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = g_traversal;
+    {
+        const char *e = std::getenv("AMVPT_WIN_RS");   /* A/B knob */
+        P.win_rs = e && e[0] ? (uint32_t) std::strtoul(e, nullptr, 0) % 32u : (uint32_t) AMVPT_WIN_RS;
+    }
     P.range_begin = lane_begin;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
 
