@@ -488,6 +488,11 @@ AD void film_put(const KParams &P, float *film, float px, float py, const float 
  * whose reprojected footprints straddle a row boundary stop colliding on banks
  * (measured: splat 206 -> 187 ms at config M; rs = ww, or % 32 in {1, 8, 17, 24}: 200-207 ms).
  * The 112-cell width leaves room for the padding (5 blocks per CU either way). */
+/* measurement-only attribution builds (wrong images): 1 skips the LDS adds, 2 the flush's
+ * film atomics, 4 the filter weights */
+#ifndef AMVPT_ATTR_SKIP
+#define AMVPT_ATTR_SKIP 0
+#endif
 #ifndef AMVPT_WIN_RS
 #define AMVPT_WIN_RS 16
 #endif
@@ -627,7 +632,7 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
         if (__double_as_longlong(d) != 0ll) {
             *src = 0.0;
             const float v = (float) d;
-            if (v != 0.f || v != v) film_add(film0 + (size_t) cy * P.W * C + r, v);
+            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + (size_t) cy * P.W * C + r, v);
         }
     }
 }
@@ -655,7 +660,8 @@ AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, c
                     const float w = wx[xs] * wy[ys];
                     double *const cp = c0 + ys * wn.rs + xs;
 #pragma unroll
-                    for (int k = 0; k < C; ++k) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
+                    for (int k = 0; k < C; ++k)
+                        if (!(AMVPT_ATTR_SKIP & 1)) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
                 }
             }
         }
@@ -682,8 +688,8 @@ AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, c
 AD void foot_weights(const KParams &P, const Foot &f, float *wx, float *wy) {
 #pragma unroll
     for (int t = 0; t < kMaxFoot; ++t) {
-        wx[t] = P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
-        wy[t] = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
+        wx[t] = P.box || (AMVPT_ATTR_SKIP & 4) ? 1.f : gaussian_eval(P.filt, f.rx + (float) t);
+        wy[t] = P.box || (AMVPT_ATTR_SKIP & 4) ? 1.f : gaussian_eval(P.filt, f.ry + (float) t);
     }
 }
 
