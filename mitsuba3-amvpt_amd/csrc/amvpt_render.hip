@@ -32,13 +32,22 @@
 #include "dbsdf.h"
 #include "internal.h"
 
+/* non-template kernels get internal linkage in the k_shadow translation unit (amvpt_shadow.hip) */
+#ifdef AMVPT_SHADOW_TU
+#define AMVPT_TU_LOCAL static
+#else
+#define AMVPT_TU_LOCAL
+#endif
+
 namespace amvpt {
 
+#ifndef AMVPT_SHADOW_TU
 uint64_t g_chunk_lanes = 1ull << 23;
 uint32_t g_traversal = 0;
 bool g_diffuse_spec = true;   /* all-diffuse kernel specialisation (AMVPT_NO_DIFFUSE_SPEC=1 turns it off) */
 amvpt_exchange_fn g_exchange = nullptr;
 void *g_exchange_ctx = nullptr;
+#endif
 
 /* ------------------------------------------------------------------ */
 /* Parameters                                                         */
@@ -864,7 +873,7 @@ AD void lane_pixel(const KParams &P, uint32_t lane, int &px, int &py) {
     px = (int) (pix - P.W * y);
 }
 
-__global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V, Bufs B) {
+AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V, Bufs B) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = slot < P.chunk_n;
     PathState s;
@@ -918,7 +927,7 @@ AD void lane_sample_pos(const KParams &P, uint32_t lane, float &sx, float &sy, f
     if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }   /* nested_gather(aperture_sample) */
 }
 
-__global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V, Bufs B) {
+AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, const DView *V, Bufs B) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     bool ok = slot < P.chunk_n;
     PathState s;
@@ -1758,7 +1767,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
 }
 
 /* develop: rgb / W (hdrfilm.cpp:400) */
-__global__ void k_develop(const float *film, float *out, uint32_t npx, uint32_t alpha) {
+AMVPT_TU_LOCAL __global__ void k_develop(const float *film, float *out, uint32_t npx, uint32_t alpha) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npx) return;
     uint32_t C = alpha ? 5u : 4u, T = alpha ? 4u : 3u;
@@ -1768,6 +1777,25 @@ __global__ void k_develop(const float *film, float *out, uint32_t npx, uint32_t 
     for (uint32_t c = 0; c < T; ++c) out[(size_t) p * T + c] = src[c] / d;
 }
 
+/*
+ * k_shadow launcher.  It is defined in its own translation unit (amvpt_shadow.hip
+ * includes this file with AMVPT_SHADOW_TU), which is compiled WITH the SLP vectorizer:
+ * k_shadow is the one kernel that is faster with it (71 vs 80 ms per config-M frame),
+ * while the rest of this file is built with -fno-slp-vectorize (see Makefile).
+ */
+void launch_shadow(int walk, dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *dS, const Bufs &B)
+#ifdef AMVPT_SHADOW_TU
+{
+    if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, dS, B);
+    else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE>), grid, dim3(256), lds, st, P, dS, B);
+    else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_UNI>), grid, dim3(256), lds, st, P, dS, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE>), grid, dim3(256), lds, st, P, dS, B);
+}
+#else
+;
+#endif
+
+#ifndef AMVPT_SHADOW_TU
 /* ------------------------------------------------------------------ */
 /* Host orchestration                                                 */
 /* ------------------------------------------------------------------ */
@@ -2175,10 +2203,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false, false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
             T.end(st);
             T.begin(AMVPT_K_SHADOW, st);
-            if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            launch_shadow(walk, dim3(bgrid), lds_ext, st, P, dS, B);
             T.end(st);
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);
@@ -2325,4 +2350,5 @@ amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h,
     return AMVPT_OK;
 }
 
+#endif /* AMVPT_SHADOW_TU */
 } // namespace amvpt
