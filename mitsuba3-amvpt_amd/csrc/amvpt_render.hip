@@ -244,7 +244,7 @@ AD bool sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, fl
     const DShape &s = sc.g->shapes[em.shape];
     ds = shape_sample_direction(s, ref.p, u1, u2);
     bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
-    spec = a ? c3(em.radiance) / ds.pdf : c3(0.f);
+    spec = csel(a, c3(em.radiance) / ds.pdf, c3(0.f));
     ds.emitter = (int32_t) index;
     ds.pdf *= sc.g->emitter_pmf;
     spec = spec * weight;
@@ -1138,7 +1138,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
         float sx = (float) px + jx, sy = (float) py + jy;
         float4 lo = B.lane_out[slot];
         bool valid = lo.w != 0.f;
-        C3 spec = valid ? C3{lo.x, lo.y, lo.z} : c3(0.f);
+        C3 spec = csel(valid, C3{lo.x, lo.y, lo.z}, c3(0.f));
         float alpha = valid ? 1.f : 0.f;
         pack_vals(P, spec, alpha, 1.f, vals);
         putx = P.path_box_pos ? (float) px : sx;
@@ -1435,7 +1435,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             bool p_hit = si.valid();
             int32_t em = si_emitter(sc, si);
             bool direct_em = em >= 0;
-            C3 emitted = direct_em ? emitter_eval(sc, em, si, true) : c3(0.f);
+            C3 emitted = c3(0.f);
+            if (direct_em) emitted = emitter_eval(sc, em, si, true);
             int32_t b = p_hit ? S.shapes[si.shape].bsdf : -1;
             bool bsdf_smooth = (bsdf_flags(S.bsdfs, b) & BF_Smooth) != 0;
             bool active_em = p_hit && bsdf_smooth;
@@ -1587,7 +1588,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     const float wk = pdf_lk / pdfSum;
                     const size_t o = (size_t) k * n + slot;
                     /* result: emission (slot 0) + direct light through this view's BSDF value */
-                    C3 res = k == 0 ? emitted : c3(0.f);
+                    C3 res = csel(k == 0, emitted, c3(0.f));
                     if (active_em && vk) {
                         C3 bvk = bsdf_val;
                         if (k > 0) {   /* the value camera_selection evaluated for view k */
@@ -1602,14 +1603,14 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     float bp;
                     bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, bsmp.wo, valid, bv, bp);
                     if (k == 0) {
-                        bv = p_not_delta ? bv : bsdf_weight;
+                        bv = csel(p_not_delta, bv, bsdf_weight);
                         bp = p_not_delta ? bp : bsmp.pdf;
                         valid = valid && (bp > 0.f || delta);
                     }
                     bool pvalid = bp > 0.f;
                     valid = valid && ((k == 0) ? (pvalid || delta) : pvalid);
                     bp = valid ? bp : 0.f;
-                    bv = valid ? bv : c3(0.f);
+                    bv = csel(valid, bv, c3(0.f));
                     rec2[o] = make_float4(bv.r, bv.g, bv.b, 0.f);
                     pdf += bp;
                     n_ind += (float) valid;
@@ -1639,7 +1640,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             }
             /* ---- BSDF sampling continuation ---- */
             Ray pd_ray = spawn_ray(si.p, si.n, si.sh.to_world(bsmp.wo));
-            C3 thr = should_mis ? c3(1.f) : bsdf_weight;
+            C3 thr = csel(should_mis, c3(1.f), bsdf_weight);
             valid_ray = valid_ray || (p_hit && !flag_null);
             bool pd_active = p_hit;
             if (!should_mis) pd_active = pd_active && (cmax(thr) != 0.f);
@@ -1680,7 +1681,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             for (int k = 0; k < G; ++k) {
                 const size_t o = (size_t) k * n + slot;
                 if (k > 0) put_wf(k, P.max_depth != 0 ? 1.f : 0.f, vflags);
-                C3 res = k == 0 ? result0 : c3(0.f);
+                C3 res = csel(k == 0, result0, c3(0.f));
                 rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
                 rec2[o] = make_float4(0.f, 0.f, 0.f, 0.f);
             }

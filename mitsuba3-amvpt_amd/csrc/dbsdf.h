@@ -37,7 +37,9 @@ AD C3 operator+(C3 a, C3 b) { return {a.r + b.r, a.g + b.g, a.b + b.b}; }
 AD C3 operator/(C3 a, float s) { return {a.r / s, a.g / s, a.b / s}; }
 AD C3 cfma(C3 a, C3 b, C3 c) { return {fmadd(a.r, b.r, c.r), fmadd(a.g, b.g, c.g), fmadd(a.b, b.b, c.b)}; }
 AD float cmax(C3 a) { return vmax(vmax(a.r, a.g), a.b); }
-AD C3 csel(bool m, C3 a, C3 b) { return m ? a : b; }
+/* component-wise select: a ternary on the structs makes clang select between two stack
+ * temporaries' addresses, which SROA cannot always undo (scratch loads in k_mv_primary) */
+AD C3 csel(bool m, C3 a, C3 b) { return {m ? a.r : b.r, m ? a.g : b.g, m ? a.b : b.b}; }
 
 struct BSample { f3 wo; float pdf, eta; uint32_t type; };
 AD BSample bs_zero() { return BSample{mk(0.f, 0.f, 0.f), 0.f, 0.f, 0u}; }
@@ -114,7 +116,7 @@ AD void diffuse_eval_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo, C3 &val, fl
     bool a = wi.z > 0.f && wo.z > 0.f;
     C3 v = c3(d.refl) * kInvPi * wo.z;
     float p = kInvPi * wo.z;
-    val = a ? v : c3(0.f);
+    val = csel(a, v, c3(0.f));
     pdf = a ? p : 0.f;
 }
 AD float diffuse_pdf(uint32_t ctx, f3 wi, f3 wo) {
@@ -129,7 +131,7 @@ AD void diffuse_sample(const DBsdf &d, uint32_t ctx, f3 wi, float u1, float u2, 
     bs.pdf = kInvPi * bs.wo.z;
     bs.eta = 1.f;
     bs.type = BF_DiffuseReflection;
-    w = (a && bs.pdf > 0.f) ? c3(d.refl) : c3(0.f);
+    w = csel(a && bs.pdf > 0.f, c3(d.refl), c3(0.f));
 }
 
 AD void leaf_eval_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo, C3 &val, float &pdf) {
@@ -146,7 +148,7 @@ AD void leaf_eval_pdf(const DBsdf &d, uint32_t ctx, f3 wi, f3 wo, C3 &val, float
     C3 F = fresnel3(d, dot(wi, H));
     C3 v = d.has_spec ? F * (value * c3(d.spec)) : F * value;
     float p = mf.visible ? D * g1 / (4.f * wi.z) : mf.eval(H) * H.z / (4.f * dot(wo, H));
-    val = a ? v : c3(0.f);
+    val = csel(a, v, c3(0.f));
     pdf = a ? p : 0.f;
 }
 
@@ -176,8 +178,8 @@ AD void leaf_sample(const DBsdf &d, uint32_t ctx, f3 wi, float u1, float u2, BSa
                               : mf.smith_g1(wi, m) * mf.smith_g1(bs.wo, m) * dot(wi, m) / (wi.z * m.z);
     bs.pdf /= 4.f * dot(bs.wo, m);
     C3 F = fresnel3(d, dot(wi, m));
-    C3 ww = d.has_spec ? c3(weight) * c3(d.spec) : c3(weight);
-    w = a ? F * ww : c3(0.f);
+    C3 ww = csel(d.has_spec, c3(weight) * c3(d.spec), c3(weight));
+    w = csel(a, F * ww, c3(0.f));
 }
 
 /* ---------------- dispatch incl. twosided ---------------- */
