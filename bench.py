@@ -6,11 +6,16 @@ sa_reuse + sa_mis, reuse_count 8, max_depth 8, rr_depth 5, seed 0.
 One step = one full frame of that workload on every rank (scene upload, film
 allocation and plan are outside the timed region; inputs are resident in HBM).
 
-Multi-GPU (one process per GPU, RCCL over xGMI): weak scaling by pass sharding.
-Rank r renders passes [4r, 4r+4) of a (64*N)-spp frame -- the reference's own
-pass seeding (seed = spp_per_pass * pass + seed, mvpath.cpp:227), so the node
-produces exactly the single-GPU (64*N)-spp image -- and the RGBW ImageBlocks
-are summed on rank 0 with one RCCL reduce inside the timed region.
+Multi-GPU (one process per GPU, RCCL over xGMI): strong scaling by lane sharding
+(SURVEY 8(e)).  Every rank renders the contiguous lane range lane_shard(L, r, N) of
+every pass of the SAME 64-spp frame (a band of quilt rows; lanes keep their global
+TEA seeds, so the image is the single-GPU one), and the RGBW ImageBlocks are summed
+on rank 0 with one RCCL reduce inside the timed region.  `--weak` instead renders
+passes [4r, 4r+4) of a (64*N)-spp frame (pass sharding; labelled "weak").
+
+After the timed region rank 0 also reports `rmse_vs_oracle`: the per-pixel RMSE of
+the developed film of a stated lane window of the same workload, HIP pipeline vs the
+CPU oracle (oracle/, a restatement of mvpath; Dr.Jit llvm_rgb cannot be built here).
 
 The JSON line carries the dominant kernel's roofline (HIP-event timing of the
 kernel inside the timed region x its algorithmic bytes, DESIGN.md "Byte model")
@@ -34,12 +39,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CHUNK_LANES = 1 << 23  # amvpt_render's default lane chunk (g_chunk_lanes)
 
 
-# SURVEY 8 config table.  M = the metric's workload (bench line); C5 = the 32-view adaptive
-# scale configuration (grid 8x4 of 2048^2 views, groups of 4, one 16-spp pass, adaptive 3),
-# lane-sharded so that every GPU count renders the same frame.
+# SURVEY 8 config table.  M = the metric's workload (the default bench line); the others are
+# reported on request (--config): C2 (4-view Cornell 512^2), C3 (Veach-MIS 8-view 1024^2 256 spp:
+# glossy MIS, sphere lights; C4 = C3 lane-sharded over the node), C5 (the 32-view adaptive array:
+# grid 8x4 of 2048^2 views, groups of 4, one 16-spp pass, adaptive 3) and `mesh` (config M's shape
+# on the OBJ/PLY Cornell box: 3.6 k triangles, per-lane BVH walks).  All lane-sharded (strong).
 CONFIGS = {
-    "M": dict(res=1024, spp=64, gx=4, gy=2, reuse=8, adaptive=0, sharding="pass"),
-    "C5": dict(res=2048, spp=16, gx=8, gy=4, reuse=4, adaptive=3, sharding="lane"),
+    "M": dict(scene="cbox_grid.xml", res=1024, spp=64, gx=4, gy=2, reuse=8, adaptive=0),
+    "C2": dict(scene="cbox_grid.xml", res=512, spp=64, gx=2, gy=2, reuse=4, adaptive=0),
+    "C3": dict(scene="veach_grid.xml", res=1024, spp=256, gx=4, gy=2, reuse=8, adaptive=0),
+    "C5": dict(scene="cbox_grid.xml", res=2048, spp=16, gx=8, gy=4, reuse=4, adaptive=3),
+    "mesh": dict(scene="cbox_mesh.xml", res=1024, spp=64, gx=4, gy=2, reuse=8, adaptive=0),
 }
 
 
@@ -62,7 +72,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="M",
-                    help="M: the metric's workload (default); C5: 32-view 2048^2 adaptive, lane-sharded")
+                    help="M: the metric's workload (default); C2, C3, C5, mesh: the other configs")
+    ap.add_argument("--weak", action="store_true",
+                    help="pass sharding: rank r renders its own passes of an (N x spp)-spp frame (weak scaling)")
+    ap.add_argument("--rmse-lanes", type=int, default=1 << 20,
+                    help="lanes of the RMSE window (0: skip); the window starts at quilt row H/4")
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--gx", type=int, default=None)
@@ -77,7 +91,8 @@ def main():
         if getattr(args, k) is not None:
             cfg[k] = getattr(args, k)
     headline = cfg == CONFIGS["M"]   # PMC traffic in profiles/ was collected on exactly this workload
-    lane_sharded = cfg.pop("sharding") == "lane"
+    scene_file = cfg.pop("scene")
+    lane_sharded = not args.weak
 
     import torch
     import torch.distributed as dist
@@ -94,7 +109,7 @@ def main():
     hip = amvpt.hip_lib()
     hip.amvpt_set_device(local)
 
-    scene = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), **cfg)
+    scene = amvpt.load_file(os.path.join(REPO, "scenes", scene_file), **cfg)
     sd, vd, p = scene.describe(0, 0, 0)
     plan = amvpt.plan(p)
     spp, spp_pp, n_passes, lanes_per_pass = plan
@@ -172,6 +187,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not p.adaptive:
         cpu = cpu_baseline(sd, vd, p, args.cpu_seconds)
+    rmse = None
+    if rank == 0 and args.rmse_lanes > 0 and not p.adaptive:
+        rmse = rmse_window(dev, sd, vd, p, plan, args.rmse_lanes, stream)
 
     if rank == 0:
         out = {
@@ -184,15 +202,17 @@ def main():
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "strong" if lane_sharded else "weak",
+            "rmse_vs_oracle": rmse,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (Cornell box of util.py:551-685 on a %dx%d grid sensor; no external assets)"
                     % (p.grid_x, p.grid_y),
             "config": {
-                "workload": "%s: %d-view %dx%d per view (quilt %dx%d), %d spp%s (%d passes x %d), G=%d, sa_mis, "
+                "workload": "%s: %s, %d-view %dx%d per view (quilt %dx%d), %d spp%s (%d passes x %d), G=%d, sa_mis, "
                             "adaptive %d, max_depth 8, rr_depth 5, seed 0"
-                            % (args.config, p.n_views, cfg["res"], cfg["res"], p.film_width, p.film_height, spp,
-                               "" if lane_sharded else "/GPU", n_passes, spp_pp, G, p.adaptive),
+                            % (args.config, scene_file, p.n_views, cfg["res"], cfg["res"], p.film_width,
+                               p.film_height, spp, "" if lane_sharded else "/GPU", n_passes, spp_pp, G,
+                               p.adaptive),
                 "samples_per_gpu_per_step": samples_per_rank,
                 "adaptive_lanes_per_gpu_per_step": c["adaptive_lanes"],
                 "parallelism": ("lane-sharded x%d (+ one count all-gather per pass) + RCCL reduce of the RGBW "
@@ -226,7 +246,39 @@ def main():
         }
         print(json.dumps(out))
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def rmse_window(dev, sd, vd, p, plan, n, stream):
+    """Per-pixel RMSE (linear RGB, developed) of lanes [b, b + n) of every pass of the workload,
+    HIP pipeline vs the CPU oracle.  The window starts at quilt row H/4 (through the cubes of the
+    top row of views); every pixel that either film touched (W > 0) is compared -- the window's
+    splats bleed into neighbouring rows and its reprojections into the other views."""
+    import torch
+    from amvpt import compare
+    from oracle import oracle as O
+    spp, spp_pp, n_passes, lanes_per_pass = plan
+    W, H = p.film_width, p.film_height
+    row = W * spp_pp                       # lanes per quilt row and pass
+    b = min(lanes_per_pass, (H // 4) * row)
+    e = min(lanes_per_pass, b + n)
+    C = 5 if p.film_alpha else 4
+    film = torch.zeros((H, W, C), dtype=torch.float32, device="cuda")
+    dev.render(vd, p, film.data_ptr(), b, e, stream)
+    torch.cuda.synchronize()
+    g = film.cpu().numpy()
+    del film
+    threads = max(1, min(16, os.cpu_count() or 1))
+    O.build()
+    o, _, st = O.render(sd, vd, p, lane_begin=b, lane_end=e, threads=threads)
+    touched = (g[..., -1] != 0) | (o[..., -1] != 0)
+    m = compare.metrics(O.develop(g)[touched], O.develop(o)[touched])
+    return {"rmse": m["rmse"], "max_abs": m["max_abs"], "pixels": int(touched.sum()),
+            "window": "lanes [%d, %d) of each of the %d passes (quilt rows %d..%d)" % (
+                b, e, n_passes, b // row, (e - 1) // row),
+            "reference": "CPU oracle (restatement of mvpath, not Dr.Jit llvm_rgb)",
+            "oracle_seconds": round(st["seconds"], 2)}
 
 
 def kernel_bytes(c, G, C):

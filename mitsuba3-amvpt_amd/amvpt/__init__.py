@@ -345,11 +345,14 @@ class DeviceScene:
 
     def render(self, views_ptr, params, film_ptr, lane_begin=0, lane_end=2 ** 64 - 1, stream=None,
                counters=None):
-        cnt = counters if counters is not None else Counters()
+        """amvpt_render over lanes [lane_begin, lane_end).  Without `counters` the render is not
+        instrumented (no per-kernel event timing, no host synchronisation); with an amvpt.Counters
+        it is filled (per-kernel HIP-event times, lane statistics) and returned."""
         _check(self._lib.amvpt_render(self.h, views_ptr, ctypes.byref(params), lane_begin, lane_end,
-                                      ctypes.c_void_p(film_ptr), ctypes.c_void_p(stream), ctypes.byref(cnt)),
+                                      ctypes.c_void_p(film_ptr), ctypes.c_void_p(stream),
+                                      ctypes.byref(counters) if counters is not None else None),
                self._lib)
-        return cnt
+        return counters
 
     def render_records(self, views_ptr, params, film_ptr, records_ptr, pass_index=0, lane_begin=0,
                        lane_end=2 ** 64 - 1, stream=None):

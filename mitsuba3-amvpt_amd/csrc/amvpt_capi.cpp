@@ -255,13 +255,14 @@ amvpt_status amvpt_plan(const amvpt_params *P, uint32_t *spp, uint32_t *spp_pp, 
     return AMVPT_OK;
 }
 
-amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
-    if (!d || !out) { set_error("amvpt_scene_create: null argument"); return AMVPT_ERR_INVALID; }
-    *out = nullptr;
-    if (!device_ok()) { set_error("amvpt_scene_create: no HIP device visible (the product path has no CPU fallback)"); return AMVPT_ERR_NO_DEVICE; }
+/* Descriptor checks of amvpt_scene_create (run before any device work, so malformed
+ * input fails with AMVPT_ERR_INVALID even on a host without a GPU). */
+static amvpt_status validate_scene(const amvpt_scene_desc *d) {
+    if ((d->shape_count && !d->shapes) || (d->bsdf_count && !d->bsdfs) || (d->emitter_count && !d->emitters)) {
+        set_error("amvpt_scene_create: null table with a non-zero count");
+        return AMVPT_ERR_INVALID;
+    }
     if (d->has_environment) { set_error("environment emitters are outside the implemented path"); return AMVPT_ERR_UNSUPPORTED; }
-    bool has_spheres = false;
-    /* validate */
     for (uint32_t i = 0; i < d->bsdf_count; ++i) {
         const amvpt_bsdf_desc &b = d->bsdfs[i];
         if (b.type == AMVPT_BSDF_ROUGHCONDUCTOR &&
@@ -289,6 +290,46 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         if (e.sampling_weight != 1.f) { set_error("non-uniform emitter sampling weights are not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     }
 
+    for (uint32_t i = 0; i < d->shape_count; ++i) {
+        const amvpt_shape_desc &s = d->shapes[i];
+        if (s.bsdf < 0 || (uint32_t) s.bsdf >= d->bsdf_count) { set_error("shape without a valid BSDF"); return AMVPT_ERR_INVALID; }
+        if (s.emitter < -1 || (s.emitter >= 0 && (uint32_t) s.emitter >= d->emitter_count)) {
+            set_error("shape.emitter outside [-1, emitter_count)");
+            return AMVPT_ERR_INVALID;
+        }
+        /* the area emitter and its shape must point at each other (Shape::set_emitter) */
+        if (s.emitter >= 0 && d->emitters[s.emitter].shape != (int32_t) i) {
+            set_error("shape.emitter and emitter.shape disagree");
+            return AMVPT_ERR_INVALID;
+        }
+        if (s.type == AMVPT_SHAPE_MESH) {
+            if (!s.positions || !s.faces) { set_error("mesh without positions/faces"); return AMVPT_ERR_INVALID; }
+            for (size_t f = 0; f < 3 * (size_t) s.face_count; ++f)
+                if (s.faces[f] >= s.vertex_count) { set_error("mesh face index >= vertex_count"); return AMVPT_ERR_INVALID; }
+        } else if (s.type != AMVPT_SHAPE_RECTANGLE && s.type != AMVPT_SHAPE_SPHERE) {
+            set_error("unknown shape type");
+            return AMVPT_ERR_INVALID;
+        }
+    }
+    for (uint32_t i = 0; i < d->emitter_count; ++i)
+        if (d->shapes[d->emitters[i].shape].emitter != (int32_t) i) {
+            set_error("shape.emitter and emitter.shape disagree");
+            return AMVPT_ERR_INVALID;
+        }
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
+    if (!d || !out) { set_error("amvpt_scene_create: null argument"); return AMVPT_ERR_INVALID; }
+    *out = nullptr;
+    /* validate the whole descriptor first (also without a device): every index the host
+     * tables or the kernels follow must be in range */
+    {
+        const amvpt_status vs = validate_scene(d);
+        if (vs != AMVPT_OK) return vs;
+    }
+    if (!device_ok()) { set_error("amvpt_scene_create: no HIP device visible (the product path has no CPU fallback)"); return AMVPT_ERR_NO_DEVICE; }
+    bool has_spheres = false;
     std::vector<DShape> shapes(d->shape_count);
     std::vector<float> vpos, vnrm, vuv;
     std::vector<uint32_t> faces;

@@ -28,6 +28,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 
 #include "dbsdf.h"
 #include "internal.h"
@@ -1865,12 +1868,46 @@ static void gaussian_coeffs(float stddev, FilterCoeffs &f) {
         if (e_ != hipSuccess) return hip_fail(#x, (int) e_);         \
     } while (0)
 
-struct Arena {
-    void *base = nullptr;
-    size_t bytes = 0;
-    int device = -1;
+/*
+ * Device buffers of amvpt_render, one set per device.  A render holds its device's
+ * lock while it enqueues (calls from several host threads on one device serialise;
+ * threads driving different devices run concurrently), and records `done` on its
+ * stream when it returns: the next render waits on that event before it touches the
+ * buffers (hipStreamWaitEvent when it runs on another stream), and a buffer is only
+ * freed for a larger one after the event completed.
+ */
+struct DevArena {
+    std::mutex mu;
+    void *base = nullptr, *adapt = nullptr;
+    size_t bytes = 0, abytes = 0;
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    bool pending = false;
 };
-static Arena g_arena;
+static std::mutex g_arenas_mu;
+static std::map<int, std::unique_ptr<DevArena>> g_arenas;
+static DevArena &dev_arena(int dev) {
+    std::lock_guard<std::mutex> g(g_arenas_mu);
+    std::unique_ptr<DevArena> &a = g_arenas[dev];
+    if (!a) a.reset(new DevArena());
+    return *a;
+}
+/* (re)allocate one of the arena's buffers; the previous contents may still be in use */
+static amvpt_status arena_reserve(DevArena &A, void *&buf, size_t &have, size_t need, const char *what) {
+    if (have >= need) return AMVPT_OK;
+    if (buf) {
+        if (A.pending) HIPCHK(hipEventSynchronize(A.done));
+        (void) hipFree(buf);
+    }
+    buf = nullptr;
+    have = 0;
+    if (hipMalloc(&buf, need) != hipSuccess) {
+        set_error(std::string("amvpt_render: device allocation of the ") + what + " failed");
+        return AMVPT_ERR_OOM;
+    }
+    have = need;
+    return AMVPT_OK;
+}
 
 /* Per-kernel HIP-event timing of an instrumented render (amvpt_counters given): an
  * event pair around every launch on the render stream, resolved in batches. */
@@ -1985,7 +2022,17 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     if (!scene || !views || !params || !film) { set_error("amvpt_render: null argument"); return AMVPT_ERR_INVALID; }
     const amvpt_params &Pp = *params;
     hipStream_t st = (hipStream_t) stream;
-    { const char *e = std::getenv("AMVPT_NO_DIFFUSE_SPEC"); g_diffuse_spec = !(e && e[0] == '1'); }
+    bool diffuse_spec = g_diffuse_spec;
+    { const char *e = std::getenv("AMVPT_NO_DIFFUSE_SPEC"); if (e && e[0] == '1') diffuse_spec = false; }
+    if (Pp.n_views == 0) { set_error("amvpt_render: n_views == 0"); return AMVPT_ERR_INVALID; }
+    if (Pp.multisensor && !Pp.batch && Pp.n_views != Pp.grid_x * Pp.grid_y) {
+        set_error("amvpt_render: a grid MultiSensor needs n_views == grid_x * grid_y");
+        return AMVPT_ERR_INVALID;
+    }
+    if (Pp.multisensor && Pp.batch && (Pp.grid_y != 1 || Pp.grid_x != Pp.n_views)) {
+        set_error("amvpt_render: a batch MultiSensor needs grid_x == n_views and grid_y == 1");
+        return AMVPT_ERR_INVALID;
+    }
     uint32_t spp, spp_pp, n_passes;
     uint64_t L;
     plan(Pp, spp, spp_pp, n_passes, L);
@@ -2005,10 +2052,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             return AMVPT_ERR_INVALID;
         }
     if (lane_end > L) lane_end = L;
-    if (lane_begin >= lane_end) {
-        if (counters) *counters = amvpt_counters{};
-        return AMVPT_OK;
-    }
     /* the adaptive fill compacts the whole pass (its RNG seeds depend on the global
      * wavefront): a lane range needs the host's count exchange (amvpt_set_adaptive_exchange) */
     const bool do_fill = n_adapt && !Pp.debug;
@@ -2019,6 +2062,20 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         set_error("amvpt_render: adaptive > 0 over a lane range needs amvpt_set_adaptive_exchange "
                   "(or the whole frame: lane_begin = 0, lane_end = all lanes)");
         return AMVPT_ERR_UNSUPPORTED;
+    }
+    if (lane_begin >= lane_end) {
+        /* an empty range still takes part in every pass's count exchange (an all-gather on
+         * the host side: the other ranks would wait for it forever) */
+        if (do_fill && partial)
+            for (uint32_t pass = 0; pass < n_passes; ++pass) {
+                uint64_t prefix = 0, total = 0;
+                if (exchange(exchange_ctx, 0, &prefix, &total) != 0) {
+                    set_error("amvpt_render: adaptive count exchange failed");
+                    return AMVPT_ERR_INVALID;
+                }
+            }
+        if (counters) *counters = amvpt_counters{};
+        return AMVPT_OK;
     }
 
     KParams P{};
@@ -2085,18 +2142,18 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t need = views_bytes + stats_bytes + cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
-    if (g_arena.bytes < need || g_arena.device != dev) {
-        if (g_arena.base) (void) hipFree(g_arena.base);
-        g_arena.base = nullptr;
-        g_arena.bytes = 0;
-        if (hipMalloc(&g_arena.base, need) != hipSuccess) {
-            set_error("amvpt_render: device allocation of the lane arena failed");
-            return AMVPT_ERR_OOM;
-        }
-        g_arena.bytes = need;
-        g_arena.device = dev;
-    }
-    char *base = (char *) g_arena.base;
+    DevArena &A = dev_arena(dev);
+    std::unique_lock<std::mutex> arena_lock(A.mu);
+    if (!A.done) HIPCHK(hipEventCreateWithFlags(&A.done, hipEventDisableTiming));
+    /* the previous render's buffers may still be in flight on another stream */
+    if (A.pending && A.last != st) HIPCHK(hipStreamWaitEvent(st, A.done, 0));
+    /* every return below records `done` on this stream (also the error paths) */
+    struct ArenaRelease {
+        DevArena &A; hipStream_t st;
+        ~ArenaRelease() { if (hipEventRecord(A.done, st) == hipSuccess) { A.pending = true; A.last = st; } }
+    } arena_release{A, st};
+    { const amvpt_status as_ = arena_reserve(A, A.base, A.bytes, need, "lane arena"); if (as_ != AMVPT_OK) return as_; }
+    char *base = (char *) A.base;
     DView *dviews = (DView *) base;
     unsigned long long *dstats = (unsigned long long *) (base + views_bytes);
     uint32_t *dcnt = (uint32_t *) (base + views_bytes + stats_bytes);   /* [3][kQParts * kCntStride] */
@@ -2107,7 +2164,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     HIPCHK(hipMemsetAsync(dstats, 0, stats_bytes, st));
 
     /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
-    static struct AdaptArena { void *base = nullptr; size_t bytes = 0; int device = -1; } g_adapt;
     uint8_t *d_amask = nullptr;
     uint32_t *d_asel = nullptr, *d_anum = nullptr;
     void *d_cub = nullptr;
@@ -2120,18 +2176,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                                              (int) sel_max, st));
         const size_t abytes = ((span_all + 255) & ~(uint64_t) 255) + 4 * ((span_all + 63) & ~(uint64_t) 63) + 256 +
                               cub_bytes + 256;
-        if (g_adapt.bytes < abytes || g_adapt.device != dev) {
-            if (g_adapt.base) (void) hipFree(g_adapt.base);
-            g_adapt.base = nullptr;
-            g_adapt.bytes = 0;
-            if (hipMalloc(&g_adapt.base, abytes) != hipSuccess) {
-                set_error("amvpt_render: device allocation of the adaptive buffers failed");
-                return AMVPT_ERR_OOM;
-            }
-            g_adapt.bytes = abytes;
-            g_adapt.device = dev;
-        }
-        char *ap = (char *) g_adapt.base;
+        { const amvpt_status as_ = arena_reserve(A, A.adapt, A.abytes, abytes, "adaptive buffers"); if (as_ != AMVPT_OK) return as_; }
+        char *ap = (char *) A.adapt;
         d_amask = (uint8_t *) ap; ap += (span_all + 255) & ~(uint64_t) 255;
         d_asel = (uint32_t *) ap; ap += 4 * ((span_all + 63) & ~(uint64_t) 63);
         d_anum = (uint32_t *) ap; ap += 256;
@@ -2167,7 +2213,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         const bool brute_on = !(e && e[0] == '0');
         if (uni && g_traversal == 0u && brute_on && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
     }
-    const bool diff = scene->all_diffuse && g_diffuse_spec;                                        /* kDiff instances */
+    const bool diff = scene->all_diffuse && diffuse_spec;                                          /* kDiff instances */
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */

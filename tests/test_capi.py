@@ -83,3 +83,65 @@ def test_product_modules_never_import_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
                 txt = open(os.path.join(root, f), errors="ignore").read()
                 assert not bad.search(txt), os.path.join(root, f)
+
+
+def _cbox_desc(amvpt_mod):
+    from conftest import SCENES
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=8, spp=4)
+    sd, vd, p = s.describe(0, 0, 0)
+    return s, sd, vd, p
+
+
+def _copy_scene(amvpt_mod, sd):
+    """Deep-enough copy of a SceneDesc whose tables can be edited."""
+    d = sd.contents
+    shapes = (amvpt_mod.ShapeDesc * d.shape_count)(*[d.shapes[i] for i in range(d.shape_count)])
+    bsdfs = (amvpt_mod.BsdfDesc * d.bsdf_count)(*[d.bsdfs[i] for i in range(d.bsdf_count)])
+    ems = (amvpt_mod.EmitterDesc * d.emitter_count)(*[d.emitters[i] for i in range(d.emitter_count)])
+    nd = amvpt_mod.SceneDesc(ctypes.cast(shapes, ctypes.POINTER(amvpt_mod.ShapeDesc)), d.shape_count,
+                             ctypes.cast(bsdfs, ctypes.POINTER(amvpt_mod.BsdfDesc)), d.bsdf_count,
+                             ctypes.cast(ems, ctypes.POINTER(amvpt_mod.EmitterDesc)), d.emitter_count, 0)
+    return nd, shapes, bsdfs, ems
+
+
+@pytest.mark.parametrize("breakage", ["emitter_range", "emitter_pair", "face_index", "bsdf_range"])
+def test_scene_create_rejects_malformed_descriptors(amvpt_mod, breakage):
+    """Malformed C-ABI input is refused with AMVPT_ERR_INVALID before any device work:
+    shape.emitter outside [-1, emitter_count), emitter.shape / shape.emitter disagreeing, mesh face
+    indices >= vertex_count, BSDF indices out of range."""
+    L = amvpt_mod.hip_lib()
+    s, sd, vd, p = _cbox_desc(amvpt_mod)
+    nd, shapes, bsdfs, ems = _copy_scene(amvpt_mod, sd)
+    keep = []
+    if breakage == "emitter_range":
+        shapes[0].emitter = nd.emitter_count + 3
+    elif breakage == "emitter_pair":
+        light = ems[0].shape
+        other = 1 if light != 1 else 2
+        shapes[other].emitter = 0            # a second shape claims emitter 0
+    elif breakage == "face_index":
+        mesh = next(i for i in range(nd.shape_count) if shapes[i].type == 1)
+        n = shapes[mesh].face_count * 3
+        faces = (ctypes.c_uint32 * n)(*[shapes[mesh].faces[k] for k in range(n)])
+        faces[n - 1] = shapes[mesh].vertex_count
+        keep.append(faces)
+        shapes[mesh].faces = ctypes.cast(faces, ctypes.POINTER(ctypes.c_uint32))
+    else:
+        shapes[0].bsdf = nd.bsdf_count
+    h = ctypes.c_void_p()
+    assert L.amvpt_scene_create(ctypes.byref(nd), ctypes.byref(h)) == 1   # AMVPT_ERR_INVALID
+    assert L.amvpt_last_error().decode()
+
+
+def test_scene_create_accepts_the_loaded_descriptor(amvpt_mod):
+    """The unmodified loader output passes validation (then needs a device)."""
+    L = amvpt_mod.hip_lib()
+    s, sd, vd, p = _cbox_desc(amvpt_mod)
+    nd, shapes, bsdfs, ems = _copy_scene(amvpt_mod, sd)
+    h = ctypes.c_void_p()
+    rc = L.amvpt_scene_create(ctypes.byref(nd), ctypes.byref(h))
+    if amvpt_mod.device_count() > 0:
+        assert rc == 0
+        L.amvpt_scene_destroy(h)
+    else:
+        assert rc == 5, L.amvpt_last_error()   # AMVPT_ERR_NO_DEVICE

@@ -1,0 +1,219 @@
+"""GPU parity at the shapes of every BASELINE config.
+
+C1/C2/C3 shapes are covered in test_gpu_parity.py.  Here:
+  * C5  -- 32-view light-field array: 8x4 grid, groups of 4, adaptive 3, rendered whole and
+           as 8 lane shards (the 8-GPU partition, one shard per rank) with the per-pass count
+           exchange; records bit-identical, shard films sum to the oracle frame;
+  * C4  -- Veach-MIS 8-view frame as 8 lane shards (film tiles of the 8-GPU run), summed;
+  * M   -- the metric's full-resolution configuration (4096x2048 quilt, G = 8, 64 spp in 4
+           passes of 16): lanes [0, 2^22) of pass 0, records bit-identical to the oracle;
+  * the group-size fallback of mvpath.cpp:192-217 (N % reuse_count != 0).
+The oracle runs on the box's host cores (16 threads); sizes keep each test within seconds.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import SCENES
+
+pytestmark = pytest.mark.gpu
+
+CBOX = os.path.join(SCENES, "cbox_grid.xml")
+VEACH = os.path.join(SCENES, "veach_grid.xml")
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _bit_equal(a, b):
+    return (a == b) | (np.isnan(a) & np.isnan(b))
+
+
+def _records_match(g, o):
+    eq = _bit_equal(g, o).all(axis=(1, 2))
+    if not eq.all():
+        bad = np.argwhere(~eq)[:3, 0]
+        for lane in bad:
+            print("lane", lane, "\ngpu", g[lane], "\noracle", o[lane])
+    return eq.mean()
+
+
+def _lane_shard(n, r, world):
+    from amvpt import dist as adist
+    return adist.lane_shard(n, r, world)
+
+
+def _render_shards(amvpt_mod, sd, vd, p, shards, exchange_counts=None):
+    """Render the lane ranges one after another on this GPU into one film (as 8 ranks would, then
+    reduce).  With adaptive > 0 the per-pass count exchange is supplied from exchange_counts."""
+    torch = _torch()
+    dev = amvpt_mod.DeviceScene(sd)
+    C = 5 if p.film_alpha else 4
+    film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
+    try:
+        for r, (b, e) in enumerate(shards):
+            if exchange_counts is not None:
+                calls = iter(range(len(exchange_counts[0])))
+
+                def fn(local, r=r, calls=calls):
+                    k = next(calls)
+                    assert local == exchange_counts[r][k]
+                    return sum(c[k] for c in exchange_counts[:r]), sum(c[k] for c in exchange_counts)
+                amvpt_mod.set_adaptive_exchange(fn)
+            dev.render(vd, p, film.data_ptr(), b, e)
+            torch.cuda.synchronize()
+    finally:
+        amvpt_mod.set_adaptive_exchange(None)
+    return film.cpu().numpy()
+
+
+def _count_phase(amvpt_mod, sd, vd, p, shards):
+    """Each range's flagged-lane count per pass (what one all-gather per pass would carry)."""
+    torch = _torch()
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    counts = []
+    try:
+        for b, e in shards:
+            got = []
+            amvpt_mod.set_adaptive_exchange(lambda local, got=got: (got.append(local), (0, local))[1])
+            dev.render(vd, p, film.data_ptr(), b, e)
+            torch.cuda.synchronize()
+            counts.append(got)
+    finally:
+        amvpt_mod.set_adaptive_exchange(None)
+    return counts
+
+
+def test_c5_light_field_array_whole_and_eight_shards(gpu_ready, amvpt_mod, oracle):
+    """C5 shape: 32 views on an 8x4 grid, reuse_count 4 (8 groups of 4), adaptive 3, 16 spp; per-view
+    16^2.  Whole frame: records bit-identical; 8 lane shards + count exchange: films sum to the frame."""
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16, gx=8, gy=4, reuse=4, adaptive=3)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    assert plan["group"] == 4 and p.n_views == 32 and p.adaptive == 3
+    n = plan["lanes"]
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    rec = torch.zeros((n, 4, 8), dtype=torch.float32, device="cuda")
+    dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, 0, n)
+    torch.cuda.synchronize()
+    ofilm, orec, st = oracle.render(sd, vd, p, threads=16, record_pass=0)
+    assert st["adaptive_lanes"] > 0
+    assert _records_match(rec.cpu().numpy(), orec) == 1.0
+    scale = np.abs(ofilm).max()
+    assert np.abs(film.cpu().numpy() - ofilm).max() <= 1e-5 * scale
+    shards = [_lane_shard(n, r, 8) for r in range(8)]
+    counts = _count_phase(amvpt_mod, sd, vd, p, shards)
+    assert sum(sum(c) for c in counts) * 3 == st["adaptive_lanes"]
+    summed = _render_shards(amvpt_mod, sd, vd, p, shards, counts)
+    assert np.abs(summed - ofilm).max() <= 1e-5 * scale
+
+
+def test_c4_veach_eight_film_tile_shards(gpu_ready, amvpt_mod, oracle):
+    """C4 shape: the Veach-MIS 8-view frame (GGX plates, sphere lights, G = 8, sa_mis) split into the
+    8 contiguous lane ranges (= bands of quilt rows) the 8-GPU run gives its ranks; every range's
+    records match the oracle's and the 8 films sum to the oracle frame (the RCCL reduce)."""
+    torch = _torch()
+    s = amvpt_mod.load_file(VEACH, res=24, spp=32)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    assert plan["group"] == 8 and plan["passes"] == 2
+    n = plan["lanes"]
+    shards = [_lane_shard(n, r, 8) for r in range(8)]
+    ofilm, orec, _ = oracle.render(sd, vd, p, threads=16, record_pass=1)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    for b, e in shards:
+        rec = torch.zeros((e - b, 8, 8), dtype=torch.float32, device="cuda")
+        dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 1, b, e)
+        torch.cuda.synchronize()
+        assert _records_match(rec.cpu().numpy(), orec[b:e]) == 1.0, (b, e)
+    scale = np.abs(ofilm).max()
+    assert np.abs(film.cpu().numpy() - ofilm).max() <= 1e-5 * scale
+
+
+def test_config_m_full_resolution_window(gpu_ready, amvpt_mod, oracle):
+    """Config M itself (8 views of 1024^2 on a 4x2 grid = 4096x2048 quilt, reuse 8, 64 spp = 4 passes
+    of 16, max_depth 8, rr_depth 5, seed 0): records of pass 0 for lanes [0, 2^22) (the first 64 quilt
+    rows) are bit-identical to the oracle's.  Pass 0's records do not depend on the pass count, so the
+    oracle renders that window with spp 16 (one pass); its film is checked against a one-pass GPU render
+    of the same window."""
+    torch = _torch()
+    n = 1 << 22
+    s = amvpt_mod.load_file(CBOX, res=1024, spp=64, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    assert (p.film_width, p.film_height, plan["group"], plan["passes"], plan["spp_per_pass"]) == (4096, 2048, 8, 4, 16)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    rec = torch.zeros((n, 8, 8), dtype=torch.float32, device="cuda")
+    dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, 0, n)
+    torch.cuda.synchronize()
+    g = rec.cpu().numpy()
+    del rec
+    s1 = amvpt_mod.load_file(CBOX, res=1024, spp=16, gx=4, gy=2, reuse=8)
+    sd1, vd1, p1 = s1.describe(0, 0, 0)
+    ofilm, orec, st = oracle.render(sd1, vd1, p1, lane_begin=0, lane_end=n, threads=16, record_pass=0)
+    assert st["lanes"] == n
+    assert _records_match(g, orec) == 1.0
+    del g, orec
+    film.zero_()
+    amvpt_mod.DeviceScene(sd1).render(vd1, p1, film.data_ptr(), 0, n)
+    torch.cuda.synchronize()
+    gf = film.cpu().numpy()
+    assert np.abs(gf - ofilm).max() <= 1e-5 * np.abs(ofilm).max()
+
+
+@pytest.mark.parametrize("gx,gy,reuse,G", [(4, 3, 5, 6), (5, 2, 3, 5)], ids=["n12_r5_g6", "n10_r3_g5"])
+def test_group_size_fallback(gpu_ready, amvpt_mod, oracle, gx, gy, reuse, G):
+    """mvpath.cpp:192-217: N % reuse_count != 0 -> the smallest divisor of N in [8, N), else the largest
+    divisor in [2, 8]."""
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16, gx=gx, gy=gy, reuse=reuse)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    assert plan["group"] == G
+    torch = _torch()
+    n = plan["lanes"]
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    rec = torch.zeros((n, G, 8), dtype=torch.float32, device="cuda")
+    dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, 0, n)
+    torch.cuda.synchronize()
+    ofilm, orec, _ = oracle.render(sd, vd, p, threads=16, record_pass=0)
+    assert _records_match(rec.cpu().numpy(), orec) == 1.0
+    assert np.abs(film.cpu().numpy() - ofilm).max() <= 1e-5 * np.abs(ofilm).max()
+
+
+def test_empty_lane_range_joins_the_count_exchange(gpu_ready, amvpt_mod):
+    """a rank whose lane range is empty still takes part in every pass's exchange."""
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=16, spp=32, adaptive=1)
+    sd, vd, p = s.describe(0, 0, 0)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    calls = []
+    amvpt_mod.set_adaptive_exchange(lambda local: (calls.append(local), (0, 0))[1])
+    try:
+        amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), 10, 10)
+    finally:
+        amvpt_mod.set_adaptive_exchange(None)
+    assert calls == [0, 0]   # one call per pass (2 passes of 16)
+
+
+def test_render_rejects_inconsistent_view_tables(gpu_ready, amvpt_mod):
+    """n_views == 0, or a grid whose n_views != grid_x * grid_y, is AMVPT_ERR_INVALID."""
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=8, spp=4)
+    sd, vd, p = s.describe(0, 0, 0)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    for n in (0, 3):
+        q = type(p).from_buffer_copy(p)
+        q.n_views = n
+        with pytest.raises(RuntimeError, match="n_views"):
+            dev.render(vd, q, film.data_ptr())
