@@ -242,6 +242,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "counters": {k: c[k] for k in ("lanes", "vertices", "reuse_lanes", "visibility_rays", "view_splats",
+                                             "nonfinite_samples", "negative_samples", "record_bytes",
                                              "splat_fallback")},
         }
         print(json.dumps(out))
@@ -287,8 +288,9 @@ def kernel_bytes(c, G, C):
     lanes, verts, shadow = c["lanes"], c["vertices"], c["shadow_rays"]
     suffix = max(0, verts - lanes)        # suffix vertices (k_extend / k_bounce entries)
     pushed = min(lanes, suffix)           # paths that left the primary vertex (= paths that terminate)
-    rec = 48 * G + 32                     # view records (3 x 16 B x G) + lane_rec + lane_out
+    rec = c["record_bytes"] or 16         # lane records (4 x 16 B) + lane_out + view records (amvpt_counters)
     adapt = c["adaptive_lanes"]
+    nee = 64                              # NEE record (shadow ray 28 B + destination + throughput + contribution)
     return {
         "k_prim_hit": 16 * lanes,                                   # hit record out
         "k_prim_req": (16 + 48) * lanes,                            # hit in, visibility requests out

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 4
+#define AMVPT_ABI_VERSION 5
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -185,6 +185,10 @@ typedef struct amvpt_counters {
     uint64_t shadow_rays;      /* suffix NEE rays traced by k_shadow */
     double kernel_ms[12];
     uint64_t kernel_launches[12];
+    /* ABI 5 */
+    uint64_t record_bytes;     /* bytes of per-lane records k_mv_primary writes and the splat reads (lane + views) */
+    uint64_t nonfinite_samples; /* splatted view samples with a NaN/Inf value (ImageBlock::put's check, imageblock.cpp:180-204) */
+    uint64_t negative_samples;  /* splatted view samples with a negative RGB component (same check) */
 } amvpt_counters;
 
 /* kernels of the pipeline, for amvpt_counters.kernel_ms */

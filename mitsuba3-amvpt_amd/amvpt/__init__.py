@@ -74,7 +74,8 @@ class Counters(ctypes.Structure):
                 ("visibility_rays", u64), ("view_splats", u64), ("adaptive_lanes", u64),
                 ("kernel_ms_primary", f64), ("kernel_ms_bounce", f64), ("kernel_ms_splat", f64),
                 ("total_ms", f64), ("splat_fallback", u64),
-                ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12)]
+                ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12),
+                ("record_bytes", u64), ("nonfinite_samples", u64), ("negative_samples", u64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

@@ -102,8 +102,11 @@ struct Bufs {
     uint32_t *cnt_in, *cnt_out;  /* kQParts partition counters each, kCntStride words apart */
     uint32_t qcap;               /* entries per queue partition */
     float4 *lane_out;     /* (indirect / result rgb, valid_ray) */
-    float4 *lane_rec;     /* (pdfW, flags) */
-    float4 *view_rec;     /* [3][G][n]: (pos | weight, flags) as two float2 planes, (result), (bsdf_val) */
+    float4 *lrec[4];      /* k_mv_primary -> splat, per lane: (R0, pdfW), (Dp, lane flags), (Bv, valid mask),
+                           * (hit point, indirect mask); R0 = slot 0's result, Dp / Bv = all-diffuse views'
+                           * direct light / BSDF value (see k_mv_primary) */
+    float4 *vrec;         /* per view [G][n]: all-diffuse scenes one float (weight); otherwise two float4
+                           * planes [G][n] (result, weight) and [G][n] (bsdf value, view flags) */
     float *film;
     float *records;       /* optional [n][G][8] */
     unsigned long long *stats; /* [0] vertices [1] reuse lanes [2] visibility rays [3] splats */
@@ -330,7 +333,64 @@ AD Ray sample_ray_idx(const KParams &P, const DView *V, float ax, float ay, uint
     return camera_sample_ray(V[index], fx - (float) ux, fy - (float) uy, apx, apy);
 }
 
+/* the view index part of sample_ray_idx (same arithmetic), for kernels that only need it */
+AD uint32_t sensor_index(const KParams &P, float ax, float ay) {
+    if (!P.multisensor) return 0;
+    if (P.batch) {
+        const uint32_t ux = (uint32_t) (ax * (float) P.n_views);
+        uint32_t index = min(ux, P.n_views - 1);
+        if (P.rev_x) index = (P.n_views - 1) - index;
+        return index;
+    }
+    uint32_t ix = (uint32_t) (ax * (float) P.gx), iy = (uint32_t) (ay * (float) P.gy);
+    if (P.rev_x) ix = (P.gx - 1) - ix;
+    if (P.rev_y) iy = (P.gy - 1) - iy;
+    return min(ix + P.gx * iy, P.n_views - 1);
+}
+
 struct Surf { f3 p, d; float uvx, uvy, pdf, Jp; bool face, valid; };
+
+/* Film position of a camera-space point: the raster part of PerspectiveCamera::sample_surface
+ * (perspective.cpp:327-385).  Shared by the primary vertex and the splat's reprojection, so
+ * both compute the same bits. */
+template <class VT> AD void persp_uv(const VT &v, f3 ref_p, float &ux, float &uy, float &uvx, float &uvy) {
+    f3 screen = xf_point(v.camera_to_sample, ref_p);
+    ux = screen.x - v.pp[0];
+    uy = screen.y - v.pp[1];
+    uvx = ux * v.res[0];
+    uvy = uy * v.res[1];
+}
+/* the same for ThinLensCamera::sample_surface (thinlens.cpp:358-418) */
+template <class VT>
+AD void thin_uv(const VT &v, f3 ref_p, float apx, float apy, f3 &aperture_p, f3 &local_d, float &inv_dist, f3 &scr,
+                float &uvx, float &uvy) {
+    float tx, ty;
+    disk_concentric(apx, apy, tx, ty);
+    aperture_p = mk(tx * v.aperture_radius, ty * v.aperture_radius, 0.f);
+    local_d = ref_p - aperture_p;
+    const float dist = norm(local_d);
+    inv_dist = rcp(dist);
+    local_d = local_d * inv_dist;
+    const float inv_f = 1.f / v.focus_distance;
+    const f3 film_plane = mk(aperture_p.x * inv_f + local_d.x / local_d.z, aperture_p.y * inv_f + local_d.y / local_d.z,
+                             aperture_p.z * inv_f + local_d.z / local_d.z);
+    scr = xf_point_affine(v.camera_to_sample, film_plane);
+    uvx = scr.x * v.res[0];
+    uvy = scr.y * v.res[1];
+}
+/* Surf::uvx/uvy of camera_sample_surface(v, {p}, active = true, ap): the splat position of a
+ * reprojected view sample, recomputed from the primary hit point instead of stored */
+template <class VT> AD void camera_uv(const VT &v, f3 p, float apx, float apy, float &uvx, float &uvy) {
+    const f3 ref_p = xf_point_affine(v.to_world_inv, p);
+    if (v.type == AMVPT_CAMERA_THINLENS) {
+        f3 ap, ld, scr;
+        float idist;
+        thin_uv(v, ref_p, apx, apy, ap, ld, idist, scr, uvx, uvy);
+    } else {
+        float ux, uy;
+        persp_uv(v, ref_p, ux, uy, uvx, uvy);
+    }
+}
 
 /* PerspectiveCamera::sample_surface under a masked vcall (perspective.cpp:327-385) */
 AD Surf persp_sample_surface(const DView &v, const SI &it, bool active) {
@@ -341,11 +401,9 @@ AD Surf persp_sample_surface(const DView &v, const SI &it, bool active) {
     if (!active) return r;
     f3 ref_p = xf_point_affine(v.to_world_inv, it.p);
     bool a = ref_p.z >= v.near_clip && ref_p.z <= v.far_clip;
-    f3 screen = xf_point(v.camera_to_sample, ref_p);
-    float ux = screen.x - v.pp[0], uy = screen.y - v.pp[1];
+    float ux, uy;
+    persp_uv(v, ref_p, ux, uy, r.uvx, r.uvy);
     a = a && ux >= 0.f && ux <= 1.f && uy >= 0.f && uy <= 1.f;
-    r.uvx = ux * v.res[0];
-    r.uvy = uy * v.res[1];
     float dist = norm(ref_p), inv_dist = rcp(dist);
     float ctf = ref_p.z;
     a = a && ctf > 0.f;
@@ -370,22 +428,13 @@ AD Surf thin_sample_surface(const DView &v, const SI &it, bool active, float apx
     if (!active) return r;
     const f3 ref_p = xf_point_affine(v.to_world_inv, it.p);
     bool a = ref_p.z >= v.near_clip && ref_p.z <= v.far_clip;
-    float tx, ty;
-    disk_concentric(apx, apy, tx, ty);
-    const f3 aperture_p = mk(tx * v.aperture_radius, ty * v.aperture_radius, 0.f);
-    f3 local_d = ref_p - aperture_p;
-    const float dist = norm(local_d), inv_dist = rcp(dist);
-    local_d = local_d * inv_dist;
+    f3 aperture_p, local_d, scr;
+    float inv_dist;
+    thin_uv(v, ref_p, apx, apy, aperture_p, local_d, inv_dist, scr, r.uvx, r.uvy);
     const float ictf = rcp(local_d.z), ictf3 = ictf * ictf * ictf;
-    const float inv_f = 1.f / v.focus_distance;
-    const f3 film_plane = mk(aperture_p.x * inv_f + local_d.x / local_d.z, aperture_p.y * inv_f + local_d.y / local_d.z,
-                             aperture_p.z * inv_f + local_d.z / local_d.z);
-    const f3 scr = xf_point_affine(v.camera_to_sample, film_plane);
     a = a && scr.x >= 0.f && scr.y >= 0.f && scr.x <= 1.f && scr.y <= 1.f;
     const float pdf_lens = rcp(sqr(v.aperture_radius) * kPi);
     r.pdf = pdf_lens * (v.normalization * ictf3);
-    r.uvx = scr.x * v.res[0];
-    r.uvy = scr.y * v.res[1];
     r.p = xf_point_affine(v.to_world, aperture_p);
     r.d = (r.p - it.p) * inv_dist;
     float cts = dot(r.d, it.n);
@@ -399,6 +448,33 @@ AD Surf camera_sample_surface(const DView &v, const SI &it, bool active, float a
     return v.type == AMVPT_CAMERA_THINLENS ? thin_sample_surface(v, it, active, apx, apy)
                                            : persp_sample_surface(v, it, active);
 }
+/* The raster fields of a DView (floats 12..23, 40..55, 60..67 of the 68-float record):
+ * all camera_uv reads.  raster_uniform() fetches them with scalar loads when the view index
+ * is wave-uniform (a splat wave = 64 pixels of one view row, so it nearly always is). */
+struct DRaster {
+    float to_world_inv[12];
+    float camera_to_sample[16];
+    float res[2], pp[2];
+    uint32_t type;
+    float aperture_radius, focus_distance, pad1;
+};
+static_assert(sizeof(DView) == 17 * 16 && sizeof(DRaster) == 9 * 16, "view record layout");
+AD DRaster raster_uniform(const DView *V, uint32_t id) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(4))) const v4u cv4u;
+    const cv4u *p = (const cv4u *) (uintptr_t) V + (size_t) __builtin_amdgcn_readfirstlane(id) * 17;
+    const v4u q[9] = {p[3], p[4], p[5], p[10], p[11], p[12], p[13], p[15], p[16]};
+    DRaster r;
+    __builtin_memcpy(&r, q, sizeof(r));
+    return r;
+}
+/* camera_uv of view `id` (wave-uniform fast path, per-lane fallback) */
+AD void view_uv(const DView *V, uint32_t id, f3 p, float apx, float apy, float &uvx, float &uvy) {
+    const uint32_t id0 = __builtin_amdgcn_readfirstlane(id);
+    if (__ballot(id != id0) == 0ull) camera_uv(raster_uniform(V, id0), p, apx, apy, uvx, uvy);
+    else camera_uv(V[id], p, apx, apy, uvx, uvy);
+}
+
 /* Surf::p of camera_sample_surface (the visibility-ray target), bit for bit */
 AD f3 camera_point(const DView &v, float apx, float apy) {
     if (v.type != AMVPT_CAMERA_THINLENS) return xf_point_affine(v.to_world, mk(0.f, 0.f, 0.f));
@@ -765,6 +841,20 @@ AD uint32_t lane_slot(const KParams &P, uint32_t lane) {
         return base + (smp / half) * (uint32_t) kSplatBlock + (smp % half) * ppb + p;
     }
     return lane;
+}
+
+/* ImageBlock::put's sample check (imageblock.cpp:180-204: warn_invalid / warn_negative): an active
+ * sample with a non-finite channel, or (finite) with a channel below -1e-5, is counted
+ * (amvpt_counters.nonfinite_samples / negative_samples) -- the reference logs a warning. */
+AD void check_sample(const KParams &P, const float *vals, bool active, unsigned long long &nf,
+                     unsigned long long &neg) {
+    bool fin = true, nonneg = true;
+    for (uint32_t k = 0; k < P.C; ++k) {
+        fin = fin && finite_(vals[k]);
+        nonneg = nonneg && vals[k] >= -1e-5f;
+    }
+    nf += (active && !fin) ? 1 : 0;
+    neg += (active && fin && !nonneg) ? 1 : 0;
 }
 
 AD void pack_vals(const KParams &P, C3 v, float alpha, float weight, float *vals) {
@@ -1151,7 +1241,10 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
             r[0] = sx; r[1] = sy; r[2] = spec.r; r[3] = spec.g; r[4] = spec.b; r[5] = alpha; r[6] = 1.f; r[7] = 1.f;
         }
     }
+    unsigned long long nonfinite = 0, negative = 0;
+    check_sample(P, vals, ok, nonfinite, negative);
     block_put<C>(P, B.film, L, 0, putx, puty, vals, ok, P.coalesce_single != 0);
+    if (B.stats) { stat_add(B.stats, 6, nonfinite); stat_add(B.stats, 7, negative); }
 }
 
 template <int C>
@@ -1170,7 +1263,10 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_adapt(KParams P, Bufs B) 
         const float w = P.adapt_w;
         pack_vals(P, C3{w * lo.x, w * lo.y, w * lo.z}, 1.f, w, vals);
     }
+    unsigned long long nonfinite = 0, negative = 0;
+    check_sample(P, vals, ok, nonfinite, negative);
     block_put<C>(P, B.film, L, 0, sx, sy, vals, ok, false);
+    if (B.stats) { stat_add(B.stats, 6, nonfinite); stat_add(B.stats, 7, negative); }
 }
 
 /* ------------------------------------------------------------------ */
@@ -1302,7 +1398,7 @@ __global__ void __launch_bounds__(64 * G) k_vis(KParams P, const DScene *Sp, con
 /* ------------------------------------------------------------------ */
 
 enum : uint32_t { VF_VALID = 1u, VF_INDIRECT = 2u };
-enum : uint32_t { LF_VALIDRAY = 1u, LF_ADAPT = 2u, LF_PHIT = 4u, LF_MIS = 8u };
+enum : uint32_t { LF_VALIDRAY = 1u, LF_ADAPT = 2u, LF_REUSE = 4u, LF_MIS = 8u, LF_DIRECT = 16u };
 
 struct SD {        /* SampleData (mvpath.h:150-167) without the derived fields */
     C3 result, bsdf_val;
@@ -1399,35 +1495,30 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         const PrimRay pr = primary_raygen(P, V, i);
         Pcg rng = pr.rng;
         const uint32_t v1 = pr.v1, p_idx = pr.p_idx;
-        const float sx = pr.sx, sy = pr.sy, apx = pr.apx, apy = pr.apy;
+        const float apx = pr.apx, apy = pr.apy;
         const Ray pray = pr.ray;
-        /* rec0 = two float2 planes, [G][n] positions then [G][n] (weight, flags): each
-         * half is written whole by one wave (512 contiguous bytes), never as a partial line */
-        float2 *const rec0 = reinterpret_cast<float2 *>(B.view_rec);
-        float4 *const rec1 = B.view_rec + (size_t) G * n,
-                      *const rec2 = B.view_rec + (size_t) 2 * G * n;
-        /* view index of slot k and its film position (quilt offset for k >= 1) */
+        /* view records (see Bufs): kDiff -> one weight per view; generic -> (result, weight) and
+         * (bsdf value, flags) per view.  Splat positions are not stored: k_splat_multi recomputes
+         * them from the hit point (camera_uv) and the lane's jitter. */
+        float *const vw = reinterpret_cast<float *>(B.vrec);
+        float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) G * n;
         auto view_of = [&](int k) -> uint32_t { return group_view<G>(p_idx, k); };
-        auto put_pos = [&](int k, float x, float y) {
-            if (k > 0) {
-                uint32_t id = view_of(k);
-                uint32_t yy = id / P.gx, xx = id - yy * P.gx;
-                if (P.rev_x) xx = (P.gx - 1) - xx;
-                if (P.rev_y) yy = (P.gy - 1) - yy;
-                x += (float) (xx * P.sres_x);
-                y += (float) (yy * P.sres_y);
+        auto put_view = [&](int k, float w, C3 res, C3 bv, uint32_t vf) {
+            const size_t o = (size_t) k * n + slot;
+            if (kDiff) {
+                vw[o] = w;
+            } else {
+                vR[o] = make_float4(res.r, res.g, res.b, w);
+                vB[o] = make_float4(bv.r, bv.g, bv.b, bitsf(vf));
             }
-            rec0[(size_t) k * n + slot] = make_float2(x, y);
         };
-        auto put_wf = [&](int k, float w, uint32_t vflags) {
-            const uint32_t vf = (((vflags >> k) & 1u) ? VF_VALID : 0u) | (((vflags >> (16 + k)) & 1u) ? VF_INDIRECT : 0u);
-            rec0[(size_t) (G + k) * n + slot] = make_float2(w, bitsf(vf));
-        };
-        uint32_t vflags = 0;   /* bit k: valid, bit 16 + k: indirect */
-        float w0 = 1.f;        /* slot 0's splat weight */
-        C3 result0 = c3(0.f);  /* slot-0 emission + direct, for the non-MIS path */
-        bool records_done = false;
-        put_pos(0, sx, sy);
+        uint32_t vmask = 0, imask = 0;   /* bit k: view k valid / indirect */
+        float w0 = 1.f;                  /* slot 0's splat weight */
+        C3 R0 = c3(0.f);                 /* slot 0's result: emission + direct light */
+        C3 Dp = c3(0.f);                 /* kDiff: direct light through a valid view k >= 1 */
+        C3 Bv = c3(0.f);                 /* kDiff: BSDF value of every indirect view */
+        f3 hp = mk(0.f, 0.f, 0.f);       /* primary hit point (reprojection in the splat) */
+        bool records_done = false, reuse_l = false, direct_l = false;
 
         /* ---- sample_multi (mvpath_multi.h:130-369) ---- */
         bool valid_ray = false, adapt_mask = false;
@@ -1436,6 +1527,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         if (P.max_depth != 0) {
             SI si = compute_si(sc, pray, hit_of(hitv));
             bool p_hit = si.valid();
+            hp = si.p;
             int32_t em = si_emitter(sc, si);
             bool direct_em = em >= 0;
             C3 emitted = c3(0.f);
@@ -1449,6 +1541,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             if (sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w) && (occm & 1u))
                 occlude_emitter_sample(ds, em_w);
             active_em = active_em && ds.pdf != 0.f;
+            direct_l = active_em;
             f3 wo = si.sh.to_local(ds.d);
             float rand_1 = rng.next_1d();
             float r2a = rng.next_1d(), r2b = rng.next_1d();
@@ -1463,6 +1556,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             bool flag_diff = (bsmp.type & BF_Diffuse) != 0;
             bool delta = flag_delta || flag_null, p_not_delta = !delta && p_hit;
             bool reuse = !direct_em && p_not_delta && bsdf_smooth;
+            reuse_l = reuse;
             st_reuse += reuse ? 1 : 0;
             bool p_face = si.wi.z > 0.f;
             if (should_mis) {
@@ -1477,17 +1571,20 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
                 VSF(F_PDF, 0) = pdf0; VSF(F_JP, 0) = Jp0;
-                vflags |= p_hit ? (1u | (1u << 16)) : 0u;
+                vmask |= p_hit ? 1u : 0u;
+                imask |= p_hit ? 1u : 0u;
                 const f3 wo_r0 = reflect_l(si.wi);
-                uint32_t wpos = 0;   /* kDiff: bit k = (wi_k.z > 0) */
                 if (!kDiff) {
                     VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
                     VSF(F_PDFM, 0) = bd.diffuse ? 1.f : (P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
                                                                    : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit));
                 }
-                /* view k's wi (kDiff: only the sign of z matters to diffuse.cpp) */
+                /* view k's wi.  kDiff runs only on scenes without shading normals: there a valid
+                 * view k sees the face the primary sees (sensors_visible), so sign(wi_k.z) =
+                 * sign(wi.z) and diffuse eval/pdf (which read wi only through that sign) give the
+                 * primary's values -- one BSDF value per lane instead of one per view. */
                 auto wi_of = [&](int k) -> f3 {
-                    if (kDiff) return k == 0 ? si.wi : mk(0.f, 0.f, ((wpos >> k) & 1u) ? 1.f : -1.f);
+                    if (kDiff) return si.wi;
                     return mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
                 };
                 /* pdf_Mat of view k toward view 0 (tv_pdf, camera_selection) */
@@ -1514,15 +1611,12 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                                                 : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
                         VSF(F_PDFM, k) = pdfM;
                         pdf_Mat = mat_pdf(wik, pdfM, valid);
-                    } else {
-                        wpos |= wik.z > 0.f ? (1u << k) : 0u;
                     }
                     float J = r.Jp * iJp0;
                     float pdf_J = J > 1.f ? rcp(J) : J;
                     float pdf_Sel = pdf_Mat * pdf_J;
                     valid = valid && (rng.next_1d() < pdf_Sel);
                     VSF(F_JP, k) = r.Jp;
-                    put_pos(k, r.uvx, r.uvy);
                     VSF(F_PDF, k) = valid ? r.pdf : 0.f;
                     bool indirect = valid, direct = valid;
                     bool replace = n_indir * rng.next_1d() < 1.f;
@@ -1542,17 +1636,27 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     /* kDiff: a valid view's sample is the primary's (same type, same wo) */
                     (void) replace;
                     n_indir += (float) indirect;
-                    vflags |= (valid ? (1u << k) : 0u) | (indirect ? (1u << (16 + k)) : 0u);
+                    vmask |= valid ? (1u << k) : 0u;
+                    imask |= indirect ? (1u << k) : 0u;
                 }
                 direct_pdf /= n_direct;
                 const float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
                 const C3 emis_mis = em_w * mis_em;
+                /* kDiff lane values: slot 0's result, a valid view's direct light, the indirect
+                 * views' BSDF value and pdf (the same for every view, see wi_of) */
+                float bp_d = 0.f;
+                if (kDiff) {
+                    R0 = emitted;
+                    if (active_em && (vmask & 1u)) R0 = cfma(bsdf_val, emis_mis, emitted);
+                    if (active_em) Dp = cfma(bsdf_val, emis_mis, c3(0.f));
+                    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, bsmp.wo, true, Bv, bp_d);
+                }
                 /* ---- per view: mis_weights (mvpath_multi.h:466-523), direct light and
                  *      the multi-view mixture pdf (mvpath_multi.h:245-317) ---- */
                 float n_ind = 0.f, pdf = 0.f;
 #pragma unroll 1
                 for (int k = 0; k < G; ++k) {
-                    const bool vk = (vflags >> k) & 1u;
+                    const bool vk = (vmask >> k) & 1u;
                     const float Jpk = VSF(F_JP, k);
                     const float iJpk = k == 0 ? iJp0 : (vk ? rcp(Jpk) : 0.f);
                     const f3 wik = wi_of(k);
@@ -1573,7 +1677,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                             if (j == k) continue;
                             float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
                             f3 worj = reflect_l(mk(VSF(F_WX, j), VSF(F_WY, j), VSF(F_WZ, j)));
-                            const bool vj = (vflags >> j) & 1u;
+                            const bool vj = (vmask >> j) & 1u;
                             float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
                                                        : tv_pdf(S.bsdfs, worj, wik, pdfMk, bd, vj);
                             acc = fmadd(VSF(F_PDF, j), pdf_J * pdf_Mat, acc);
@@ -1589,43 +1693,46 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     }
                     pdfSum += acc;
                     const float wk = pdf_lk / pdfSum;
-                    const size_t o = (size_t) k * n + slot;
-                    /* result: emission (slot 0) + direct light through this view's BSDF value */
-                    C3 res = csel(k == 0, emitted, c3(0.f));
-                    if (active_em && vk) {
-                        C3 bvk = bsdf_val;
-                        if (k > 0) {   /* the value camera_selection evaluated for view k */
-                            float bpk;
-                            bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, wo, true, bvk, bpk);
-                        }
-                        res = cfma(bvk, emis_mis, res);
-                    }
-                    rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
-                    bool valid = (vflags >> (16 + k)) & 1u;
-                    C3 bv;
+                    bool valid = (imask >> k) & 1u;
+                    C3 res = c3(0.f), bv = c3(0.f);
                     float bp;
-                    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, bsmp.wo, valid, bv, bp);
-                    if (k == 0) {
-                        bv = csel(p_not_delta, bv, bsdf_weight);
-                        bp = p_not_delta ? bp : bsmp.pdf;
-                        valid = valid && (bp > 0.f || delta);
+                    if (kDiff) {
+                        bp = valid ? bp_d : 0.f;
+                    } else {
+                        /* result: emission (slot 0) + direct light through this view's BSDF value */
+                        res = csel(k == 0, emitted, c3(0.f));
+                        if (active_em && vk) {
+                            C3 bvk = bsdf_val;
+                            if (k > 0) {   /* the value camera_selection evaluated for view k */
+                                float bpk;
+                                bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, wo, true, bvk, bpk);
+                            }
+                            res = cfma(bvk, emis_mis, res);
+                        }
+                        if (k == 0) R0 = res;
+                        bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, wik, bsmp.wo, valid, bv, bp);
+                        if (k == 0) {
+                            bv = csel(p_not_delta, bv, bsdf_weight);
+                            bp = p_not_delta ? bp : bsmp.pdf;
+                            valid = valid && (bp > 0.f || delta);
+                        }
                     }
                     bool pvalid = bp > 0.f;
-                    valid = valid && ((k == 0) ? (pvalid || delta) : pvalid);
+                    valid = valid && ((k == 0 && !kDiff) ? (pvalid || delta) : pvalid);
                     bp = valid ? bp : 0.f;
                     bv = csel(valid, bv, c3(0.f));
-                    rec2[o] = make_float4(bv.r, bv.g, bv.b, 0.f);
                     pdf += bp;
                     n_ind += (float) valid;
-                    if (!valid) vflags &= ~(1u << (16 + k));
+                    if (!valid) imask &= ~(1u << k);
                     if (k == 0) w0 = wk;
-                    else put_wf(k, wk, vflags);
+                    else put_view(k, wk, res, bv, (vk ? VF_VALID : 0u) | (valid ? VF_INDIRECT : 0u));
+                    if (k == 0 && !kDiff) Bv = bv;   /* slot 0's (bsdf value), stored with slot 0 below */
                 }
                 bsmp.pdf = p_not_delta ? pdf / n_ind : bsmp.pdf;
                 adapt_mask = p_hit && !flag_null && (n_ind <= 1.f);
                 records_done = true;
             } else {
-                vflags |= p_hit ? 1u : 0u;
+                vmask |= p_hit ? 1u : 0u;
 #pragma unroll 1
                 for (int k = 1; k < G; ++k) {
                     Surf r = camera_sample_surface(V[view_of(k)], si, reuse, apx, apy);
@@ -1634,12 +1741,11 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                         ++st_vis;
                         valid = !((occm >> k) & 1u);
                     }
-                    put_pos(k, r.uvx, r.uvy);
-                    vflags |= valid ? (1u << k) : 0u;
+                    vmask |= valid ? (1u << k) : 0u;
                 }
                 float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
-                result0 = emitted;
-                if (active_em) result0 = cfma(bsdf_val, em_w * mis_em, result0);
+                R0 = emitted;
+                if (active_em) R0 = cfma(bsdf_val, em_w * mis_em, R0);
             }
             /* ---- BSDF sampling continuation ---- */
             Ray pd_ray = spawn_ray(si.p, si.n, si.sh.to_world(bsmp.wo));
@@ -1666,28 +1772,27 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             }
             /* p_sample.weight/valid finalisation happens after the suffix */
             if (!p_hit) w0 = 1.f;
-            vflags |= 1u;
+            vmask |= 1u;
         }
         if (!push) B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) | (should_mis ? LF_MIS : 0u);
-        B.lane_rec[slot] = make_float4(pdfW, bitsf(lflags), 0.f, 0.f);
         if (P.max_depth == 0) {
-            /* no intersection at all: slots k >= 1 keep position 0 (+ quilt offset), slot 0 stays invalid */
-#pragma unroll 1
-            for (int k = 1; k < G; ++k) put_pos(k, 0.f, 0.f);
-            vflags = 0;
-            w0 = 0.f;   /* no vertex: every slot keeps weight 0 */
+            /* no intersection at all: every slot keeps weight 0 and is invalid */
+            vmask = 0;
+            imask = 0;
+            w0 = 0.f;
         }
-        put_wf(0, w0, vflags);
+        const uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) |
+                                (should_mis ? LF_MIS : 0u) | (reuse_l ? LF_REUSE : 0u) | (direct_l ? LF_DIRECT : 0u);
+        B.lrec[0][slot] = make_float4(R0.r, R0.g, R0.b, pdfW);
+        B.lrec[1][slot] = make_float4(Dp.r, Dp.g, Dp.b, bitsf(lflags));
+        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(vmask));
+        B.lrec[3][slot] = make_float4(hp.x, hp.y, hp.z, bitsf(imask));
+        /* slot 0 (generic: its bsdf value rides in L2), and the views the MIS loop did not write */
+        put_view(0, w0, R0, Bv, (vmask & 1u ? VF_VALID : 0u) | (imask & 1u ? VF_INDIRECT : 0u));
         if (!records_done) {
 #pragma unroll 1
-            for (int k = 0; k < G; ++k) {
-                const size_t o = (size_t) k * n + slot;
-                if (k > 0) put_wf(k, P.max_depth != 0 ? 1.f : 0.f, vflags);
-                C3 res = csel(k == 0, result0, c3(0.f));
-                rec1[o] = make_float4(res.r, res.g, res.b, 0.f);
-                rec2[o] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            for (int k = 1; k < G; ++k)
+                put_view(k, P.max_depth != 0 ? 1.f : 0.f, c3(0.f), c3(0.f), ((vmask >> k) & 1u) ? VF_VALID : 0u);
         }
     }
     const uint32_t qslot = push_slot(push, B.cnt_out, B.qcap);
@@ -1704,49 +1809,85 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
 /* k_splat_multi<G>: indirect accumulation + splats (mvpath_multi.h:343-368,44-76) */
 /* ------------------------------------------------------------------ */
 
-template <int G, int C>
-__global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) {
+template <int G, int C, bool kDiff>
+__global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, const DView *V, Bufs B) {
     __shared__ SplatLds<C> L;
     splat_lds_init(L);
     const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
     const bool ok = slot < P.chunk_n;
-    const uint32_t i = ok ? slot_lane(P, slot) : 0u;   /* lane (records test hook only) */
+    const uint32_t i = ok ? slot_lane(P, slot) : 0u;   /* chunk-local lane */
     const uint32_t n = P.chunk_n;
-    float4 lr = make_float4(0.f, 0.f, 0.f, 0.f), lo = lr;
-    if (ok) { lr = B.lane_rec[slot]; lo = B.lane_out[slot]; }
-    uint32_t lflags = fbits(lr.y);
-    float pdfW = lr.x;
+    float4 l0 = make_float4(0.f, 0.f, 0.f, 0.f), l1 = l0, l2 = l0, l3 = l0, lo = l0;
+    if (ok) { l0 = B.lrec[0][slot]; l1 = B.lrec[1][slot]; l2 = B.lrec[2][slot]; l3 = B.lrec[3][slot]; lo = B.lane_out[slot]; }
+    const uint32_t lflags = fbits(l1.w), vmask = fbits(l2.w), imask = fbits(l3.w);
+    const float pdfW = l0.w;
+    const C3 R0 = C3{l0.x, l0.y, l0.z}, Dp = C3{l1.x, l1.y, l1.z}, Bv = C3{l2.x, l2.y, l2.z};
+    const f3 hp = mk(l3.x, l3.y, l3.z);
     if (ok && B.amask) B.amask[P.chunk_begin - P.range_begin + i] = (lflags & LF_ADAPT) ? 1u : 0u;
-    bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
-    bool mis = (lflags & LF_MIS) != 0;
-    bool adapt_mask = (lflags & LF_ADAPT) != 0;
-    C3 indirect = C3{lo.x, lo.y, lo.z};
-    float alpha = valid_ray ? 1.f : 0.f;
-    C3 res0 = c3(0.f);
-    if (ok && !mis) {
-        float4 r0 = B.view_rec[(size_t) G * n + slot];
-        res0 = C3{r0.x, r0.y, r0.z} + indirect;
+    const bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
+    const bool mis = (lflags & LF_MIS) != 0, adapt_mask = (lflags & LF_ADAPT) != 0;
+    const bool reuse = (lflags & LF_REUSE) != 0, direct = (lflags & LF_DIRECT) != 0;
+    const C3 indirect = C3{lo.x, lo.y, lo.z};
+    const float alpha = valid_ray ? 1.f : 0.f;
+    const C3 res0 = R0 + indirect;   /* sa_mis = false: every view splats the primary's radiance */
+    /* slot 0's position = the jittered sample (the lane's first two draws), aperture sample, and
+     * the primary view (sample_ray_idx) -- recomputed, not stored */
+    float sx = 0.f, sy = 0.f, apx = .5f, apy = .5f;
+    uint32_t p_idx = 0;
+    if (ok) {
+        const uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        int px, py;
+        lane_pixel(P, lane, px, py);
+        Pcg rng = lane_rng(P.seed_value, lane);
+        const float jx = rng.next_1d(), jy = rng.next_1d();
+        sx = (float) px + jx;
+        sy = (float) py + jy;
+        if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
+        p_idx = sensor_index(P, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f));
     }
-    unsigned long long splats = 0, fallback = 0;
+    const float *const vw = reinterpret_cast<const float *>(B.vrec);
+    const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) G * n;
+    unsigned long long splats = 0, fallback = 0, nonfinite = 0, negative = 0;
     for (int k = 0; k < G; ++k) {
-        size_t o = (size_t) k * n + slot;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) {
-            const float2 *const r0 = reinterpret_cast<const float2 *>(B.view_rec);
-            const float2 pos = r0[o], wf = r0[(size_t) G * n + o];
-            a = make_float4(pos.x, pos.y, wf.x, wf.y);
-        }
-        uint32_t vf = fbits(a.w);
-        bool valid = ok && (vf & VF_VALID) != 0;
-        float weight = a.z;
+        const size_t o = (size_t) k * n + slot;
+        float weight = 0.f;
+        bool valid = false;
         C3 result = c3(0.f);
+        float x = sx, y = sy;
+        if (k > 0) {
+            /* reprojected position in view k (camera_sample_surface, inactive -> 0) + quilt offset */
+            const uint32_t id = group_view<G>(p_idx, k);
+            float ux = 0.f, uy = 0.f;
+            view_uv(V, id, hp, apx, apy, ux, uy);
+            x = reuse ? ux : 0.f;
+            y = reuse ? uy : 0.f;
+            uint32_t yy = id / P.gx, xx = id - yy * P.gx;
+            if (P.rev_x) xx = (P.gx - 1) - xx;
+            if (P.rev_y) yy = (P.gy - 1) - yy;
+            x += (float) (xx * P.sres_x);
+            y += (float) (yy * P.sres_y);
+        }
         if (ok) {
-            if (mis) {
-                float4 r = B.view_rec[(size_t) G * n + o], bvv = B.view_rec[(size_t) 2 * G * n + o];
-                result = C3{r.x, r.y, r.z};
-                if (vf & VF_INDIRECT) result = cfma(C3{bvv.x, bvv.y, bvv.z} * pdfW, indirect, result);
+            if (kDiff) {
+                weight = vw[o];
+                valid = (vmask >> k) & 1u;
+                if (mis) {
+                    result = k == 0 ? R0 : csel(direct && valid, Dp, c3(0.f));
+                    if ((imask >> k) & 1u) result = cfma(Bv * pdfW, indirect, result);
+                } else {
+                    result = res0;
+                }
             } else {
-                result = res0;
+                const float4 r = vR[o], bv = vB[o];
+                const uint32_t vf = fbits(bv.w);
+                weight = r.w;
+                valid = (vf & VF_VALID) != 0;
+                if (mis) {
+                    result = C3{r.x, r.y, r.z};
+                    if (vf & VF_INDIRECT) result = cfma(C3{bv.x, bv.y, bv.z} * pdfW, indirect, result);
+                } else {
+                    result = res0;
+                }
             }
         }
         if (k == 0 && P.n_adapt && adapt_mask) weight = weight * P.adapt_w;
@@ -1755,19 +1896,23 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, Bufs B) 
         if (P.debug) {
             if (k > 0) break; /* uniform: every thread breaks at k == 1 */
             pack_vals(P, c3(adapt_mask ? 1.f : 0.f), alpha, 1.f, vals);
-            block_put<C>(P, B.film, L, 0, a.x, a.y, vals, ok, true);
+            block_put<C>(P, B.film, L, 0, x, y, vals, ok, true);
             continue;
         }
         pack_vals(P, v, alpha, weight, vals);
-        block_put<C>(P, B.film, L, k & 1, a.x, a.y, vals, valid, k == 0, &fallback);
+        check_sample(P, vals, valid, nonfinite, negative);
+        block_put<C>(P, B.film, L, k & 1, x, y, vals, valid, k == 0, &fallback);
         splats += valid ? 1 : 0;
         if (ok && P.record) {
             float *rr = B.records + ((size_t) i * G + k) * 8;
-            rr[0] = a.x; rr[1] = a.y; rr[2] = v.r; rr[3] = v.g; rr[4] = v.b; rr[5] = alpha; rr[6] = weight;
+            rr[0] = x; rr[1] = y; rr[2] = v.r; rr[3] = v.g; rr[4] = v.b; rr[5] = alpha; rr[6] = weight;
             rr[7] = valid ? 1.f : 0.f;
         }
     }
-    if (B.stats) { stat_add(B.stats, 3, splats); stat_add(B.stats, 4, fallback); }
+    if (B.stats) {
+        stat_add(B.stats, 3, splats); stat_add(B.stats, 4, fallback);
+        stat_add(B.stats, 6, nonfinite); stat_add(B.stats, 7, negative);
+    }
 }
 
 /* develop: rgb / W (hdrfilm.cpp:400) */
@@ -1995,14 +2140,16 @@ static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStrea
     T.end(st);
 }
 template <int G>
-static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const Bufs &B) {
-    if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5>), grid, dim3(kSplatBlock), 0, st, P, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4>), grid, dim3(kSplatBlock), 0, st, P, B);
+static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff) {
+    if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
 }
 
 typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
                            const Bufs &, bool, bool, bool, KTimer &);
-typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const Bufs &);
+typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const DView *, const Bufs &, bool);
 /* group sizes 2..16: the per-view bit masks (k_prim_req's request bits below the view index at
  * bit 16, k_mv_primary's valid / indirect flags at bits k and 16 + k) hold 16 views */
 static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
@@ -2129,11 +2276,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         o.pad1 = 0.f;
     }
 
-    /* lane arena: queues (2 x 6 x 16 B), lane_out/lane_rec/hit (48 B), NEE queue (64 B), visibility
-     * requests (48 B), view records (48 B x G), occlusion ballots (G / 8 B) */
+    /* lane arena: queues (2 x 6 x 16 B), lane_out + hit (32 B), NEE queue (64 B), visibility requests
+     * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
     const uint64_t span = lane_end - lane_begin;
     const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
-    const size_t per_lane = 12 * 16 + 48 + 64 + 48 + (size_t) 48 * G + (G + 7) / 8;
+    const bool diff_rec = scene->all_diffuse && !scene->shading_normals && diffuse_spec;   /* compact view records */
+    const size_t per_lane = 12 * 16 + 32 + 64 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8;
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
@@ -2189,14 +2337,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     for (int k = 0; k < 6; ++k) qa[k] = (float4 *) carve(16 * qlen);
     for (int k = 0; k < 6; ++k) qb[k] = (float4 *) carve(16 * qlen);
     B.lane_out = (float4 *) carve(16 * chunk);
-    B.lane_rec = (float4 *) carve(16 * chunk);
+    for (int k = 0; k < 4; ++k) B.lrec[k] = (float4 *) carve(16 * chunk);
     B.hit = (float4 *) carve(16 * std::max<uint64_t>(chunk, qlen));
     for (int k = 0; k < 4; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
     for (int k = 0; k < 3; ++k) B.vreq[k] = (float4 *) carve(16 * chunk);
     B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
     B.cnt_nee = cntN;
     B.qcap = qcap;
-    B.view_rec = (float4 *) carve((size_t) 48 * G * chunk);
+    B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : 32) * G * chunk);
     B.film = film;
     B.records = records;
     B.stats = dstats;
@@ -2213,7 +2361,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         const bool brute_on = !(e && e[0] == '0');
         if (uni && g_traversal == 0u && brute_on && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
     }
-    const bool diff = scene->all_diffuse && diffuse_spec;                                          /* kDiff instances */
+    const bool diff = diff_rec;                                                                           /* kDiff instances */
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
@@ -2299,7 +2447,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             T.begin(AMVPT_K_SPLAT, st);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else if (G == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
-            else kSplat[G](sgrid, st, P, B);
+            else kSplat[G](sgrid, st, P, dviews, B, diff_rec);
             T.end(st);
             T.mark(st);
             HIPCHK(hipGetLastError());
@@ -2378,6 +2526,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.splat_fallback = hs[4];
         c.adaptive_lanes = adaptive_lanes;
         c.shadow_rays = hs[5];
+        c.record_bytes = G > 1 ? 64 + 16 + (diff_rec ? 4 : 32) * (uint64_t) G : 0;
+        c.nonfinite_samples = hs[6];
+        c.negative_samples = hs[7];
         T.flush();
         HIPCHK(T.err);
         for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }

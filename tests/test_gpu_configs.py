@@ -217,3 +217,19 @@ def test_render_rejects_inconsistent_view_tables(gpu_ready, amvpt_mod):
         q.n_views = n
         with pytest.raises(RuntimeError, match="n_views"):
             dev.render(vd, q, film.data_ptr())
+
+
+@pytest.mark.parametrize("scene,G,compact", [(CBOX, 4, True), (VEACH, 8, False)], ids=["cbox", "veach"])
+def test_counters_report_records_and_invalid_samples(gpu_ready, amvpt_mod, scene, G, compact):
+    """Debug counters (SURVEY section 5): ImageBlock::put's invalid / negative sample check runs on the
+    device (imageblock.cpp:180-204) -- zero on these scenes -- and the record size is reported (all-diffuse
+    flat scenes: one weight per view; glossy: result + BSDF value per view)."""
+    torch = _torch()
+    s = amvpt_mod.load_file(scene, res=16, spp=16)
+    sd, vd, p = s.describe(0, 0, 0)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    cnt = amvpt_mod.Counters()
+    amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), counters=cnt)
+    assert cnt.record_bytes == 80 + (4 if compact else 32) * G
+    assert cnt.nonfinite_samples == 0 and cnt.negative_samples == 0
+    assert cnt.view_splats > 0
