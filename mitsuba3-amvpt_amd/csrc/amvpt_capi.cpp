@@ -533,8 +533,6 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     sc->n_prims = (uint32_t) bprims.size();
     sc->all_diffuse = d->bsdf_count > 0;
     for (uint32_t i = 0; i < d->bsdf_count; ++i) sc->all_diffuse = sc->all_diffuse && d->bsdfs[i].type == AMVPT_BSDF_DIFFUSE;
-    for (uint32_t i = 0; i < d->shape_count; ++i)
-        sc->shading_normals = sc->shading_normals || (d->shapes[i].type == AMVPT_SHAPE_MESH && d->shapes[i].normals);
     std::vector<DScene> one(1, D);
     if ((st = upload(one.data(), sizeof(DScene), &sc->dev_scene_struct)) != AMVPT_OK) {
         amvpt_scene_destroy(sc);

@@ -591,13 +591,43 @@ constexpr int kWinW = AMVPT_WIN_W, kWinH = AMVPT_WIN_H, kMaxWaves = 16, kMaxFoot
 constexpr int kSplatSuper = 1024;   /* lanes per splat super-block (see slot_lane) */
 constexpr int kSplatBlock = AMVPT_SPLAT_BLOCK;   /* threads per splat block (see slot_lane) */
 constexpr int kWinCells = kWinW * kWinH;
+/*
+ * Window cell format.  AMVPT_WIN_FIXED = 1 (default): signed 32.32 fixed point in an int64 word,
+ * accumulated with ds_add_u64 -- 9.7 lane-ops/clk/CU against 7.5 for ds_add_f64 on gfx950
+ * (tools/ubench_lds.hip, 8-B stride; profiles/r02a_ubench.log).  Integer adds are exact and
+ * order-independent, so a block's window sum no longer depends on the order of its adds; each
+ * contribution is truncated to 2^-32 (~2e-10, far below the f32 film's resolution at the film's
+ * scale).  Samples with a non-finite channel or one of magnitude >= 2^20 bypass the window
+ * (direct global float atomics), so a cell sum stays far from int64 overflow and NaN/Inf still
+ * reach the film as in the reference.  AMVPT_WIN_FIXED = 0: fp64 cells with ds_add_f64.
+ */
+#ifndef AMVPT_WIN_FIXED
+#define AMVPT_WIN_FIXED 1
+#endif
+#if AMVPT_WIN_FIXED
+typedef long long WinT;
+#else
+typedef double WinT;
+#endif
+constexpr float kFixMax = 1048576.f;   /* 2^20 */
+/* round toward zero of x * 2^32, |x| < 2^31 (every step exact but the final truncation) */
+AD long long to_fixed(float x) {
+    const float a = fabsf(x) * 4294967296.f;
+    const float hf = truncf(a * 2.3283064365386963e-10f);
+    const uint32_t hi = (uint32_t) hf;
+    const uint32_t lo = (uint32_t) fmadd(-hf, 4294967296.f, a);
+    const long long u = (long long) (((unsigned long long) hi << 32) | lo);
+    return x < 0.f ? -u : u;
+}
+AD float from_fixed(long long q) { return (float) ((double) q * 2.3283064365386963e-10); }
+
 template <int C> struct SplatLds {
-    double win[kWinCells * C];              /* channel k of cell c at win[k * plane + c] */
+    WinT win[kWinCells * C];                /* channel k of cell c at win[k * plane + c] */
     alignas(16) int bb[2][kMaxWaves][4];
 };
 
 template <int C> AD void splat_lds_init(SplatLds<C> &L) {
-    for (int c = threadIdx.x; c < kWinCells * C; c += blockDim.x) L.win[c] = 0.0;
+    for (int c = threadIdx.x; c < kWinCells * C; c += blockDim.x) L.win[c] = 0;
     __syncthreads();
 }
 
@@ -657,6 +687,24 @@ AD int wave_max(int v) {
 AD void lds_add64(double *p, double v) {
     (void) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+/* ds_add_u64, result unused; one window contribution in the cell format */
+AD void lds_add64(long long *p, long long v) {
+    (void) __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(p), (unsigned long long) v, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+AD void win_add(double *p, float x) { lds_add64(p, (double) x); }
+AD void win_add(long long *p, float x) { lds_add64(p, to_fixed(x)); }
+/* may the sample go through the window?  (fixed point: finite and below 2^20 in every channel) */
+template <int C> AD bool win_fits(const float *vals) {
+#if AMVPT_WIN_FIXED
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < C; ++k) ok = ok && fabsf(vals[k]) < kFixMax;
+    return ok;
+#else
+    return true;
+#endif
+}
 
 /* The block's window: union of the active footprints, clamped to kWinW x kWinH. */
 struct Win { int bx0, by0, ww, wh, rs; };   /* rs: LDS row stride (cells) >= ww */
@@ -708,18 +756,24 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
     const int rowlen = w.ww * C;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
-    double *win = L.win;
+    WinT *win = L.win;
     const int n_elems = w.ww * w.wh * C;                    /* touched film floats (rows of ww cells) */
     for (int e = threadIdx.x; e < n_elems; e += blockDim.x) {
         int cy = (int) ((float) e * inv_rowlen);            /* e < 2^24: off by at most one */
         cy -= (cy * rowlen > e) ? 1 : 0;
         cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
         const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
-        double *src = win + k * plane + cy * w.rs + cx;
-        const double d = *src;
+        WinT *src = win + k * plane + cy * w.rs + cx;
+        const WinT d = *src;
+#if AMVPT_WIN_FIXED
+        if (d != 0) {
+            *src = 0;
+            const float v = from_fixed(d);
+#else
         if (__double_as_longlong(d) != 0ll) {
             *src = 0.0;
             const float v = (float) d;
+#endif
             if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + (size_t) cy * P.W * C + r, v);
         }
     }
@@ -734,9 +788,9 @@ AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, c
     const bool in_win = cx0 >= wn.bx0 && cy0 >= wn.by0 && f.x0 + f.nx <= wn.bx0 + wn.ww && f.y0 + f.ny <= wn.by0 + wn.wh;
     /* cells per footprint side: uniform over the call (filter radius and method only) */
     const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
-    if (in_win && cnt <= kMaxFoot) {
+    if (in_win && cnt <= kMaxFoot && win_fits<C>(vals)) {
         /* straight-line cnt x cnt cells; clipped cells are masked off (no retry, no branch body) */
-        double *const c0 = L.win + ((f.y0 - wn.by0) * wn.rs + (f.x0 - wn.bx0));
+        WinT *const c0 = L.win + ((f.y0 - wn.by0) * wn.rs + (f.x0 - wn.bx0));
 #pragma unroll
         for (int ys = 0; ys < kMaxFoot; ++ys) {
             if (ys >= cnt) break;
@@ -746,10 +800,10 @@ AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, c
                 if (xs >= cnt) break;
                 if (rok && xs < f.nx && f.x0 + xs >= 0) {
                     const float w = wx[xs] * wy[ys];
-                    double *const cp = c0 + ys * wn.rs + xs;
+                    WinT *const cp = c0 + ys * wn.rs + xs;
 #pragma unroll
                     for (int k = 0; k < C; ++k)
-                        if (!(AMVPT_ATTR_SKIP & 1)) lds_add64(cp + k * plane, (double) (P.box ? vals[k] : vals[k] * w));
+                        if (!(AMVPT_ATTR_SKIP & 1)) win_add(cp + k * plane, P.box ? vals[k] : vals[k] * w);
                 }
             }
         }
@@ -1519,6 +1573,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         C3 Bv = c3(0.f);                 /* kDiff: BSDF value of every indirect view */
         f3 hp = mk(0.f, 0.f, 0.f);       /* primary hit point (reprojection in the splat) */
         bool records_done = false, reuse_l = false, direct_l = false;
+        uint32_t nf_bits = 0, smask = 0;   /* kDiff: non-finite emis_mis channels, wi_k.z > 0 views */
 
         /* ---- sample_multi (mvpath_multi.h:130-369) ---- */
         bool valid_ray = false, adapt_mask = false;
@@ -1574,17 +1629,15 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 vmask |= p_hit ? 1u : 0u;
                 imask |= p_hit ? 1u : 0u;
                 const f3 wo_r0 = reflect_l(si.wi);
+                uint32_t wpos = p_face ? 1u : 0u;   /* kDiff: bit k = (wi_k.z > 0) */
                 if (!kDiff) {
                     VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
                     VSF(F_PDFM, 0) = bd.diffuse ? 1.f : (P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
                                                                    : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, si.wi, wo_r0, p_hit));
                 }
-                /* view k's wi.  kDiff runs only on scenes without shading normals: there a valid
-                 * view k sees the face the primary sees (sensors_visible), so sign(wi_k.z) =
-                 * sign(wi.z) and diffuse eval/pdf (which read wi only through that sign) give the
-                 * primary's values -- one BSDF value per lane instead of one per view. */
+                /* view k's wi (kDiff: diffuse eval / pdf read wi only through the sign of its z) */
                 auto wi_of = [&](int k) -> f3 {
-                    if (kDiff) return si.wi;
+                    if (kDiff) return k == 0 ? si.wi : mk(0.f, 0.f, ((wpos >> k) & 1u) ? 1.f : -1.f);
                     return mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
                 };
                 /* pdf_Mat of view k toward view 0 (tv_pdf, camera_selection) */
@@ -1611,6 +1664,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                                                 : bsdf_pdf(S.bsdfs, b, CTX_GLOSSY, wik, wor, valid);
                         VSF(F_PDFM, k) = pdfM;
                         pdf_Mat = mat_pdf(wik, pdfM, valid);
+                    } else {
+                        wpos |= wik.z > 0.f ? (1u << k) : 0u;
                     }
                     float J = r.Jp * iJp0;
                     float pdf_J = J > 1.f ? rcp(J) : J;
@@ -1642,14 +1697,25 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 direct_pdf /= n_direct;
                 const float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
                 const C3 emis_mis = em_w * mis_em;
-                /* kDiff lane values: slot 0's result, a valid view's direct light, the indirect
-                 * views' BSDF value and pdf (the same for every view, see wi_of) */
+                /* kDiff lane values.  A diffuse eval sees wi only through sign(wi.z) and is zero
+                 * for wi.z <= 0, so every view's value is one of two per lane: the direct light
+                 * of a valid view k >= 1 is Dp (wi_k.z > 0) or cfma(0, emis_mis, 0) (= 0, or NaN
+                 * where emis_mis is not finite: bit 8 + c of the lane flags), and an indirect view
+                 * (pdf > 0, so wi_k.z > 0) has Bv = eval(+z, wo) with pdf bp_d. */
                 float bp_d = 0.f;
                 if (kDiff) {
                     R0 = emitted;
                     if (active_em && (vmask & 1u)) R0 = cfma(bsdf_val, emis_mis, emitted);
-                    if (active_em) Dp = cfma(bsdf_val, emis_mis, c3(0.f));
-                    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, bsmp.wo, true, Bv, bp_d);
+                    if (active_em) {
+                        C3 ep;
+                        float epd;
+                        bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, mk(0.f, 0.f, 1.f), wo, true, ep, epd);
+                        Dp = cfma(ep, emis_mis, c3(0.f));
+                        nf_bits = (finite_(emis_mis.r) ? 0u : 1u) | (finite_(emis_mis.g) ? 0u : 2u) |
+                                  (finite_(emis_mis.b) ? 0u : 4u);
+                    }
+                    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, mk(0.f, 0.f, 1.f), bsmp.wo, true, Bv, bp_d);
+                    smask = wpos;
                 }
                 /* ---- per view: mis_weights (mvpath_multi.h:466-523), direct light and
                  *      the multi-view mixture pdf (mvpath_multi.h:245-317) ---- */
@@ -1697,7 +1763,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     C3 res = c3(0.f), bv = c3(0.f);
                     float bp;
                     if (kDiff) {
-                        bp = valid ? bp_d : 0.f;
+                        bp = (valid && ((wpos >> k) & 1u)) ? bp_d : 0.f;
                     } else {
                         /* result: emission (slot 0) + direct light through this view's BSDF value */
                         res = csel(k == 0, emitted, c3(0.f));
@@ -1782,11 +1848,12 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             w0 = 0.f;
         }
         const uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) |
-                                (should_mis ? LF_MIS : 0u) | (reuse_l ? LF_REUSE : 0u) | (direct_l ? LF_DIRECT : 0u);
+                                (should_mis ? LF_MIS : 0u) | (reuse_l ? LF_REUSE : 0u) | (direct_l ? LF_DIRECT : 0u) |
+                                (nf_bits << 8) | (smask << 16);
         B.lrec[0][slot] = make_float4(R0.r, R0.g, R0.b, pdfW);
         B.lrec[1][slot] = make_float4(Dp.r, Dp.g, Dp.b, bitsf(lflags));
-        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(vmask));
-        B.lrec[3][slot] = make_float4(hp.x, hp.y, hp.z, bitsf(imask));
+        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(vmask | (imask << 16)));
+        B.lrec[3][slot] = make_float4(hp.x, hp.y, hp.z, 0.f);
         /* slot 0 (generic: its bsdf value rides in L2), and the views the MIS loop did not write */
         put_view(0, w0, R0, Bv, (vmask & 1u ? VF_VALID : 0u) | (imask & 1u ? VF_INDIRECT : 0u));
         if (!records_done) {
@@ -1819,7 +1886,11 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, const DV
     const uint32_t n = P.chunk_n;
     float4 l0 = make_float4(0.f, 0.f, 0.f, 0.f), l1 = l0, l2 = l0, l3 = l0, lo = l0;
     if (ok) { l0 = B.lrec[0][slot]; l1 = B.lrec[1][slot]; l2 = B.lrec[2][slot]; l3 = B.lrec[3][slot]; lo = B.lane_out[slot]; }
-    const uint32_t lflags = fbits(l1.w), vmask = fbits(l2.w), imask = fbits(l3.w);
+    const uint32_t lflags = fbits(l1.w), vmask = fbits(l2.w) & 0xffffu, imask = fbits(l2.w) >> 16;
+    const uint32_t smask = lflags >> 16;
+    const float qnan = __builtin_nanf("");
+    /* cfma(0, emis_mis, 0) of a valid view whose wi.z <= 0 (kDiff, see k_mv_primary) */
+    const C3 Dn = {(lflags & 0x100u) ? qnan : 0.f, (lflags & 0x200u) ? qnan : 0.f, (lflags & 0x400u) ? qnan : 0.f};
     const float pdfW = l0.w;
     const C3 R0 = C3{l0.x, l0.y, l0.z}, Dp = C3{l1.x, l1.y, l1.z}, Bv = C3{l2.x, l2.y, l2.z};
     const f3 hp = mk(l3.x, l3.y, l3.z);
@@ -1872,7 +1943,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, const DV
                 weight = vw[o];
                 valid = (vmask >> k) & 1u;
                 if (mis) {
-                    result = k == 0 ? R0 : csel(direct && valid, Dp, c3(0.f));
+                    result = k == 0 ? R0 : csel(direct && valid, csel((smask >> k) & 1u, Dp, Dn), c3(0.f));
                     if ((imask >> k) & 1u) result = cfma(Bv * pdfW, indirect, result);
                 } else {
                     result = res0;
@@ -2280,7 +2351,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
     const uint64_t span = lane_end - lane_begin;
     const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
-    const bool diff_rec = scene->all_diffuse && !scene->shading_normals && diffuse_spec;   /* compact view records */
+    const bool diff_rec = scene->all_diffuse && diffuse_spec && G <= 16;   /* kDiff instances, compact view records */
     const size_t per_lane = 12 * 16 + 32 + 64 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8;
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */

@@ -16,8 +16,6 @@ struct amvpt_scene {
     uint32_t n_nodes = 0, n_prims = 0;
     bool has_spheres = false;   /* the brute-force suffix walks take their sphere-free instances otherwise */
     bool all_diffuse = false;   /* every BSDF is plain `diffuse`: kernels take their kDiff instances */
-    bool shading_normals = false; /* some mesh has vertex normals (shading frame != geometric frame):
-                                   * the kDiff instances need flat shading (k_mv_primary) */
     int device = 0;
 };
 
