@@ -93,6 +93,7 @@ struct KParams {
     uint64_t chunk_begin;
     uint32_t chunk_n;
     uint32_t record;      /* write per-lane splat records */
+    uint32_t row_splat;   /* row-reduced splat (row_put): lanes in pixel-major order, see slot_lane */
 };
 
 /* SoA streams of one chunk */
@@ -610,24 +611,26 @@ typedef long long WinT;
 typedef double WinT;
 #endif
 constexpr float kFixMax = 1048576.f;   /* 2^20 */
-/* round toward zero of x * 2^32, |x| < 2^31 (every step exact but the final truncation) */
+/* floor(x * 2^32) as a 64-bit two's-complement word, |x| < 2^31: the high dword is floor(x), the
+ * low dword the fraction x - floor(x) (exact) times 2^32, truncated (clamped below 2^32, where a
+ * tiny negative x rounds the fraction up to 1) -- six VALU ops, no 64-bit arithmetic */
 AD long long to_fixed(float x) {
-    const float a = fabsf(x) * 4294967296.f;
-    const float hf = truncf(a * 2.3283064365386963e-10f);
-    const uint32_t hi = (uint32_t) hf;
-    const uint32_t lo = (uint32_t) fmadd(-hf, 4294967296.f, a);
-    const long long u = (long long) (((unsigned long long) hi << 32) | lo);
-    return x < 0.f ? -u : u;
+    const float hf = floorf(x);
+    const uint32_t lo = (uint32_t) fminf((x - hf) * 4294967296.f, 4294967040.f);
+    const uint32_t hi = (uint32_t) (int32_t) hf;
+    return (long long) (((unsigned long long) hi << 32) | lo);
 }
 AD float from_fixed(long long q) { return (float) ((double) q * 2.3283064365386963e-10); }
 
+/* channel planes of the window are `plane` cells apart, plane <= kWinPlane (see window_bbox) */
+constexpr int kWinPlane = kWinCells + 32;
 template <int C> struct SplatLds {
-    WinT win[kWinCells * C];                /* channel k of cell c at win[k * plane + c] */
+    WinT win[kWinPlane * C];                /* channel k of cell c at win[k * plane + c] */
     alignas(16) int bb[2][kMaxWaves][4];
 };
 
 template <int C> AD void splat_lds_init(SplatLds<C> &L) {
-    for (int c = threadIdx.x; c < kWinCells * C; c += blockDim.x) L.win[c] = 0;
+    for (int c = threadIdx.x; c < kWinPlane * C; c += blockDim.x) L.win[c] = 0;
     __syncthreads();
 }
 
@@ -707,9 +710,9 @@ template <int C> AD bool win_fits(const float *vals) {
 }
 
 /* The block's window: union of the active footprints, clamped to kWinW x kWinH. */
-struct Win { int bx0, by0, ww, wh, rs; };   /* rs: LDS row stride (cells) >= ww */
+struct Win { int bx0, by0, ww, wh, rs, plane; };   /* rs: LDS row stride (cells) >= ww; plane >= rs * wh */
 template <int C>
-AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, int y1, int win_rs) {
+AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, int y1, int win_rs, bool row_splat) {
     int lx = act ? cx0 : 0x7fffffff, ly = act ? cy0 : 0x7fffffff;
     int hx = act ? x1 : (int) 0x80000000, hy = act ? y1 : (int) 0x80000000;
     lx = wave_min(lx); ly = wave_min(ly); hx = wave_max(hx); hy = wave_max(hy);
@@ -744,6 +747,11 @@ AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, 
         const int r = (w.ww & ~31) + win_rs, r2 = r >= w.ww ? r : r + 32;
         w.rs = r2 <= kWinW ? r2 : w.ww;
     }
+    /* row_put's atomics of one 16-lane row hit 4 channels x 2 row sets (3 rows apart) x 2 column
+     * sets (3 cells apart): with rs % 32 == 16 and plane % 32 == 4 their cell indices are 16
+     * distinct residues mod 32, so the 16 lanes of an LDS cycle use 16 distinct bank pairs */
+    w.plane = w.rs * w.wh;
+    if (row_splat) w.plane += (36 - (w.plane & 31)) & 31;
     return w;
 }
 
@@ -752,7 +760,7 @@ AD Win window_bbox(SplatLds<C> &L, int buf, bool act, int cx0, int cy0, int x1, 
 template <int C>
 AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w) {
     __syncthreads();
-    const int plane = w.rs * w.wh;
+    const int plane = w.plane;
     const int rowlen = w.ww * C;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
@@ -784,7 +792,7 @@ template <int C>
 AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, const Foot &f, const float *wx,
                  const float *wy, const float *vals, bool coalesce, unsigned long long *fallback) {
     const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
-    const int plane = wn.rs * wn.wh;
+    const int plane = wn.plane;
     const bool in_win = cx0 >= wn.bx0 && cy0 >= wn.by0 && f.x0 + f.nx <= wn.bx0 + wn.ww && f.y0 + f.ny <= wn.by0 + wn.wh;
     /* cells per footprint side: uniform over the call (filter radius and method only) */
     const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
@@ -836,6 +844,111 @@ AD void foot_weights(const KParams &P, const Foot &f, float *wx, float *wy) {
 }
 
 /*
+ * Row-reduced put (KParams::row_splat, RGBW films).  Lanes run pixel-major (slot_lane is the
+ * identity), so a DPP row of 16 lanes holds 16 samples of one pixel: for view 0 (coalesced
+ * method) the 16 footprints are the same 5 x 5 cells, and a reprojected view's 16 footprints
+ * usually fall inside one 6 x 6 box.  When every active footprint of a row lies in the window,
+ * the union box of the row is at most 6 x 6 and every value is finite and below kFixMax, the
+ * row adds its 16 footprints as ONE reduced 6 x 6 x 4 block: every lane forms its products
+ * value_c * (wx * wy) (the reference's per-cell products, imageblock.cpp:265-558) for all 36
+ * union cells (zero weight outside its own footprint), and a 4-step reduce-scatter over the row
+ * (DPP quad xor 1, quad xor 2, row rotate 4, row rotate 8) leaves each lane the row's sum for 9
+ * cells of one channel -- 9 ds_add_u64 per lane and view instead of 64 (reprojected) or 100
+ * (coalesced).  The products are summed in f32 before the window (the reference's f32 film
+ * sums them in some atomic order as well).  Other rows take the per-lane path (foot_add).
+ *
+ * Ownership: lane bits b0 b1 pick the channel (b0 + 2 b1), b2 the row set (rows 0-2 or 3-5),
+ * b3 the column set.  Steps 1-2 and 3 read their partner's values in a lane-permuted order
+ * chosen once per sample (channel operands, rows), step 4 selects its column halves.
+ */
+enum : int { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128 };
+template <int kCtrl> AD float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xf, 0xf, false));
+}
+template <int kCtrl> AD int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, false); }
+/* min / max over the lane's 16-lane row (every lane of the wave active) */
+AD int row_min(int v) {
+    v = min(v, dpp_i<DPP_XOR1>(v)); v = min(v, dpp_i<DPP_XOR2>(v));
+    v = min(v, dpp_i<DPP_ROR4>(v)); return min(v, dpp_i<DPP_ROR8>(v));
+}
+AD int row_max(int v) {
+    v = max(v, dpp_i<DPP_XOR1>(v)); v = max(v, dpp_i<DPP_XOR2>(v));
+    v = max(v, dpp_i<DPP_ROR4>(v)); return max(v, dpp_i<DPP_ROR8>(v));
+}
+/* filter weight of film cell `cell` for a footprint starting at x0 with argument r, zero outside
+ * the footprint's cells [lo, hi) -- inside it eval(r + (cell - x0)), the reference's argument */
+AD float union_weight(const KParams &P, float r, int x0, int cell, int lo, int hi) {
+    const float w = gaussian_eval(P.filt, r + (float) (cell - x0));
+    return (cell >= lo && cell < hi) ? w : 0.f;
+}
+
+template <int C>
+AD void row_put(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, const Foot &f, bool act,
+                const float *vals, bool coalesce, unsigned long long *fallback) {
+    const int x0c = max(f.x0, 0), y0c = max(f.y0, 0), x1 = f.x0 + f.nx, y1 = f.y0 + f.ny;
+    const bool inw = x0c >= wn.bx0 && y0c >= wn.by0 && x1 <= wn.bx0 + wn.ww && y1 <= wn.by0 + wn.wh;
+    const bool good = inw && win_fits<C>(vals);
+    constexpr int kBig = 0x3fffffff;
+    const int ux0 = row_min(act ? x0c : kBig), uy0 = row_min(act ? y0c : kBig);
+    const int ux1 = row_max(act ? x1 : -kBig), uy1 = row_max(act ? y1 : -kBig);
+    const int bad = row_max((act && !good) ? 1 : 0);
+    const bool fast = C == 4 && ux1 > ux0 && bad == 0 && ux1 - ux0 <= 6 && uy1 - uy0 <= 6;
+    if (fast) {
+        const int lane = (int) (__lane_id() & 15u);
+        const int b0 = lane & 1, b1 = (lane >> 1) & 1, b2 = (lane >> 2) & 1, b3 = (lane >> 3) & 1;
+        float v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = act ? vals[c] : 0.f;
+        auto pick = [&](int c) { return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3]; };
+        /* K1: the channel this lane ends with, K2: kept in step 1 and handed on in step 2, S1 / S2:
+         * handed to the xor-1 partner in step 1 (whose K1 / K2 they are) */
+        const float K1 = pick(b0 + 2 * b1), K2 = pick(b0 + 2 * (1 - b1));
+        const float S1 = pick(1 - b0 + 2 * b1), S2 = pick(1 - b0 + 2 * (1 - b1));
+        float wx[6], wy[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) wx[c] = act ? union_weight(P, f.rx, f.x0, ux0 + c, x0c, x1) : 0.f;
+        /* row position r holds union row (r + 3 b2) mod 6 */
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const int row = r + 3 * b2 - (r + 3 * b2 >= 6 ? 6 : 0);
+            wy[r] = act ? union_weight(P, f.ry, f.y0, uy0 + row, y0c, y1) : 0.f;
+        }
+        WinT *const wch = L.win + (b0 + 2 * b1) * wn.plane;
+        /* one row pair (r, r + 3) at a time: steps 1-3 give z[c] (row set of b2, all 6 columns),
+         * step 4 the 3 columns of b3 -> 3 window adds; few values live at once */
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            float z[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                float y[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float w = wx[c] * wy[r + 3 * h];
+                    const float xa = K1 * w + dpp_f<DPP_XOR1>(S1 * w);
+                    const float xb = K2 * w + dpp_f<DPP_XOR1>(S2 * w);
+                    y[h] = xa + dpp_f<DPP_XOR2>(xb);
+                }
+                z[c] = y[0] + dpp_f<DPP_ROR4>(y[1]);
+            }
+            const int row = r + 3 * b2;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float keep = b3 ? z[c + 3] : z[c], send = b3 ? z[c] : z[c + 3];
+                const float u = keep + dpp_f<DPP_ROR8>(send);
+                const int col = c + 3 * b3;
+                if (ux0 + col < ux1 && uy0 + row < uy1 && !(AMVPT_ATTR_SKIP & 1))
+                    win_add(wch + (uy0 + row - wn.by0) * wn.rs + (ux0 + col - wn.bx0), u);
+            }
+        }
+    } else if (act) {
+        float wx[kMaxFoot], wy[kMaxFoot];
+        foot_weights(P, f, wx, wy);
+        foot_add<C>(P, film, L, wn, f, wx, wy, vals, coalesce, fallback);
+    }
+}
+
+/*
  * Block-cooperative put into window buffer `buf`.  Cells xs in [0, nx) x ys in
  * [0, ny) of the footprint with x0 + xs >= 0 and y0 + ys >= 0 are accumulated (the
  * coalesced footprint may start left/above the film).  Weight of a cell =
@@ -849,8 +962,11 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
     if (valid) f = footprint(P, px, py, coalesce);
     const bool act = valid && f.ok;
-    const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny, (int) P.win_rs);
-    if (act) {
+    const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny, (int) P.win_rs,
+                               P.row_splat != 0);
+    if (C == 4 && P.row_splat) {
+        row_put<C>(P, film, L, wn, f, act, vals, coalesce, fallback);
+    } else if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
         foot_add<C>(P, film, L, wn, f, wx, wy, vals, coalesce, fallback);
@@ -872,6 +988,7 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
  */
 constexpr int kSplatSplit = kSplatSuper / kSplatBlock;
 AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
+    if (P.row_splat) return slot;   /* pixel-major: a 16-lane row = 16 samples of one pixel (row_put) */
     const uint32_t super = slot / (uint32_t) kSplatSuper, within = slot % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
     const uint32_t remain = P.chunk_n > base ? P.chunk_n - base : 0;
@@ -885,6 +1002,7 @@ AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
 }
 /* inverse of slot_lane */
 AD uint32_t lane_slot(const KParams &P, uint32_t lane) {
+    if (P.row_splat) return lane;
     const uint32_t super = lane / (uint32_t) kSplatSuper, off = lane % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
     const uint32_t remain = P.chunk_n > base ? P.chunk_n - base : 0;
@@ -1876,8 +1994,13 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
 /* k_splat_multi<G>: indirect accumulation + splats (mvpath_multi.h:343-368,44-76) */
 /* ------------------------------------------------------------------ */
 
+/* waves per SIMD the register allocation must allow: the 30-KB window admits 5 blocks (20 waves)
+ * per CU */
+#ifndef AMVPT_SPLAT_WAVES
+#define AMVPT_SPLAT_WAVES 4
+#endif
 template <int G, int C, bool kDiff>
-__global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, const DView *V, Bufs B) {
+__global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(KParams P, const DView *V, Bufs B) {
     __shared__ SplatLds<C> L;
     splat_lds_init(L);
     const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
@@ -1919,6 +2042,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_multi(KParams P, const DV
     const float *const vw = reinterpret_cast<const float *>(B.vrec);
     const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) G * n;
     unsigned long long splats = 0, fallback = 0, nonfinite = 0, negative = 0;
+#pragma unroll 1
     for (int k = 0; k < G; ++k) {
         const size_t o = (size_t) k * n + slot;
         float weight = 0.f;
@@ -2328,6 +2452,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     }
     P.range_begin = lane_begin;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
+    /* row-reduced splat (row_put): RGBW film, Gaussian filter, >= 16 samples per pixel and pass
+     * (a 16-lane row = one pixel); AMVPT_ROW_SPLAT=0 keeps the per-lane splat (A/B) */
+    {
+        const char *e = std::getenv("AMVPT_ROW_SPLAT");
+        const bool on = !(e && e[0] == '0');
+        P.row_splat = (on && P.C == 4 && !P.box && P.pow2 && spp_pp >= 16) ? 1u : 0u;
+    }
 
     /* views to device (tiny) */
     std::vector<DView> hv(Pp.n_views);
