@@ -31,6 +31,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 
 #include "dbsdf.h"
 #include "internal.h"
@@ -624,10 +625,32 @@ AD float from_fixed(long long q) { return (float) ((double) q * 2.32830643653869
 
 /* channel planes of the window are `plane` cells apart, plane <= kWinPlane (see window_bbox) */
 constexpr int kWinPlane = kWinCells + 32;
+/*
+ * AMVPT_WAVE_WIN = 1: the row-reduced splat (row_put) gives every wave a window of its own
+ * (kWaveWinW x kWaveWinH cells): a wave's bounding box, adds and flush need no block barrier
+ * (LDS operations of one wave complete in order).  A wave = 4 pixels x 16 samples, whose
+ * footprints span ~8 x 5 cells (view 0) to ~10 x 6 (reprojected views).
+ */
+#ifndef AMVPT_WAVE_WIN
+#define AMVPT_WAVE_WIN 1
+#endif
+#ifndef AMVPT_WAVE_WIN_W
+#define AMVPT_WAVE_WIN_W 32
+#endif
+constexpr int kWaveWinW = AMVPT_WAVE_WIN_W, kWaveWinH = 6, kWavePlane = kWaveWinW * kWaveWinH + 32;
+constexpr int kSplatWaves = AMVPT_SPLAT_BLOCK / 64;
 template <int C> struct SplatLds {
     WinT win[kWinPlane * C];                /* channel k of cell c at win[k * plane + c] */
     alignas(16) int bb[2][kMaxWaves][4];
 };
+/* the wave windows of a row-splat block: wave w's window at win[w * kWavePlane * C] */
+template <int C> struct WaveLds {
+    WinT win[kSplatWaves * kWavePlane * C];
+};
+template <int C> AD void wave_lds_init(WaveLds<C> &L) {
+    for (int c = threadIdx.x; c < kSplatWaves * kWavePlane * C; c += blockDim.x) L.win[c] = 0;
+    __syncthreads();
+}
 
 template <int C> AD void splat_lds_init(SplatLds<C> &L) {
     for (int c = threadIdx.x; c < kWinPlane * C; c += blockDim.x) L.win[c] = 0;
@@ -788,8 +811,10 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
 }
 
 /* one footprint's cells straight into the window (or the film when it does not fit) */
-template <int C>
-AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, const Foot &f, const float *wx,
+/* kRolled: the window loop is not unrolled (row_put's rare per-lane path: an unrolled 5 x 5 x C
+ * body would set the register allocation of the whole splat kernel) */
+template <int C, bool kRolled = false>
+AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, const float *wx,
                  const float *wy, const float *vals, bool coalesce, unsigned long long *fallback) {
     const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
     const int plane = wn.plane;
@@ -798,8 +823,8 @@ AD void foot_add(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, c
     const int cnt = P.box ? 1 : (coalesce ? 2 * (int) ceilf(P.filt.radius - .5f) + 1 : (int) ceilf(2.f * P.filt.radius));
     if (in_win && cnt <= kMaxFoot && win_fits<C>(vals)) {
         /* straight-line cnt x cnt cells; clipped cells are masked off (no retry, no branch body) */
-        WinT *const c0 = L.win + ((f.y0 - wn.by0) * wn.rs + (f.x0 - wn.bx0));
-#pragma unroll
+        WinT *const c0 = wbase + ((f.y0 - wn.by0) * wn.rs + (f.x0 - wn.bx0));
+#pragma unroll(kRolled ? 1 : kMaxFoot)
         for (int ys = 0; ys < kMaxFoot; ++ys) {
             if (ys >= cnt) break;
             const bool rok = ys < f.ny && f.y0 + ys >= 0;
@@ -861,11 +886,11 @@ AD void foot_weights(const KParams &P, const Foot &f, float *wx, float *wy) {
  * b3 the column set.  Steps 1-2 and 3 read their partner's values in a lane-permuted order
  * chosen once per sample (channel operands, rows), step 4 selects its column halves.
  */
-enum : int { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128 };
+enum : int { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_XOR3 = 0x1B, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128 };
 template <int kCtrl> AD float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xf, 0xf, true));
 }
-template <int kCtrl> AD int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, false); }
+template <int kCtrl> AD int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, true); }
 /* min / max over the lane's 16-lane row (every lane of the wave active) */
 AD int row_min(int v) {
     v = min(v, dpp_i<DPP_XOR1>(v)); v = min(v, dpp_i<DPP_XOR2>(v));
@@ -883,8 +908,8 @@ AD float union_weight(const KParams &P, float r, int x0, int cell, int lo, int h
 }
 
 template <int C>
-AD void row_put(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, const Foot &f, bool act,
-                const float *vals, bool coalesce, unsigned long long *fallback) {
+AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, bool act,
+                    const float *vals, bool coalesce, unsigned long long *fallback) {
     const int x0c = max(f.x0, 0), y0c = max(f.y0, 0), x1 = f.x0 + f.nx, y1 = f.y0 + f.ny;
     const bool inw = x0c >= wn.bx0 && y0c >= wn.by0 && x1 <= wn.bx0 + wn.ww && y1 <= wn.by0 + wn.wh;
     const bool good = inw && win_fits<C>(vals);
@@ -895,39 +920,44 @@ AD void row_put(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, co
     const bool fast = C == 4 && ux1 > ux0 && bad == 0 && ux1 - ux0 <= 6 && uy1 - uy0 <= 6;
     if (fast) {
         const int lane = (int) (__lane_id() & 15u);
-        const int b0 = lane & 1, b1 = (lane >> 1) & 1, b2 = (lane >> 2) & 1, b3 = (lane >> 3) & 1;
+        const int b2 = (lane >> 2) & 1, b3 = (lane >> 3) & 1, ch = lane & 3;
         float v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = act ? vals[c] : 0.f;
         auto pick = [&](int c) { return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3]; };
-        /* K1: the channel this lane ends with, K2: kept in step 1 and handed on in step 2, S1 / S2:
-         * handed to the xor-1 partner in step 1 (whose K1 / K2 they are) */
-        const float K1 = pick(b0 + 2 * b1), K2 = pick(b0 + 2 * (1 - b1));
-        const float S1 = pick(1 - b0 + 2 * b1), S2 = pick(1 - b0 + 2 * (1 - b1));
-        float wx[6], wy[6];
+        /* K: this lane's value of its channel; Bj: the value of this lane's channel at quad lane
+         * (lane ^ j), which hands over its own v[ch ^ j] */
+        const float K = pick(ch);
+        const float B1 = dpp_f<DPP_XOR1>(pick(ch ^ 1)), B2 = dpp_f<DPP_XOR2>(pick(ch ^ 2)),
+                    B3 = dpp_f<DPP_XOR3>(pick(ch ^ 3));
+        float wx[6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) wx[c] = act ? union_weight(P, f.rx, f.x0, ux0 + c, x0c, x1) : 0.f;
-        /* row position r holds union row (r + 3 b2) mod 6 */
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-            const int row = r + 3 * b2 - (r + 3 * b2 >= 6 ? 6 : 0);
-            wy[r] = act ? union_weight(P, f.ry, f.y0, uy0 + row, y0c, y1) : 0.f;
-        }
-        WinT *const wch = L.win + (b0 + 2 * b1) * wn.plane;
-        /* one row pair (r, r + 3) at a time: steps 1-3 give z[c] (row set of b2, all 6 columns),
-         * step 4 the 3 columns of b3 -> 3 window adds; few values live at once */
+        WinT *const wch = wbase + ch * wn.plane;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
+            /* row position r + 3 h holds union row r + 3 (h ^ b2); the quad shares b2 */
+            float Ky[2], B1y[2], B2y[2], B3y[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float wy = act ? union_weight(P, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1) : 0.f;
+                Ky[h] = K * wy;
+                B1y[h] = B1 * dpp_f<DPP_XOR1>(wy);
+                B2y[h] = B2 * dpp_f<DPP_XOR2>(wy);
+                B3y[h] = B3 * dpp_f<DPP_XOR3>(wy);
+            }
+            /* steps 1-2: the quad's sum of this lane's channel, sum_j v_j[ch] wy_j wx_j; step 3: plus
+             * the rotate-4 partner's quad sum of the other row half */
             float z[6];
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
                 float y[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const float w = wx[c] * wy[r + 3 * h];
-                    const float xa = K1 * w + dpp_f<DPP_XOR1>(S1 * w);
-                    const float xb = K2 * w + dpp_f<DPP_XOR1>(S2 * w);
-                    y[h] = xa + dpp_f<DPP_XOR2>(xb);
+                    float a = Ky[h] * wx[c];
+                    a = fmaf(dpp_f<DPP_XOR1>(wx[c]), B1y[h], a);
+                    a = fmaf(dpp_f<DPP_XOR2>(wx[c]), B2y[h], a);
+                    y[h] = fmaf(dpp_f<DPP_XOR3>(wx[c]), B3y[h], a);
                 }
                 z[c] = y[0] + dpp_f<DPP_ROR4>(y[1]);
             }
@@ -944,8 +974,80 @@ AD void row_put(const KParams &P, float *film, SplatLds<C> &L, const Win &wn, co
     } else if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
-        foot_add<C>(P, film, L, wn, f, wx, wy, vals, coalesce, fallback);
+        foot_add<C, true>(P, film, wbase, wn, f, wx, wy, vals, coalesce, fallback);
     }
+}
+
+/* min / max over the wave (every lane active): DPP within the rows, then the 4 row results */
+AD int wave_min_dpp(int v) {
+    v = row_min(v);
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+AD int wave_max_dpp(int v) {
+    v = row_max(v);
+    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+/* the wave's window flush: one global float atomic per touched film float, re-zeroing the
+ * window (wave-local, in LDS order after the wave's own adds) */
+template <int C>
+AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int rowlen = w.ww * C;
+    const int n_elems = rowlen * w.wh;
+    float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
+    for (int e = (int) __lane_id(); e < n_elems; e += 64) {
+        const int cy = e / rowlen, r = e - cy * rowlen, cx = r / C, k = r - cx * C;
+        WinT *src = win + k * w.plane + cy * w.rs + cx;
+        const WinT d = *src;
+#if AMVPT_WIN_FIXED
+        if (d != 0) {
+            *src = 0;
+            const float v = from_fixed(d);
+#else
+        if (__double_as_longlong(d) != 0ll) {
+            *src = 0.0;
+            const float v = (float) d;
+#endif
+            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + (size_t) cy * P.W * C + r, v);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+/* ImageBlock::put of a wave's samples through its own window (AMVPT_WAVE_WIN, row_splat) */
+template <int C>
+AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float py, const float *vals, bool valid,
+                 bool coalesce, unsigned long long *fallback) {
+    Foot f;
+    f.ok = false;
+    f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
+    if (valid) f = footprint(P, px, py, coalesce);
+    const bool act = valid && f.ok;
+    constexpr int kBig = 0x3fffffff;
+    const int bx0 = wave_min_dpp(act ? max(f.x0, 0) : kBig), by0 = wave_min_dpp(act ? max(f.y0, 0) : kBig);
+    const int bx1 = wave_max_dpp(act ? f.x0 + f.nx : -kBig), by1 = wave_max_dpp(act ? f.y0 + f.ny : -kBig);
+    if (bx1 <= bx0) return;   /* no active footprint in the wave (uniform) */
+    Win wn;
+    wn.bx0 = bx0; wn.by0 = by0;
+    wn.ww = min(bx1 - bx0, kWaveWinW);
+    wn.wh = min(by1 - by0, kWaveWinH);
+    wn.rs = wn.ww;
+    wn.plane = wn.ww * wn.wh;
+    /* row_put's bank spread (see window_bbox): rows 16 mod 32 apart, planes 4 mod 32 apart */
+    {
+        const int r2 = (wn.ww & ~31) + 16, r3 = r2 >= wn.ww ? r2 : r2 + 32;
+        if (r3 * wn.wh + 32 <= kWavePlane) wn.rs = r3;
+        wn.plane = wn.rs * wn.wh;
+        wn.plane += (36 - (wn.plane & 31)) & 31;
+        if (wn.plane > kWavePlane) { wn.rs = wn.ww; wn.plane = wn.ww * wn.wh; }
+    }
+    WinT *const win = L.win + (threadIdx.x >> 6) * (kWavePlane * C);
+    /* row_put reads the window through L.win: hand it this wave's window */
+    row_put_win<C>(P, film, win, wn, f, act, vals, coalesce, fallback);
+    wave_flush<C>(P, film, win, wn);
 }
 
 /*
@@ -965,11 +1067,11 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny, (int) P.win_rs,
                                P.row_splat != 0);
     if (C == 4 && P.row_splat) {
-        row_put<C>(P, film, L, wn, f, act, vals, coalesce, fallback);
+        row_put_win<C>(P, film, L.win, wn, f, act, vals, coalesce, fallback);
     } else if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
-        foot_add<C>(P, film, L, wn, f, wx, wy, vals, coalesce, fallback);
+        foot_add<C>(P, film, L.win, wn, f, wx, wy, vals, coalesce, fallback);
     }
     window_flush<C>(P, film, L, wn);
 }
@@ -1999,10 +2101,17 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
 #ifndef AMVPT_SPLAT_WAVES
 #define AMVPT_SPLAT_WAVES 4
 #endif
-template <int G, int C, bool kDiff>
+/* kRow: the row-reduced splat with wave windows (P.row_splat, RGBW), else the block window */
+template <int G, int C, bool kDiff, bool kRow>
 __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(KParams P, const DView *V, Bufs B) {
-    __shared__ SplatLds<C> L;
-    splat_lds_init(L);
+    __shared__ typename std::conditional<kRow, WaveLds<C>, SplatLds<C>>::type L;
+    if (kRow) wave_lds_init(reinterpret_cast<WaveLds<C> &>(L));
+    else splat_lds_init(reinterpret_cast<SplatLds<C> &>(L));
+    /* one put of this kernel's kind */
+    auto put = [&](float x, float y, const float *vals, bool valid, bool coalesce, int buf, unsigned long long *fb) {
+        if constexpr (kRow) wave_put<C>(P, B.film, L, x, y, vals, valid, coalesce, fb);
+        else block_put<C>(P, B.film, L, buf, x, y, vals, valid, coalesce, fb);
+    };
     const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
     const bool ok = slot < P.chunk_n;
     const uint32_t i = ok ? slot_lane(P, slot) : 0u;   /* chunk-local lane */
@@ -2091,12 +2200,12 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         if (P.debug) {
             if (k > 0) break; /* uniform: every thread breaks at k == 1 */
             pack_vals(P, c3(adapt_mask ? 1.f : 0.f), alpha, 1.f, vals);
-            block_put<C>(P, B.film, L, 0, x, y, vals, ok, true);
+            put(x, y, vals, ok, true, 0, nullptr);
             continue;
         }
         pack_vals(P, v, alpha, weight, vals);
         check_sample(P, vals, valid, nonfinite, negative);
-        block_put<C>(P, B.film, L, k & 1, x, y, vals, valid, k == 0, &fallback);
+        put(x, y, vals, valid, k == 0, k & 1, &fallback);
         splats += valid ? 1 : 0;
         if (ok && P.record) {
             float *rr = B.records + ((size_t) i * G + k) * 8;
@@ -2139,7 +2248,7 @@ void launch_shadow(int walk, dim3 grid, size_t lds, hipStream_t st, const KParam
 ;
 #endif
 
-#ifndef AMVPT_SHADOW_TU
+#if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_KERNEL_PROBE)
 /* ------------------------------------------------------------------ */
 /* Host orchestration                                                 */
 /* ------------------------------------------------------------------ */
@@ -2336,10 +2445,13 @@ static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStrea
 }
 template <int G>
 static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff) {
-    if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    const bool row = AMVPT_WAVE_WIN && P.row_splat && P.C == 4;
+    if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (diff && row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
 }
 
 typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
@@ -2750,5 +2862,5 @@ amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h,
     return AMVPT_OK;
 }
 
-#endif /* AMVPT_SHADOW_TU */
+#endif /* !AMVPT_SHADOW_TU && !AMVPT_KERNEL_PROBE */
 } // namespace amvpt

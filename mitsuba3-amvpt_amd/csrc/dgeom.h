@@ -288,21 +288,31 @@ template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray
     return sphere_hit(p, r, t);
 }
 
+/* closest-hit update of the brute-force walks: (t, scene-order index) as trace_closest */
+template <bool kSph> AD void brute_test(const DPrim &p, uint32_t pi, const Ray &ray, Hit &best, uint32_t &best_orig) {
+    float t, u, v;
+    if (prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v)) {
+        const uint32_t orig = ufirst(p.pad);
+        if (t < best.t || (t == best.t && orig < best_orig)) {
+            best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+            best_orig = orig;
+        }
+    }
+}
+/* Two records in flight (a, b), each reloaded in place right after its own test: the next
+ * record's scalar load overlaps the current test and no record is copied between registers
+ * (a one-record prefetch made the compiler move all 16 SGPRs of the record every iteration). */
 template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
     const uint32_t np = ufirst(sc.g->n_prims);
-    DPrim nxt = load_uniform(sc.gprims, 0);
-    for (uint32_t pi = 0; pi < np; ++pi) {
-        const DPrim p = nxt;
-        if (pi + 1 < np) nxt = load_uniform(sc.gprims, pi + 1);
-        float t, u, v;
-        if (prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v)) {
-            const uint32_t orig = ufirst(p.pad);
-            if (t < best.t || (t == best.t && orig < best_orig)) {
-                best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
-                best_orig = orig;
-            }
+    DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, np > 1 ? 1u : 0u);
+    for (uint32_t pi = 0; pi < np; pi += 2) {
+        brute_test<kSph>(a, pi, ray, best, best_orig);
+        if (pi + 2 < np) a = load_uniform(sc.gprims, pi + 2);
+        if (pi + 1 < np) {
+            brute_test<kSph>(b, pi + 1, ray, best, best_orig);
+            if (pi + 3 < np) b = load_uniform(sc.gprims, pi + 3);
         }
     }
     return best;
@@ -311,14 +321,17 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
 template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray) {
     const uint32_t np = ufirst(sc.g->n_prims);
     bool found = false;
-    DPrim nxt = load_uniform(sc.gprims, 0);
-    for (uint32_t pi = 0; pi < np; ++pi) {
-        const DPrim p = nxt;
-        if (pi + 1 < np) nxt = load_uniform(sc.gprims, pi + 1);
+    DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, np > 1 ? 1u : 0u);
+    for (uint32_t pi = 0; pi < np; pi += 2) {
         float t, u, v;
-        const bool h = !found && prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v);
-        found = found || h;
+        found = found || prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
+        if (pi + 2 < np) a = load_uniform(sc.gprims, pi + 2);
         if (!wave_any(!found)) break;
+        if (pi + 1 < np) {
+            found = found || prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
+            if (pi + 3 < np) b = load_uniform(sc.gprims, pi + 3);
+            if (!wave_any(!found)) break;
+        }
     }
     return found;
 }
