@@ -95,12 +95,14 @@ struct KParams {
     uint32_t chunk_n;
     uint32_t record;      /* write per-lane splat records */
     uint32_t row_splat;   /* row-reduced splat (row_put): lanes in pixel-major order, see slot_lane */
+    uint32_t adapt_pass;  /* the suffix runs paths of the adaptive wavefront (path_seq) */
 };
 
 /* SoA streams of one chunk */
+constexpr int kQPlanes = 5;   /* float4 planes of a path state (80 B, see store_state) */
 struct Bufs {
-    float4 *q_in[6];
-    float4 *q_out[6];
+    float4 *q_in[kQPlanes];
+    float4 *q_out[kQPlanes];
     uint32_t *cnt_in, *cnt_out;  /* kQParts partition counters each, kCntStride words apart */
     uint32_t qcap;               /* entries per queue partition */
     float4 *lane_out;     /* (indirect / result rgb, valid_ray) */
@@ -115,7 +117,8 @@ struct Bufs {
     uint8_t *amask;       /* adaptive: per-lane adapt_mask of the pass (lane order), or null */
     const uint32_t *asel; /* adaptive: compacted lanes with adapt_mask (ascending) */
     float4 *hit;          /* k_extend / k_prim_hit -> shading: closest hit (t, u, v, prim) per entry */
-    float4 *nee[4];       /* k_bounce -> k_shadow: deferred emitter-sample shadow rays (NEE records) */
+    float4 *nee[3];       /* k_bounce -> k_shadow: deferred emitter-sample shadow rays (NEE records), */
+    float *nee_cb;        /* + the contribution's blue channel as a float plane (52 B per record) */
     uint32_t *cnt_nee;
     float4 *vreq[3];      /* k_prim_req -> k_vis: (p, bits), (n, ap.x), (emitter point, ap.y) per lane */
     unsigned long long *occ; /* k_vis -> k_mv_primary: occlusion ballots, word (i >> 6) * G + slot */
@@ -1193,45 +1196,65 @@ struct PathState {
     uint32_t depth;
     bool prev_delta, valid_ray;
     f3 prev_p;
-    uint32_t idx;         /* chunk-local lane index */
+    uint32_t idx;         /* chunk-local slot of the lane (lane_out, slot_lane) */
     uint64_t rng_state;
-    uint32_t rng_seq;     /* v1 of TEA -> inc = 2*v1+1 */
+    uint32_t rng_seq;     /* v1 of TEA -> inc = 2*v1+1 (not stored: path_seq re-derives it) */
 };
 
+/*
+ * Path state in the queues: 5 float4 planes, 80 B per live path --
+ *   q0 (o.xyz, d.x)  q1 (d.yz, thr.rg)  q2 (thr.b, prev_pdf, bits, rng lo)  q3 (prev_p, idx)
+ *   q4 (result, rng hi)
+ * bits = depth (29 bits) | eta == 0 (bit 29) | prev_delta (30) | valid_ray (31).  eta is a
+ * product of BSDF-sample etas, which are 1 for every supported BSDF (diffuse, roughconductor,
+ * twosided) and 0 for an empty sample (bs_zero, e.g. a twosided BSDF at wi.z == 0), so one bit
+ * holds it exactly.  The PCG increment's seed v1 is re-derived from the slot (path_seq), not
+ * stored.  k_shadow adds NEE into q4's xyz in place.
+ */
 AD void store_state(float4 *const *q, uint32_t slot, const PathState &s) {
-    uint32_t bits = (s.depth & 0x3fffffffu) | (s.prev_delta ? 0x40000000u : 0u) | (s.valid_ray ? 0x80000000u : 0u);
+    const uint32_t bits = (s.depth & 0x1fffffffu) | (s.eta == 0.f ? 0x20000000u : 0u) |
+                          (s.prev_delta ? 0x40000000u : 0u) | (s.valid_ray ? 0x80000000u : 0u);
     q[0][slot] = make_float4(s.ray.o.x, s.ray.o.y, s.ray.o.z, s.ray.d.x);
     q[1][slot] = make_float4(s.ray.d.y, s.ray.d.z, s.thr.r, s.thr.g);
-    q[2][slot] = make_float4(s.thr.b, s.eta, s.prev_pdf, bitsf(bits));
+    q[2][slot] = make_float4(s.thr.b, s.prev_pdf, bitsf(bits), bitsf((uint32_t) s.rng_state));
     q[3][slot] = make_float4(s.prev_p.x, s.prev_p.y, s.prev_p.z, bitsf(s.idx));
-    q[4][slot] = make_float4(s.res.r, s.res.g, s.res.b, bitsf(s.rng_seq));
-    q[5][slot] = make_float4(bitsf((uint32_t) s.rng_state), bitsf((uint32_t) (s.rng_state >> 32)), 0.f, 0.f);
+    q[4][slot] = make_float4(s.res.r, s.res.g, s.res.b, bitsf((uint32_t) (s.rng_state >> 32)));
 }
 
 AD PathState load_state(float4 *const *q, uint32_t slot) {
     PathState s;
-    float4 a = q[0][slot], b = q[1][slot], c = q[2][slot], d = q[3][slot], e = q[4][slot], f = q[5][slot];
+    float4 a = q[0][slot], b = q[1][slot], c = q[2][slot], d = q[3][slot], e = q[4][slot];
     s.ray.o = mk(a.x, a.y, a.z);
     s.ray.d = mk(a.w, b.x, b.y);
     s.ray.maxt = kLargest;
     s.thr = C3{b.z, b.w, c.x};
-    s.eta = c.y;
-    s.prev_pdf = c.z;
-    uint32_t bits = fbits(c.w);
-    s.depth = bits & 0x3fffffffu;
+    s.prev_pdf = c.y;
+    const uint32_t bits = fbits(c.z);
+    s.depth = bits & 0x1fffffffu;
+    s.eta = (bits & 0x20000000u) ? 0.f : 1.f;
     s.prev_delta = (bits & 0x40000000u) != 0;
     s.valid_ray = (bits & 0x80000000u) != 0;
     s.prev_p = mk(d.x, d.y, d.z);
     s.idx = fbits(d.w);
     s.res = C3{e.x, e.y, e.z};
-    s.rng_seq = fbits(e.w);
-    s.rng_state = (uint64_t) fbits(f.x) | ((uint64_t) fbits(f.y) << 32);
+    s.rng_state = (uint64_t) fbits(c.w) | ((uint64_t) fbits(e.w) << 32);
+    s.rng_seq = 0;
     return s;
 }
 
 /* ------------------------------------------------------------------ */
 /* k_raygen_single: render_sample prologue (mvpath_single.h:50-76)     */
 /* ------------------------------------------------------------------ */
+
+/* TEA's v1 of the lane whose path sits in chunk slot `slot` (PCG increment 2 v1 + 1): the main
+ * pass seeds lane chunk_begin + slot_lane(slot) with seed_value (k_raygen_single, primary_raygen),
+ * the adaptive pass wavefront entry chunk_begin + slot with adapt_seed (k_raygen_adapt) */
+AD uint32_t path_seq(const KParams &P, uint32_t slot) {
+    uint32_t v0, v1;
+    if (P.adapt_pass) tea4(P.adapt_seed, P.adapt_base + (uint32_t) (P.chunk_begin + slot), v0, v1);
+    else tea4(P.seed_value, (uint32_t) (P.chunk_begin + slot_lane(P, slot)), v0, v1);
+    return v1;
+}
 
 AD void lane_pixel(const KParams &P, uint32_t lane, int &px, int &py) {
     uint32_t pix = P.pow2 ? (lane >> P.log_spp) : (lane / P.spp_pp);
@@ -1374,15 +1397,21 @@ __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Buf
         const uint32_t i = pbase + e0 + threadIdx.x;
         if (e0 + threadIdx.x < count) {
             const float4 a = B.nee[0][i], b = B.nee[1][i];
-            const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z};
+            /* spawn_ray_to's direction and extent from its origin and target (same operations) */
+            const f3 o = mk(a.x, a.y, a.z);
+            f3 d = mk(b.x, b.y, b.z) - o;
+            const float dist = norm(d);
+            d = d / dist;
+            const Ray r{o, d, dist * (1.f - kShadowEps)};
             if (!walk_any<kWalk>(sc, r)) {
-                const float4 t = B.nee[2][i], c = B.nee[3][i];
-                const uint32_t dest = fbits(b.w);
+                const float4 t = B.nee[2][i];
+                const float cb = B.nee_cb[i];
+                const uint32_t dest = fbits(a.w);
                 float4 *const dp = (dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest];
                 float4 v = *dp;
-                v.x = fmadd(t.x, c.x, v.x);
-                v.y = fmadd(t.y, c.y, v.y);
-                v.z = fmadd(t.z, c.z, v.z);
+                v.x = fmadd(b.w, t.z, v.x);
+                v.y = fmadd(t.x, t.w, v.y);
+                v.z = fmadd(t.y, cb, v.z);
                 *dp = v;
             }
         }
@@ -1406,12 +1435,13 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
         PathState s;
         bool keep = false, nee = false;
         Ray shr;
+        f3 nee_to;
         C3 nee_thr, nee_c;
         if (ok) {
             s = load_state(B.q_in, i);
             Pcg rng;
             rng.state = s.rng_state;
-            rng.inc = (((uint64_t) s.rng_seq) << 1) | 1u;
+            rng.inc = (((uint64_t) path_seq(P, s.idx)) << 1) | 1u;
             ++verts;
             SI si = compute_si(sc, s.ray, hit_of(B.hit[i]));
             int32_t em = si_emitter(sc, si);
@@ -1450,6 +1480,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
                 nee_thr = s.thr;
                 nee_c = bval * em_w * mis_em;
                 shr = spawn_ray_to(si.p, si.n, ds.p);
+                nee_to = ds.p;
             }
             s.ray = spawn_ray(si.p, si.n, si.sh.to_world(bs.wo));
             s.thr = s.thr * bw;
@@ -1474,10 +1505,12 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
         shadows += nee ? 1 : 0;
         if (nee) {
             const uint32_t dest = keep ? slot : (0x80000000u | s.idx);
-            B.nee[0][ns] = make_float4(shr.o.x, shr.o.y, shr.o.z, shr.d.x);
-            B.nee[1][ns] = make_float4(shr.d.y, shr.d.z, shr.maxt, bitsf(dest));
-            B.nee[2][ns] = make_float4(nee_thr.r, nee_thr.g, nee_thr.b, 0.f);
-            B.nee[3][ns] = make_float4(nee_c.r, nee_c.g, nee_c.b, 0.f);
+            /* (origin, destination), (light point, thr.r), (thr.gb, c.rg), c.b: k_shadow re-derives the
+             * direction and extent exactly as spawn_ray_to did */
+            B.nee[0][ns] = make_float4(shr.o.x, shr.o.y, shr.o.z, bitsf(dest));
+            B.nee[1][ns] = make_float4(nee_to.x, nee_to.y, nee_to.z, nee_thr.r);
+            B.nee[2][ns] = make_float4(nee_thr.g, nee_thr.b, nee_c.r, nee_c.g);
+            B.nee_cb[ns] = nee_c.b;
         }
     }
     if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
@@ -2590,12 +2623,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         o.pad1 = 0.f;
     }
 
-    /* lane arena: queues (2 x 6 x 16 B), lane_out + hit (32 B), NEE queue (64 B), visibility requests
+    /* lane arena: queues (2 x 5 x 16 B), lane_out + hit (32 B), NEE queue (52 B), visibility requests
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
     const uint64_t span = lane_end - lane_begin;
     const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
     const bool diff_rec = scene->all_diffuse && diffuse_spec && G <= 16;   /* kDiff instances, compact view records */
-    const size_t per_lane = 12 * 16 + 32 + 64 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8;
+    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8;
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
@@ -2647,13 +2680,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     }
 
     Bufs B{};
-    float4 *qa[6], *qb[6];
-    for (int k = 0; k < 6; ++k) qa[k] = (float4 *) carve(16 * qlen);
-    for (int k = 0; k < 6; ++k) qb[k] = (float4 *) carve(16 * qlen);
+    float4 *qa[kQPlanes], *qb[kQPlanes];
+    for (int k = 0; k < kQPlanes; ++k) qa[k] = (float4 *) carve(16 * qlen);
+    for (int k = 0; k < kQPlanes; ++k) qb[k] = (float4 *) carve(16 * qlen);
     B.lane_out = (float4 *) carve(16 * chunk);
     for (int k = 0; k < 4; ++k) B.lrec[k] = (float4 *) carve(16 * chunk);
     B.hit = (float4 *) carve(16 * std::max<uint64_t>(chunk, qlen));
-    for (int k = 0; k < 4; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
+    for (int k = 0; k < 3; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
+    B.nee_cb = (float *) carve(4 * qlen);
     for (int k = 0; k < 3; ++k) B.vreq[k] = (float4 *) carve(16 * chunk);
     B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
     B.cnt_nee = cntN;
@@ -2692,7 +2726,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         const uint32_t bgrid = kQParts * std::max<uint32_t>(1, std::min<uint32_t>(16, (cn + 256 * kQParts - 1) / (256 * kQParts)));
         bool a_is_in = true;
         for (uint32_t bnc = 0; bnc < max_bounces; ++bnc) {
-            for (int k = 0; k < 6; ++k) {
+            for (int k = 0; k < kQPlanes; ++k) {
                 B.q_in[k] = a_is_in ? qa[k] : qb[k];
                 B.q_out[k] = a_is_in ? qb[k] : qa[k];
             }
@@ -2741,7 +2775,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             const dim3 grid((cn + 255) / 256);
             /* counters: [0] = queue A, [1] = queue B */
             HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
-            for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
+            for (int k = 0; k < kQPlanes; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
             B.cnt_out = cntA; B.cnt_in = cntB;
             T.mark(st);
             if (G == 1) {
@@ -2797,13 +2831,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             P.pass_seed = P.seed_value;
             P.adapt_seed = Pp.base_seed + (uint32_t) (total * n_adapt);   /* sampler->fork(); seed(wavefront, wavefront) */
             P.adapt_base = (uint32_t) (prefix * n_adapt);
+            P.adapt_pass = 1;
             P.record = 0;
             for (uint64_t c0 = 0; c0 < wf; c0 += chunk) {
                 const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, wf - c0);
                 P.chunk_begin = c0;
                 P.chunk_n = cn;
                 HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
-                for (int k = 0; k < 6; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
+                for (int k = 0; k < kQPlanes; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
                 B.cnt_out = cntA; B.cnt_in = cntB;
                 T.begin(AMVPT_K_RAYGEN, st);
                 hipLaunchKernelGGL(k_raygen_adapt, dim3((cn + 255) / 256), dim3(256), 0, st, P, dviews, B);

@@ -306,14 +306,15 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
     const uint32_t np = ufirst(sc.g->n_prims);
-    DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, np > 1 ? 1u : 0u);
+    const uint32_t last = np - 1u;
+    DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
     for (uint32_t pi = 0; pi < np; pi += 2) {
+        /* unconditional reloads (index clamped to the table): a conditional one would merge two
+         * values of the record and cost a register copy per primitive */
         brute_test<kSph>(a, pi, ray, best, best_orig);
-        if (pi + 2 < np) a = load_uniform(sc.gprims, pi + 2);
-        if (pi + 1 < np) {
-            brute_test<kSph>(b, pi + 1, ray, best, best_orig);
-            if (pi + 3 < np) b = load_uniform(sc.gprims, pi + 3);
-        }
+        a = load_uniform(sc.gprims, min(pi + 2u, last));
+        if (pi + 1 < np) brute_test<kSph>(b, pi + 1, ray, best, best_orig);
+        b = load_uniform(sc.gprims, min(pi + 3u, last));
     }
     return best;
 }
@@ -321,17 +322,15 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
 template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray) {
     const uint32_t np = ufirst(sc.g->n_prims);
     bool found = false;
-    DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, np > 1 ? 1u : 0u);
+    const uint32_t last = np - 1u;
+    DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
     for (uint32_t pi = 0; pi < np; pi += 2) {
         float t, u, v;
-        found = found || prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
-        if (pi + 2 < np) a = load_uniform(sc.gprims, pi + 2);
+        if (!found) found = prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
+        a = load_uniform(sc.gprims, min(pi + 2u, last));
+        if (pi + 1 < np && !found) found = prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
+        b = load_uniform(sc.gprims, min(pi + 3u, last));
         if (!wave_any(!found)) break;
-        if (pi + 1 < np) {
-            found = found || prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
-            if (pi + 3 < np) b = load_uniform(sc.gprims, pi + 3);
-            if (!wave_any(!found)) break;
-        }
     }
     return found;
 }
