@@ -1421,7 +1421,14 @@ __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Buf
 #ifndef AMVPT_BOUNCE_WAVES
 #define AMVPT_BOUNCE_WAVES 4
 #endif
-template <bool kTab, bool kDiff>
+/*
+ * kNee >= 0: the NEE shadow ray is traced inside k_bounce with walk kNee (the brute-force walks of
+ * tiny scenes, which are ALU-bound and need no occupancy to hide node-load latency): no NEE
+ * record goes through HBM, no k_shadow launch, and the visible light's contribution is added to
+ * the path's result right after the vertex's emitter-hit term -- the order k_shadow keeps.
+ * kNee < 0: NEE records for k_shadow.
+ */
+template <bool kTab, bool kDiff, int kNee>
 __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -1497,12 +1504,20 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             if (rractive) s.thr = s.thr * rcp(rr_prob);
             keep = active_next && (!rractive || rr_continue) && (tmax != 0.f);
             s.rng_state = rng.state;
-            if (!keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
+            if (kNee < 0 && !keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
+        }
+        shadows += nee ? 1 : 0;
+        if constexpr (kNee >= 0) {
+            /* every lane of the wave walks (wave-uniform brute force); lanes without a shadow ray
+             * start as found */
+            const bool occluded = brute_any<kNee == WALK_BRUTE>(sc, shr, !nee);
+            if (nee && !occluded) s.res = cfma(nee_thr, nee_c, s.res);
+            if (ok && !keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
         }
         const uint32_t slot = push_slot(keep, B.cnt_out, B.qcap);
         if (keep) store_state(B.q_out, slot, s);
+        if constexpr (kNee >= 0) continue;
         const uint32_t ns = push_slot(nee, B.cnt_nee, B.qcap);
-        shadows += nee ? 1 : 0;
         if (nee) {
             const uint32_t dest = keep ? slot : (0x80000000u | s.idx);
             /* (origin, destination), (light point, thr.r), (thr.gb, c.rg), c.b: k_shadow re-derives the
@@ -2449,6 +2464,23 @@ struct KTimer {
     }
 };
 
+static void launch_bounce(bool tab, bool diff, int nee_walk, dim3 grid, size_t lds, hipStream_t st, const KParams &P,
+                          const DScene *S, const Bufs &B) {
+#define AMVPT_BOUNCE(T_, D_, N_) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<T_, D_, N_>), grid, dim3(256), lds, st, P, S, B)
+#define AMVPT_BOUNCE_N(T_, D_)                                            \
+    do {                                                                 \
+        if (nee_walk == WALK_BRUTE_NS) AMVPT_BOUNCE(T_, D_, WALK_BRUTE_NS); \
+        else if (nee_walk == WALK_BRUTE) AMVPT_BOUNCE(T_, D_, WALK_BRUTE);  \
+        else AMVPT_BOUNCE(T_, D_, -1);                                    \
+    } while (0)
+    if (tab && diff) AMVPT_BOUNCE_N(true, true);
+    else if (tab) AMVPT_BOUNCE_N(true, false);
+    else if (diff) AMVPT_BOUNCE_N(false, true);
+    else AMVPT_BOUNCE_N(false, false);
+#undef AMVPT_BOUNCE_N
+#undef AMVPT_BOUNCE
+}
+
 /* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
 template <int G>
 static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
@@ -2710,6 +2742,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         if (uni && g_traversal == 0u && brute_on && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
     }
     const bool diff = diff_rec;                                                                           /* kDiff instances */
+    /* NEE traced inside k_bounce (brute-force walks; AMVPT_FUSE_NEE=0 keeps k_shadow, A/B) */
+    bool fuse_nee = walk == WALK_BRUTE || walk == WALK_BRUTE_NS;
+    { const char *e = std::getenv("AMVPT_FUSE_NEE"); if (e && e[0] == '0') fuse_nee = false; }
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
@@ -2740,14 +2775,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             T.end(st);
             T.begin(AMVPT_K_BOUNCE, st);
-            if (tab_b && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true, true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
-            else if (tab_b) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<true, false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
-            else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false, true>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
-            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bounce<false, false>), dim3(bgrid), dim3(256), lds, st, P, dS, B);
+            launch_bounce(tab_b, diff, fuse_nee ? walk : -1, dim3(bgrid), lds, st, P, dS, B);
             T.end(st);
-            T.begin(AMVPT_K_SHADOW, st);
-            launch_shadow(walk, dim3(bgrid), lds_ext, st, P, dS, B);
-            T.end(st);
+            if (!fuse_nee) {
+                T.begin(AMVPT_K_SHADOW, st);
+                launch_shadow(walk, dim3(bgrid), lds_ext, st, P, dS, B);
+                T.end(st);
+            }
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);
             a_is_in = !a_is_in;

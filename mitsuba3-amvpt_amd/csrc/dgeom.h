@@ -319,9 +319,10 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     return best;
 }
 
-template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray) {
+/* skip: the lane has no ray (it counts as found, so the wave stops when every real ray is) */
+template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool skip = false) {
     const uint32_t np = ufirst(sc.g->n_prims);
-    bool found = false;
+    bool found = skip;
     const uint32_t last = np - 1u;
     DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
     for (uint32_t pi = 0; pi < np; pi += 2) {
