@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 5
+#define AMVPT_ABI_VERSION 6
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -91,13 +91,19 @@ typedef struct amvpt_bsdf_desc {
     float specular_reflectance[3];
 } amvpt_bsdf_desc;
 
-enum { AMVPT_EMITTER_AREA = 0 };
+enum {
+    AMVPT_EMITTER_AREA = 0,     /* src/emitters/area.cpp: attached to a rectangle / sphere shape */
+    AMVPT_EMITTER_CONSTANT = 1  /* src/emitters/constant.cpp: environment, shape = -1 */
+};
 
+/* emitters[] is Scene::m_emitters: the order in which the scene lists them (an area emitter at
+ * its shape's position, a constant emitter at its own), which emitter sampling indexes */
 typedef struct amvpt_emitter_desc {
     uint32_t type;
-    int32_t shape;          /* shape the area emitter is attached to */
+    int32_t shape;          /* shape the area emitter is attached to; -1 for AMVPT_EMITTER_CONSTANT */
     float radiance[3];
-    float sampling_weight;  /* != 1 on any emitter -> DiscreteDistribution (unsupported, reported) */
+    float sampling_weight;  /* Emitter 'sampling_weight' (>= 0); any != 1 -> DiscreteDistribution
+                               emitter sampling (scene.cpp:100-119, 222-244) */
 } amvpt_emitter_desc;
 
 typedef struct amvpt_scene_desc {
@@ -107,7 +113,8 @@ typedef struct amvpt_scene_desc {
     uint32_t bsdf_count;
     const amvpt_emitter_desc *emitters;
     uint32_t emitter_count;
-    uint32_t has_environment; /* no environment emitter on the implemented path: must be 0 */
+    uint32_t has_environment; /* number of AMVPT_EMITTER_CONSTANT entries in emitters[] (0 or 1:
+                                 Scene::m_environment); its bounding sphere is the scene bbox's */
 } amvpt_scene_desc;
 
 /* ------------------------------------------------------------------ */

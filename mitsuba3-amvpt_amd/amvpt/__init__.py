@@ -90,6 +90,7 @@ KERNELS = ("k_prim_hit", "k_prim_req", "k_vis", "k_mv_primary", "k_raygen", "k_e
 
 
 INTEGRATOR_MVPATH, INTEGRATOR_PATH = 0, 1
+EMITTER_AREA, EMITTER_CONSTANT = 0, 1
 _hip = None
 _host = None
 

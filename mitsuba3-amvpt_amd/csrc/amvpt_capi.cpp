@@ -262,7 +262,25 @@ static amvpt_status validate_scene(const amvpt_scene_desc *d) {
         set_error("amvpt_scene_create: null table with a non-zero count");
         return AMVPT_ERR_INVALID;
     }
-    if (d->has_environment) { set_error("environment emitters are outside the implemented path"); return AMVPT_ERR_UNSUPPORTED; }
+    {
+        uint32_t n_env = 0;
+        bool positive = false;
+        for (uint32_t i = 0; i < d->emitter_count; ++i) {
+            n_env += d->emitters[i].type == AMVPT_EMITTER_CONSTANT ? 1u : 0u;
+            const float w = d->emitters[i].sampling_weight;
+            if (!(w >= 0.f) || !std::isfinite(w)) {
+                set_error("DiscreteDistribution: entries must be non-negative!");
+                return AMVPT_ERR_INVALID;
+            }
+            positive = positive || w > 0.f;
+        }
+        if (d->emitter_count && !positive) { set_error("DiscreteDistribution: no probability mass found!"); return AMVPT_ERR_INVALID; }
+        if (n_env > 1) { set_error("Only one environment emitter can be specified per scene."); return AMVPT_ERR_INVALID; }
+        if (d->has_environment != n_env) {
+            set_error("amvpt_scene_create: has_environment must count the AMVPT_EMITTER_CONSTANT emitters");
+            return AMVPT_ERR_INVALID;
+        }
+    }
     for (uint32_t i = 0; i < d->bsdf_count; ++i) {
         const amvpt_bsdf_desc &b = d->bsdfs[i];
         if (b.type == AMVPT_BSDF_ROUGHCONDUCTOR &&
@@ -285,9 +303,13 @@ static amvpt_status validate_scene(const amvpt_scene_desc *d) {
     }
     for (uint32_t i = 0; i < d->emitter_count; ++i) {
         const amvpt_emitter_desc &e = d->emitters[i];
+        if (e.type == AMVPT_EMITTER_CONSTANT) {
+            if (e.shape != -1) { set_error("a constant emitter is not attached to a shape (shape must be -1)"); return AMVPT_ERR_INVALID; }
+            continue;
+        }
+        if (e.type != AMVPT_EMITTER_AREA) { set_error("unknown emitter type"); return AMVPT_ERR_INVALID; }
         if (e.shape < 0 || (uint32_t) e.shape >= d->shape_count) { set_error("emitter without a valid shape"); return AMVPT_ERR_INVALID; }
         if (d->shapes[e.shape].type == AMVPT_SHAPE_MESH) { set_error("area emitters on meshes are not implemented"); return AMVPT_ERR_UNSUPPORTED; }
-        if (e.sampling_weight != 1.f) { set_error("non-uniform emitter sampling weights are not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     }
 
     for (uint32_t i = 0; i < d->shape_count; ++i) {
@@ -312,11 +334,48 @@ static amvpt_status validate_scene(const amvpt_scene_desc *d) {
         }
     }
     for (uint32_t i = 0; i < d->emitter_count; ++i)
-        if (d->shapes[d->emitters[i].shape].emitter != (int32_t) i) {
+        if (d->emitters[i].type == AMVPT_EMITTER_AREA && d->shapes[d->emitters[i].shape].emitter != (int32_t) i) {
             set_error("shape.emitter and emitter.shape disagree");
             return AMVPT_ERR_INVALID;
         }
     return AMVPT_OK;
+}
+
+/* Transform::transform_affine of a point with the reference's fmadd chains (row-major 4x4) */
+static void xform_affine(const float *m, const float p[3], float out[3]) {
+    for (int i = 0; i < 3; ++i)
+        out[i] = std::fmaf(m[i * 4 + 2], p[2], std::fmaf(m[i * 4 + 1], p[1], std::fmaf(m[i * 4 + 0], p[0], m[i * 4 + 3])));
+}
+
+/* ConstantBackgroundEmitter::set_scene (constant.cpp:73-88): the bounding sphere of Scene::bbox()
+ * (union of Shape::bbox(): rectangle corners, mesh vertices, sphere center -+ radius), center =
+ * (min + max) / 2, radius = |center - max| enlarged by (1 + RayEpsilon), at least RayEpsilon */
+static void scene_bsphere(const amvpt_scene_desc *d, float center[3], float &radius) {
+    const float ray_eps = 1500.f * 5.9604644775390625e-8f;   /* math.h:18-23: 1500 * 2^-24 */
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool any = false;
+    auto expand = [&](const float p[3]) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+        any = true;
+    };
+    for (uint32_t i = 0; i < d->shape_count; ++i) {
+        const amvpt_shape_desc &s = d->shapes[i];
+        if (s.type == AMVPT_SHAPE_RECTANGLE) {
+            const float corners[4][3] = {{-1.f, -1.f, 0.f}, {1.f, -1.f, 0.f}, {1.f, 1.f, 0.f}, {-1.f, 1.f, 0.f}};
+            for (auto &c : corners) { float w[3]; xform_affine(s.to_world, c, w); expand(w); }
+        } else if (s.type == AMVPT_SHAPE_MESH) {
+            for (uint32_t v = 0; v < s.vertex_count; ++v) expand(s.positions + 3 * (size_t) v);
+        } else {
+            const float a[3] = {s.center[0] - s.radius, s.center[1] - s.radius, s.center[2] - s.radius};
+            const float b[3] = {s.center[0] + s.radius, s.center[1] + s.radius, s.center[2] + s.radius};
+            expand(a); expand(b);
+        }
+    }
+    if (!any) { center[0] = center[1] = center[2] = 0.f; radius = ray_eps; return; }
+    for (int k = 0; k < 3; ++k) center[k] = (hi[k] + lo[k]) * .5f;
+    const float dx = center[0] - hi[0], dy = center[1] - hi[1], dz = center[2] - hi[2];
+    radius = std::sqrt(std::fmaf(dz, dz, std::fmaf(dy, dy, dx * dx)));
+    radius = std::max(ray_eps, radius * (1.f + ray_eps));
 }
 
 amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
@@ -476,9 +535,20 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         }
     }
     std::vector<DEmitter> emitters(std::max<uint32_t>(1, d->emitter_count));
+    bool distr = false;
+    int32_t environment = -1;
+    float cdf_acc = 0.f;
     for (uint32_t i = 0; i < d->emitter_count; ++i) {
-        emitters[i].shape = d->emitters[i].shape;
-        std::memcpy(emitters[i].radiance, d->emitters[i].radiance, 12);
+        DEmitter &e = emitters[i];
+        std::memset(&e, 0, sizeof(e));
+        e.shape = d->emitters[i].shape;
+        e.type = d->emitters[i].type;
+        std::memcpy(e.radiance, d->emitters[i].radiance, 12);
+        e.weight = d->emitters[i].sampling_weight;
+        cdf_acc += e.weight;   /* DiscreteDistribution::compute_cdf: dr::prefix_sum in float */
+        e.cdf = cdf_acc;
+        distr = distr || e.weight != 1.f;
+        if (e.type == AMVPT_EMITTER_CONSTANT) environment = (int32_t) i;
     }
     if (vpos.empty()) vpos.resize(3, 0.f);
     if (vnrm.empty()) vnrm.resize(3, 0.f);
@@ -521,6 +591,12 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;
     D.emitter_pmf = d->emitter_count ? 1.f / (float) d->emitter_count : 0.f;
+    D.environment = environment;
+    D.distr = distr ? 1u : 0u;
+    D.distr_sum = d->emitter_count ? emitters[d->emitter_count - 1].cdf : 0.f;
+    D.distr_norm = D.distr_sum != 0.f ? 1.f / D.distr_sum : 0.f;
+    if (environment >= 0) scene_bsphere(d, D.bs_center, D.bs_radius);
+    else { D.bs_center[0] = D.bs_center[1] = D.bs_center[2] = 0.f; D.bs_radius = 0.f; }
     D.n_bsdfs = d->bsdf_count;
     {
         const uint32_t tb = tab_round(d->shape_count * (uint32_t) sizeof(DShape)) +

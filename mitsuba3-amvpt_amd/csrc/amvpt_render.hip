@@ -96,6 +96,8 @@ struct KParams {
     uint32_t record;      /* write per-lane splat records */
     uint32_t row_splat;   /* row-reduced splat (row_put): lanes in pixel-major order, see slot_lane */
     uint32_t adapt_pass;  /* the suffix runs paths of the adaptive wavefront (path_seq) */
+    uint32_t valid_ray0;  /* !hide_emitters && environment: escaped camera rays count as valid
+                           * (mvpath_multi.h:140, mvpath_single.h:98, path.cpp:114) */
 };
 
 /* SoA streams of one chunk */
@@ -219,45 +221,94 @@ AD float4 hit_rec(const Hit &h) { return make_float4(h.t, h.u, h.v, bitsf((uint3
 /* Emitters at scene level                                            */
 /* ------------------------------------------------------------------ */
 
+/* SurfaceInteraction::emitter: the shape's area emitter, or the scene's environment (constant)
+ * emitter for a ray that left the scene */
 AD int32_t si_emitter(const SceneRef &sc, const SI &si) {
-    return si.valid() ? sc.g->shapes[si.shape].emitter : -1;
+    return si.valid() ? sc.g->shapes[si.shape].emitter : sc.g->environment;
 }
 
+/* AreaLight::eval (area.cpp:82-88: front side only), ConstantBackgroundEmitter::eval
+ * (constant.cpp:90-94) */
 AD C3 emitter_eval(const SceneRef &sc, int32_t e, const SI &si, bool active) {
     if (e < 0 || !active) return c3(0.f);
-    if (!(si.wi.z > 0.f)) return c3(0.f);
-    return c3(sc.g->emitters[e].radiance);
+    const DEmitter &em = sc.g->emitters[e];
+    if (em.type != AMVPT_EMITTER_CONSTANT && !(si.wi.z > 0.f)) return c3(0.f);
+    return c3(em.radiance);
+}
+
+/* Scene::pdf_emitter (scene.cpp:245-250) */
+AD float emitter_pick_pmf(const DScene &S, uint32_t i) {
+    return S.distr ? S.emitters[i].weight * S.distr_norm : S.emitter_pmf;
+}
+
+/* Scene::sample_emitter (scene.cpp:222-244); non-uniform weights: DiscreteDistribution::
+ * sample_reuse_pmf (distr_1d.h:201-215) with the JIT predicate of sample() (:116-134) and
+ * dr::binary_search over [0, n - 1] (floor(log2(n - 1)) + 1 halvings) */
+AD uint32_t sample_emitter(const DScene &S, float &u, float &weight) {
+    const uint32_t n = S.n_emitters;
+    weight = 1.f;
+    if (n < 2) return 0;
+    if (S.distr) {
+        const float sample = u * S.distr_sum;
+        uint32_t start = 0, end = n - 1u;
+        const uint32_t it = 32u - (uint32_t) __builtin_clz(end);
+        for (uint32_t k = 0; k < it; ++k) {
+            const uint32_t middle = (start + end) >> 1;
+            const float c = S.emitters[middle].cdf;
+            const bool cond = ((c < sample) || c == 0.f) && c != S.distr_sum;
+            start = cond ? min(middle + 1u, end) : start;
+            end = cond ? end : middle;
+        }
+        const float pmf = S.emitters[start].weight * S.distr_norm;
+        const float cdf = start > 0 ? S.emitters[start - 1].cdf * S.distr_norm : 0.f;
+        u = (u - cdf) / pmf;
+        weight = rcp(pmf);
+        return start;
+    }
+    const float scaled = u * (float) n;
+    const uint32_t index = min((uint32_t) scaled, n - 1u);
+    weight = (float) n;
+    u = scaled - (float) index;
+    return index;
 }
 
 /*
  * Scene::sample_emitter_direction (scene.cpp:294-348) up to its ray_test: returns
  * true when the reference would trace the shadow ray spawn_ray_to(ref.p, ref.n,
  * ds.p).  The test itself runs in its own wavefront (k_vis slot 0 for primary
- * vertices, k_shadow for suffix vertices); an occluded sample is then zeroed
+ * vertices, k_shadow / k_bounce for suffix vertices); an occluded sample is then zeroed
  * exactly as the reference does (spec = 0, ds.pdf = 0).
  */
 AD bool sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, float u2, bool active, DSamp &ds,
                                  C3 &spec) {
     ds = ds_zero();
     spec = c3(0.f);
-    uint32_t n = sc.g->n_emitters;
-    if (n == 0) return false;
-    uint32_t index = 0;
-    float weight = 1.f;
-    if (n >= 2) {
-        float scaled = u1 * (float) n;
-        index = min((uint32_t) scaled, n - 1u);
-        weight = (float) n;
-        u1 = scaled - (float) index;
-    }
+    const DScene &S = *sc.g;
+    if (S.n_emitters == 0) return false;
+    float weight;
+    const uint32_t index = sample_emitter(S, u1, weight);
     if (!active) return false;
-    const DEmitter &em = sc.g->emitters[index];
-    const DShape &s = sc.g->shapes[em.shape];
-    ds = shape_sample_direction(s, ref.p, u1, u2);
-    bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
-    spec = csel(a, c3(em.radiance) / ds.pdf, c3(0.f));
+    const DEmitter &em = S.emitters[index];
+    if (em.type == AMVPT_EMITTER_CONSTANT) {
+        /* ConstantBackgroundEmitter::sample_direction (constant.cpp:125-152) */
+        const f3 d = uniform_sphere(u1, u2);
+        const f3 c = mk(S.bs_center[0], S.bs_center[1], S.bs_center[2]);
+        const float radius = vmax(S.bs_radius, norm(ref.p - c)), dist = 2.f * radius;
+        ds.p = fma3(d, dist, ref.p);
+        ds.n = -d;
+        ds.pdf = kInvFourPi;
+        ds.delta = false;
+        ds.d = d;
+        ds.dist = dist;
+        spec = c3(em.radiance) / ds.pdf;
+    } else {
+        const DShape &s = S.shapes[em.shape];
+        ds = shape_sample_direction(s, ref.p, u1, u2);
+        bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
+        spec = csel(a, c3(em.radiance) / ds.pdf, c3(0.f));
+    }
     ds.emitter = (int32_t) index;
-    ds.pdf *= sc.g->emitter_pmf;
+    ds.pdf *= emitter_pick_pmf(S, index);
     spec = spec * weight;
     return ds.pdf != 0.f;
 }
@@ -266,10 +317,13 @@ AD void occlude_emitter_sample(DSamp &ds, C3 &spec) { spec = c3(0.f); ds.pdf = 0
 AD float pdf_emitter_direction(const SceneRef &sc, f3 refp, const DSamp &ds, bool active) {
     if (ds.emitter < 0 || !active) return 0.f;
     const DEmitter &em = sc.g->emitters[ds.emitter];
+    const float pick = emitter_pick_pmf(*sc.g, (uint32_t) ds.emitter);
+    /* ConstantBackgroundEmitter::pdf_direction (constant.cpp:154-159): the uniform sphere */
+    if (em.type == AMVPT_EMITTER_CONSTANT) return kInvFourPi * pick;
     const DShape &s = sc.g->shapes[em.shape];
     bool a = dot(ds.d, ds.n) < 0.f;
     float v = shape_pdf_direction(s, refp, ds);
-    return (a ? v : 0.f) * sc.g->emitter_pmf;
+    return (a ? v : 0.f) * pick;
 }
 
 AD float mis_weight(float a, float b) {
@@ -1283,7 +1337,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
         uint32_t index;
         s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
-        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
+        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
         s.prev_p = mk(0.f, 0.f, 0.f);
         s.idx = slot;
         s.rng_state = rng.state;
@@ -1333,7 +1387,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
         uint32_t index;
         s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
-        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = false;
+        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
         s.prev_p = mk(0.f, 0.f, 0.f);
         s.idx = slot;
         s.rng_state = rng.state;
@@ -1844,7 +1898,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         uint32_t nf_bits = 0, smask = 0;   /* kDiff: non-finite emis_mis channels, wi_k.z > 0 views */
 
         /* ---- sample_multi (mvpath_multi.h:130-369) ---- */
-        bool valid_ray = false, adapt_mask = false;
+        bool valid_ray = P.valid_ray0 != 0 && P.max_depth != 0, adapt_mask = false;
         float pdfW = 1.f;
         bool should_mis = P.sa_mis != 0;
         if (P.max_depth != 0) {
@@ -2628,6 +2682,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         P.win_rs = e && e[0] ? (uint32_t) std::strtoul(e, nullptr, 0) % 32u : (uint32_t) AMVPT_WIN_RS;
     }
     P.range_begin = lane_begin;
+    P.valid_ray0 = (!Pp.hide_emitters && scene->dev.environment >= 0) ? 1u : 0u;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
     /* row-reduced splat (row_put): RGBW film, Gaussian filter, >= 16 samples per pixel and pass
      * (a 16-lane row = one pixel); AMVPT_ROW_SPLAT=0 keeps the per-lane splat (A/B) */

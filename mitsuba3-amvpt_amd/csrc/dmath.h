@@ -38,6 +38,7 @@ AD bool finite_(float x) { return (fbits(x) & 0x7f800000u) != 0x7f800000u; }
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInvPi = 0.31830988618379067154f;
 constexpr float kInvTwoPi = 0.15915494309189533577f;
+constexpr float kInvFourPi = 0.07957747154594766788f;
 constexpr float kEps = 5.9604644775390625e-08f;
 constexpr float kRayEps = kEps * 1500.f;
 constexpr float kShadowEps = kRayEps * 10.f;
@@ -195,12 +196,14 @@ AD f3 cosine_hemisphere(float u, float v) {
     disk_concentric(u, v, x, y);
     return {x, y, safe_sqrt(1.f - fmadd(y, y, x * x))};
 }
+/* warp::square_to_uniform_sphere (warp.h:249-255): z = 1 - 2 v, r = circ(z), phi = 2 pi u */
 AD f3 uniform_sphere(float u, float v) {
-    float x, y;
-    disk_concentric(u, v, x, y);
-    float z = 1.f - fmadd(y, y, x * x);
-    float f = dsqrt(z + 1.f);
-    return {x * f, y * f, z};
+    const float z = fmadd(-2.f, v, 1.f);
+    const float q = fmadd(-z, z, 1.f);
+    const float r = dsqrt(q > 0.f ? q : 0.f);   /* circ = safe_sqrt(1 - z^2) */
+    float s, c;
+    sincos_c(u * (2.f * kPi), s, c);
+    return {r * c, r * s, z};
 }
 
 } // namespace amvpt

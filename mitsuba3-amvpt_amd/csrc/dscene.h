@@ -62,10 +62,12 @@ struct DBsdf {
 };
 
 struct DEmitter {
-    int32_t shape;
-    uint32_t pad;
+    int32_t shape;          /* area: its shape; constant (environment): -1 */
+    uint32_t type;          /* AMVPT_EMITTER_AREA / AMVPT_EMITTER_CONSTANT */
     float radiance[3];
-    float pad2;
+    float weight;           /* sampling_weight (DiscreteDistribution pmf entry) */
+    float cdf;              /* inclusive prefix sum of the weights (float, compute_cdf) */
+    float pad[3];
 };
 
 struct DView {
@@ -95,6 +97,10 @@ struct DScene {
     const uint32_t *faces;  /* 3 per face, indices relative to the shape's vbase */
     uint32_t n_nodes, n_prims, n_shapes, n_emitters;
     float emitter_pmf;
+    int32_t environment;    /* the constant emitter's index, or -1 */
+    uint32_t distr;         /* non-uniform emitter sampling (scene.cpp:100-119) */
+    float distr_sum, distr_norm;
+    float bs_center[3], bs_radius;  /* the constant emitter's bounding sphere (constant.cpp:73-88) */
     uint32_t lds_bytes;     /* nodes+prims footprint (LDS staging when small) */
     uint32_t n_bsdfs;
     uint32_t tab_bytes;     /* shapes+bsdfs+emitters footprint if <= kTabBytes (staged in LDS), else 0 */

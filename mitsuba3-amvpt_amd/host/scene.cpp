@@ -517,8 +517,24 @@ static void build(amvpt_host_scene &S) {
             S.sensors.push_back(make_sensor(o));
         } else if (o.tag == "emitter") {
             std::string t = lower(o.props.plugin);
-            if (t == "constant" || t == "envmap") { S.has_env = true; Throw("Environment emitters are outside the implemented path"); }
-            Throw("Emitter \"" + o.props.plugin + "\" must be attached to a shape (area) on the implemented path");
+            if (t == "constant") {
+                /* ConstantBackgroundEmitter (constant.cpp:52-65): radiance (default 1), infinite */
+                if (S.has_env) Throw("Only one environment emitter can be specified per scene.");
+                amvpt_emitter_desc ed;
+                std::memset(&ed, 0, sizeof(ed));
+                ed.type = AMVPT_EMITTER_CONSTANT;
+                ed.shape = -1;
+                float rad[3] = {1.f, 1.f, 1.f};
+                (void) o.props.get_rgb("radiance", rad);
+                std::memcpy(ed.radiance, rad, 12);
+                ed.sampling_weight = (float) o.props.get_float("sampling_weight", 1.0);
+                S.emitters.push_back(ed);
+                S.has_env = true;
+            } else if (t == "envmap") {
+                Throw("Emitter \"envmap\" is outside the implemented path (constant, area)");
+            } else {
+                Throw("Emitter \"" + o.props.plugin + "\" must be attached to a shape (area) on the implemented path");
+            }
         } else if (o.tag == "shape") {
             const Properties &p = o.props;
             std::string t = lower(p.plugin);

@@ -134,11 +134,13 @@ static inline V3 square_to_cosine_hemisphere(V2 s) {
     return {p.x, p.y, z};
 }
 static inline float cosine_hemisphere_pdf(V3 v) { return InvPi * v.z; }
+/* warp::square_to_uniform_sphere (warp.h:249-255): z = 1 - 2 y, r = circ(z), phi = 2 pi x */
 static inline V3 square_to_uniform_sphere(V2 s) {
-    V2 p = square_to_uniform_disk_concentric(s);
-    float z = 1.f - fmadd(p.y, p.y, p.x * p.x);
-    float f = std::sqrt(z + 1.f);
-    return {p.x * f, p.y * f, z};
+    float z = fmadd(-2.f, s.y, 1.f);
+    float r = safe_sqrt(fmadd(-z, z, 1.f));
+    float sn, cs;
+    sincos_(s.x * (2.f * Pi), sn, cs);
+    return {r * cs, r * sn, z};
 }
 static inline float uniform_cone_pdf(float cos_cutoff) { return InvTwoPi / (1.f - cos_cutoff); }
 
@@ -167,6 +169,13 @@ struct Scene {
     std::vector<amvpt_emitter_desc> emitters;
     std::vector<Prim> prims;
     float emitter_pmf = 0.f;
+    /* non-uniform sampling weights: DiscreteDistribution (distr_1d.h:218-231, JIT compute_cdf) */
+    bool distr = false;
+    std::vector<float> cdf;       /* inclusive prefix sums of the weights (float) */
+    float distr_sum = 0.f, distr_norm = 0.f;
+    int environment = -1;         /* the constant emitter (Scene::m_environment), or -1 */
+    V3 bs_center{0, 0, 0};        /* ConstantBackgroundEmitter::m_bsphere after set_scene */
+    float bs_radius = 0.f;
 };
 
 /* PreliminaryIntersection */
@@ -366,17 +375,64 @@ struct DS {            /* DirectionSample3f */
     int emitter = -1;
 };
 
+/* SurfaceInteraction::emitter (interaction.h): the shape's area emitter, or the scene's
+ * environment emitter for a ray that left the scene */
 static int si_emitter(const Scene &sc, const SI &si) {
-    if (!si.valid()) return -1;
+    if (!si.valid()) return sc.environment;
     return sc.shapes[si.shape].emitter;
 }
 
-/* AreaLight::eval (area.cpp:82-88); masked vcall -> 0 when !active */
+/* AreaLight::eval (area.cpp:82-88), ConstantBackgroundEmitter::eval (constant.cpp:90-94);
+ * masked vcall -> 0 when !active */
 static Spec emitter_eval(const Scene &sc, int e, const SI &si, bool active) {
     if (e < 0 || !active) return sp(0.f);
     const amvpt_emitter_desc &ed = sc.emitters[e];
-    if (!(si.wi.z > 0.f)) return sp(0.f);
+    if (ed.type != AMVPT_EMITTER_CONSTANT && !(si.wi.z > 0.f)) return sp(0.f);
     return {ed.radiance[0], ed.radiance[1], ed.radiance[2]};
+}
+
+/* Scene::pdf_emitter (scene.cpp:245-250): the probability of picking emitter `i` */
+static float emitter_pick_pmf(const Scene &sc, uint32_t i) {
+    return sc.distr ? sc.emitters[i].sampling_weight * sc.distr_norm : sc.emitter_pmf;
+}
+
+/* DiscreteDistribution::sample (distr_1d.h:116-134, JIT predicate) with dr::binary_search over
+ * [0, n - 1]: iterations = floor(log2(n - 1)) + 1, middle = (start + end) >> 1, a true predicate
+ * moves start to min(middle + 1, end), a false one moves end to middle */
+static uint32_t distr_sample(const Scene &sc, float value) {
+    const uint32_t n = (uint32_t) sc.cdf.size();
+    const float sample = value * sc.distr_sum;
+    uint32_t start = 0, end = n - 1, it = 0;
+    if (end > 0) { uint32_t x = end; while (x) { ++it; x >>= 1; } }
+    for (uint32_t i = 0; i < it; ++i) {
+        const uint32_t middle = (start + end) >> 1;
+        const float c = sc.cdf[middle];
+        const bool cond = ((c < sample) || c == 0.f) && c != sc.distr_sum;
+        if (cond) start = std::min(middle + 1u, end);
+        else end = middle;
+    }
+    return start;
+}
+
+/* Scene::sample_emitter (scene.cpp:222-244): (index, weight, re-used sample) */
+static uint32_t sample_emitter(const Scene &sc, float &u, float &weight) {
+    const size_t n = sc.emitters.size();
+    weight = 1.f;
+    if (n < 2) return 0;
+    if (sc.distr) {
+        /* sample_reuse_pmf (distr_1d.h:201-215) */
+        const uint32_t index = distr_sample(sc, u);
+        const float pmf = sc.emitters[index].sampling_weight * sc.distr_norm;
+        const float cdf = index > 0 ? sc.cdf[index - 1] * sc.distr_norm : 0.f;
+        u = (u - cdf) / pmf;
+        weight = rcp(pmf);
+        return index;
+    }
+    float scaled = u * (float) n;
+    uint32_t index = std::min((uint32_t) scaled, (uint32_t) n - 1u);
+    weight = (float) n;
+    u = scaled - (float) index;
+    return index;
 }
 
 /* Shape::sample_direction (shape.cpp:360-377) / Sphere::sample_direction (sphere.cpp:234-309) */
@@ -464,24 +520,32 @@ static std::pair<DS, Spec> sample_emitter_direction(const Scene &sc, const SI &r
     Spec spec = sp(0.f);
     size_t n = sc.emitters.size();
     if (n == 0) return {ds, spec};
-    uint32_t index = 0;
     float weight = 1.f;
-    if (n >= 2) {
-        float scaled = sample.x * (float) n;
-        index = std::min((uint32_t) scaled, (uint32_t) n - 1u);
-        weight = (float) n;
-        sample.x = scaled - (float) index;
-    }
+    const uint32_t index = sample_emitter(sc, sample.x, weight);
     if (!active) return {ds, spec}; /* masked vcall: zeros */
     const amvpt_emitter_desc &ed = sc.emitters[index];
-    const Shape &s = sc.shapes[ed.shape];
-    /* AreaLight::sample_direction (area.cpp:117-167) */
-    ds = shape_sample_direction(s, ref.p, sample);
-    bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
     Spec rad{ed.radiance[0], ed.radiance[1], ed.radiance[2]};
-    spec = a ? rad / ds.pdf : sp(0.f);
+    if (ed.type == AMVPT_EMITTER_CONSTANT) {
+        /* ConstantBackgroundEmitter::sample_direction (constant.cpp:125-152) */
+        V3 d = square_to_uniform_sphere(sample);
+        float radius = std::max(sc.bs_radius, norm(ref.p - sc.bs_center)), dist = 2.f * radius;
+        ds.p = fmadd(d, dist, ref.p);
+        ds.n = -d;
+        ds.uv = sample;
+        ds.pdf = InvFourPi;
+        ds.delta = false;
+        ds.d = d;
+        ds.dist = dist;
+        spec = rad / ds.pdf;
+    } else {
+        /* AreaLight::sample_direction (area.cpp:117-167) */
+        const Shape &s = sc.shapes[ed.shape];
+        ds = shape_sample_direction(s, ref.p, sample);
+        bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
+        spec = a ? rad / ds.pdf : sp(0.f);
+    }
     ds.emitter = (int) index;
-    ds.pdf *= sc.emitter_pmf;
+    ds.pdf *= emitter_pick_pmf(sc, index);
     spec = spec * weight;
     bool act = ds.pdf != 0.f;
     if (act) {
@@ -495,11 +559,14 @@ static std::pair<DS, Spec> sample_emitter_direction(const Scene &sc, const SI &r
 static float pdf_emitter_direction(const Scene &sc, V3 refp, const DS &ds, bool active) {
     if (ds.emitter < 0 || !active) return 0.f;
     const amvpt_emitter_desc &ed = sc.emitters[ds.emitter];
+    const float pick = emitter_pick_pmf(sc, (uint32_t) ds.emitter);
+    /* ConstantBackgroundEmitter::pdf_direction (constant.cpp:154-159): uniform sphere */
+    if (ed.type == AMVPT_EMITTER_CONSTANT) return InvFourPi * pick;
     const Shape &s = sc.shapes[ed.shape];
     float dp = dot(ds.d, ds.n);
     bool a = dp < 0.f;
     float value = shape_pdf_direction(s, refp, ds);
-    return (a ? value : 0.f) * sc.emitter_pmf;
+    return (a ? value : 0.f) * pick;
 }
 
 /* --------------------------------------------------------------------- */
@@ -1018,7 +1085,7 @@ struct Renderer {
         Spec throughput = sp(1.f), result = sp(0.f);
         float eta = 1.f;
         uint32_t depth = 0;
-        bool valid_ray = false;
+        bool valid_ray = !P.hide_emitters && sc.environment >= 0;   /* mvpath_single.h:98, path.cpp:114 */
         SI prev_si; prev_si.t = 0.f; /* dr::zeros<Interaction3f> */
         float prev_bsdf_pdf = 1.f;
         bool prev_bsdf_delta = true;
@@ -1252,7 +1319,7 @@ struct Renderer {
         bool adapt_mask = false;
         if (P.max_depth == 0) return {false, adapt_mask};
         SampleData &p = S[0];
-        bool valid_ray = false;
+        bool valid_ray = !P.hide_emitters && sc.environment >= 0;   /* mvpath_multi.h:140 */
         ++verts;
         SI si = intersect(sc, p_ray);
         bool p_hit = si.valid();
@@ -1377,6 +1444,16 @@ bool build_scene(const amvpt_scene_desc *d, Scene &sc) {
             return false; /* Beckmann / anisotropic non-visible sampling: not on the implemented path */
     sc.emitters.assign(d->emitters, d->emitters + d->emitter_count);
     sc.emitter_pmf = sc.emitters.empty() ? 0.f : 1.f / (float) sc.emitters.size();
+    /* Scene::update_emitter_sampling_distribution (scene.cpp:100-119) */
+    for (auto &e : sc.emitters) sc.distr = sc.distr || e.sampling_weight != 1.f;
+    if (sc.distr) {
+        float acc = 0.f;
+        for (auto &e : sc.emitters) { acc += e.sampling_weight; sc.cdf.push_back(acc); }
+        sc.distr_sum = sc.cdf.back();
+        sc.distr_norm = rcp(sc.distr_sum);
+    }
+    for (uint32_t i = 0; i < d->emitter_count; ++i)
+        if (d->emitters[i].type == AMVPT_EMITTER_CONSTANT) sc.environment = (int) i;
     for (uint32_t i = 0; i < d->shape_count; ++i) {
         const amvpt_shape_desc &s = d->shapes[i];
         Shape sh;
@@ -1405,6 +1482,39 @@ bool build_scene(const amvpt_scene_desc *d, Scene &sc) {
             sc.prims.push_back({AMVPT_SHAPE_SPHERE, i, 0});
         }
         sc.shapes.push_back(std::move(sh));
+    }
+    if (sc.environment >= 0) {
+        /* ConstantBackgroundEmitter::set_scene (constant.cpp:73-88): the bounding sphere of the scene's
+         * bounding box (union of Shape::bbox: rectangle corners rectangle.cpp bbox(), mesh vertices,
+         * sphere center -+ radius), radius enlarged by (1 + RayEpsilon) */
+        V3 lo{Infinity, Infinity, Infinity}, hi{-Infinity, -Infinity, -Infinity};
+        bool any = false;
+        auto expand = [&](V3 p) {
+            lo = {std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z)};
+            hi = {std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z)};
+            any = true;
+        };
+        for (const Shape &sh : sc.shapes) {
+            if (sh.type == AMVPT_SHAPE_RECTANGLE) {
+                expand(xform_point_affine(sh.to_world, v3(-1.f, -1.f, 0.f)));
+                expand(xform_point_affine(sh.to_world, v3(1.f, -1.f, 0.f)));
+                expand(xform_point_affine(sh.to_world, v3(1.f, 1.f, 0.f)));
+                expand(xform_point_affine(sh.to_world, v3(-1.f, 1.f, 0.f)));
+            } else if (sh.type == AMVPT_SHAPE_MESH) {
+                for (size_t v = 0; v + 2 < sh.pos.size(); v += 3) expand(v3(sh.pos[v], sh.pos[v + 1], sh.pos[v + 2]));
+            } else {
+                expand(v3(sh.center[0] - sh.radius, sh.center[1] - sh.radius, sh.center[2] - sh.radius));
+                expand(v3(sh.center[0] + sh.radius, sh.center[1] + sh.radius, sh.center[2] + sh.radius));
+            }
+        }
+        if (any) {
+            sc.bs_center = (hi + lo) * .5f;
+            sc.bs_radius = norm(sc.bs_center - hi);
+            sc.bs_radius = std::max(RayEpsilon, sc.bs_radius * (1.f + RayEpsilon));
+        } else {
+            sc.bs_center = v3(0.f, 0.f, 0.f);
+            sc.bs_radius = RayEpsilon;
+        }
     }
     return true;
 }
@@ -1476,9 +1586,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
     Scene sc;
     if (!build_scene(sd, sc)) return 4;
     for (auto &e : sc.emitters)
-        if (e.sampling_weight != 1.f) return 4;
-    for (auto &e : sc.emitters)
-        if (sc.shapes[e.shape].type == AMVPT_SHAPE_MESH) return 4;
+        if (e.type == AMVPT_EMITTER_AREA && sc.shapes[e.shape].type == AMVPT_SHAPE_MESH) return 4;
     amvpt_params P = *params;
     uint32_t spp, spp_pp, n_passes;
     uint64_t L;

@@ -45,6 +45,7 @@ static inline bool isfinite_(float x) { return (f2u(x) & 0x7f800000u) != 0x7f800
 static const float Pi = 3.14159265358979323846f;
 static const float InvPi = 0.31830988618379067154f;
 static const float InvTwoPi = 0.15915494309189533577f;
+static const float InvFourPi = 0.07957747154594766788f;
 static const float Epsilon = 5.9604644775390625e-08f;       /* 2^-24 */
 static const float RayEpsilon = Epsilon * 1500.f;            /* math.h:18-23 */
 static const float ShadowEpsilon = RayEpsilon * 10.f;

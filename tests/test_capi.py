@@ -104,7 +104,8 @@ def _copy_scene(amvpt_mod, sd):
     return nd, shapes, bsdfs, ems
 
 
-@pytest.mark.parametrize("breakage", ["emitter_range", "emitter_pair", "face_index", "bsdf_range"])
+@pytest.mark.parametrize("breakage", ["emitter_range", "emitter_pair", "face_index", "bsdf_range",
+                                      "env_count", "env_shape", "negative_weight", "zero_weights"])
 def test_scene_create_rejects_malformed_descriptors(amvpt_mod, breakage):
     """Malformed C-ABI input is refused with AMVPT_ERR_INVALID before any device work:
     shape.emitter outside [-1, emitter_count), emitter.shape / shape.emitter disagreeing, mesh face
@@ -126,6 +127,22 @@ def test_scene_create_rejects_malformed_descriptors(amvpt_mod, breakage):
         faces[n - 1] = shapes[mesh].vertex_count
         keep.append(faces)
         shapes[mesh].faces = ctypes.cast(faces, ctypes.POINTER(ctypes.c_uint32))
+    elif breakage == "env_count":
+        nd.has_environment = 1               # claims a constant emitter the table does not hold
+    elif breakage == "env_shape":
+        env = (amvpt_mod.EmitterDesc * (nd.emitter_count + 1))(*[ems[i] for i in range(nd.emitter_count)])
+        env[nd.emitter_count].type = amvpt_mod.EMITTER_CONSTANT
+        env[nd.emitter_count].shape = 0      # a constant emitter attached to a shape
+        env[nd.emitter_count].sampling_weight = 1.0
+        keep.append(env)
+        nd.emitters = ctypes.cast(env, ctypes.POINTER(amvpt_mod.EmitterDesc))
+        nd.emitter_count += 1
+        nd.has_environment = 1
+    elif breakage == "negative_weight":
+        ems[0].sampling_weight = -1.0        # DiscreteDistribution: entries must be non-negative
+    elif breakage == "zero_weights":
+        for i in range(nd.emitter_count):
+            ems[i].sampling_weight = 0.0     # no probability mass
     else:
         shapes[0].bsdf = nd.bsdf_count
     h = ctypes.c_void_p()

@@ -95,10 +95,29 @@ def test_xml_defaults_and_overrides(amvpt_mod):
     assert "path" in s2.integrator_string().lower()
 
 
+def test_constant_emitter_loads(amvpt_mod):
+    """`constant` (constant.cpp:52-65): radiance defaults to 1, one per scene; `envmap` stays refused."""
+    s = amvpt_mod.load_string("<scene version='3.0.0'><emitter type='constant'>"
+                              "<float name='sampling_weight' value='2'/></emitter>"
+                              "<shape type='sphere'><float name='radius' value='2'/></shape>"
+                              "<sensor type='perspective'><film type='hdrfilm'><integer name='width' value='8'/>"
+                              "<integer name='height' value='8'/></film></sensor></scene>")
+    sd, _, _ = s.describe(0, 0, 0)
+    d = sd.contents
+    assert d.emitter_count == 1 and d.has_environment == 1
+    e = d.emitters[0]
+    assert e.type == amvpt_mod.EMITTER_CONSTANT and e.shape == -1
+    assert list(e.radiance) == [1.0, 1.0, 1.0] and e.sampling_weight == 2.0
+    with pytest.raises(RuntimeError, match="one environment"):
+        amvpt_mod.load_string("<scene version='3.0.0'><emitter type='constant'/><emitter type='constant'/></scene>")
+    with pytest.raises(RuntimeError, match="envmap"):
+        amvpt_mod.load_string("<scene version='3.0.0'><emitter type='envmap'/></scene>")
+
+
 def test_xml_errors_are_loud(amvpt_mod):
-    # environment emitters are outside the implemented path (DESIGN.md "Scope"): refused, never ignored
-    with pytest.raises(RuntimeError, match="[Ee]nvironment"):
-        amvpt_mod.load_string("<scene version='3.0.0'><emitter type='constant'/></scene>")
+    # plugins outside the implemented path (DESIGN.md "Scope") are refused, never ignored
+    with pytest.raises(RuntimeError):
+        amvpt_mod.load_string("<scene version='3.0.0'><emitter type='point'/></scene>")
     with pytest.raises(RuntimeError):
         amvpt_mod.load_string("<scene version='3.0.0'><shape type='nosuchshape'/></scene>")
     with pytest.raises(RuntimeError):
