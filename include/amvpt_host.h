@@ -50,6 +50,22 @@ int amvpt_host_render(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t s
                       int raw, float *out_host, amvpt_counters *counters);
 
 /*
+ * Integrator::render over n_devices GPUs of one node, one host thread per device:
+ * device devices[r] renders the lane range amvpt_host_lane_shard(L, r, n_devices) of every pass
+ * (L = lanes per pass, amvpt_plan) into its own RGBW ImageBlock; the blocks are summed onto
+ * devices[0] with one RCCL reduce (ncclReduce, sum, fp32, communicators from ncclCommInitAll) and
+ * developed there.  The adaptive fill's per-pass count exchange runs between the threads.  The
+ * image equals amvpt_host_render's up to float summation order.  Counters: lane statistics summed,
+ * times of the slowest device.
+ */
+int amvpt_host_render_multi(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t seed, uint32_t spp,
+                            int raw, const int *devices, int n_devices, float *out_host,
+                            amvpt_counters *counters);
+
+/* [begin, end) of rank's contiguous lane range (sizes differ by at most one; amvpt.dist.lane_shard) */
+void amvpt_host_lane_shard(uint64_t lanes, uint32_t rank, uint32_t world, uint64_t *begin, uint64_t *end);
+
+/*
  * The exact descriptors render() hands to the C-ABI (for the parity tests: the oracle
  * consumes the same scene, views and params).  Pointers stay valid until the scene is freed.
  */

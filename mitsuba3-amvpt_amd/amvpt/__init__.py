@@ -151,6 +151,11 @@ def host_lib():
         L.amvpt_host_film_info.argtypes = [ctypes.c_void_p, u32] + [ctypes.POINTER(u32)] * 4
         L.amvpt_host_render.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.POINTER(Counters)]
+        L.amvpt_host_render_multi.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.POINTER(Counters)]
+        L.amvpt_host_lane_shard.argtypes = [u64, u32, u32, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.amvpt_host_lane_shard.restype = None
         L.amvpt_host_describe.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.POINTER(ctypes.POINTER(SceneDesc)),
                                           ctypes.POINTER(ctypes.POINTER(ViewDesc)), ctypes.POINTER(Params)]
         L.amvpt_host_integrator_string.argtypes = [ctypes.c_void_p]
@@ -239,6 +244,27 @@ def render(scene, sensor=0, seed=0, spp=0, raw=False, counters=None):
     _check(scene._lib.amvpt_host_render(scene._h, sensor, seed, spp, 1 if raw else 0,
                                         out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cnt)), scene._lib)
     return out
+
+
+def render_multi(scene, devices, sensor=0, seed=0, spp=0, raw=False, counters=None):
+    """Integrator::render over several GPUs of this node (C++ threads, lane shards, one RCCL reduce of
+    the RGBW ImageBlocks onto devices[0]; amvpt_host_render_multi) -> numpy (H, W, C)."""
+    w, h, c, _ = scene.film_info(sensor)
+    _, _, p = scene.describe(sensor, seed, spp)
+    ch = (5 if p.film_alpha else 4) if raw else c
+    out = np.zeros((h, w, ch), dtype=np.float32)
+    cnt = counters if counters is not None else Counters()
+    devs = (ctypes.c_int * len(devices))(*devices)
+    _check(scene._lib.amvpt_host_render_multi(scene._h, sensor, seed, spp, 1 if raw else 0, devs, len(devices),
+                                              out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cnt)), scene._lib)
+    return out
+
+
+def host_lane_shard(n_lanes, rank, world):
+    """The C++ host's lane partition (amvpt_host_lane_shard), for checks against dist.lane_shard."""
+    b, e = u64(), u64()
+    host_lib().amvpt_host_lane_shard(n_lanes, rank, world, ctypes.byref(b), ctypes.byref(e))
+    return b.value, e.value
 
 
 def plan(params):

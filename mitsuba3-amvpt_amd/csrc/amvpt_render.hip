@@ -22,6 +22,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -2413,6 +2414,15 @@ static void gaussian_coeffs(float stddev, FilterCoeffs &f) {
     f.c[0] -= std::fmaf(x8, w1, w0);
 }
 
+/* roctx range over a host scope (the reference's ScopedPhase, profiler.h:20-110): the render,
+ * each pass and each chunk's stages show up on rocprofv3's marker trace (--marker-trace) */
+struct RoctxScope {
+    explicit RoctxScope(const char *name) { roctxRangePushA(name); }
+    ~RoctxScope() { roctxRangePop(); }
+    RoctxScope(const RoctxScope &) = delete;
+    RoctxScope &operator=(const RoctxScope &) = delete;
+};
+
 #define HIPCHK(x)                                                    \
     do {                                                             \
         hipError_t e_ = (x);                                         \
@@ -2593,6 +2603,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                          uint64_t lane_begin, uint64_t lane_end, float *film, void *stream,
                          amvpt_counters *counters, float *records, uint32_t record_pass) {
     if (!scene || !views || !params || !film) { set_error("amvpt_render: null argument"); return AMVPT_ERR_INVALID; }
+    RoctxScope range_render("amvpt_render");
     const amvpt_params &Pp = *params;
     hipStream_t st = (hipStream_t) stream;
     bool diffuse_spec = g_diffuse_spec;
@@ -2854,6 +2865,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     uint64_t adaptive_lanes = 0;
 
     for (uint32_t pass = 0; pass < n_passes; ++pass) {
+        RoctxScope range_pass("amvpt pass");
         P.seed_value = Pp.base_seed + (is_mv ? (spp_pp * pass + Pp.seed) : Pp.seed);
         P.record = (records && pass == record_pass) ? 1u : 0u;
         for (uint64_t c0 = lane_begin; c0 < lane_end; c0 += chunk) {
@@ -2867,19 +2879,27 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             for (int k = 0; k < kQPlanes; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
             B.cnt_out = cntA; B.cnt_in = cntB;
             T.mark(st);
-            if (G == 1) {
-                T.begin(AMVPT_K_RAYGEN, st);
-                hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
-                T.end(st);
-            } else {
-                kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, diff, T);
+            {
+                RoctxScope range_primary("amvpt primary vertex (raygen, visibility, camera selection, MIS)");
+                if (G == 1) {
+                    T.begin(AMVPT_K_RAYGEN, st);
+                    hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
+                    T.end(st);
+                } else {
+                    kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, diff, T);
+                }
             }
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);
             T.mark(st);
             /* suffix bounces: ping-pong A <-> B */
-            { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
+            {
+                RoctxScope range_suffix("amvpt shared suffix (extend, bounce, NEE)");
+                const amvpt_status rs_ = run_suffix(cn);
+                if (rs_ != AMVPT_OK) return rs_;
+            }
             T.mark(st);
+            RoctxScope range_splat("amvpt splat (ImageBlock::put)");
             const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
             T.begin(AMVPT_K_SPLAT, st);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
@@ -2892,6 +2912,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             HIPCHK(T.err);
         }
         if (do_fill) {
+            RoctxScope range_fill("amvpt adaptive fill");
             /* compact the pass's adapt_mask lanes in lane order, then n_adapt re-traces each */
             /* (hipcub counts in int: select in pieces of <= 2^30 lanes, appending) */
             uint64_t n_sel = 0;

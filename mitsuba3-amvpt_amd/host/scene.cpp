@@ -696,6 +696,11 @@ template <class F> static int guarded(F &&f) {
     }
 }
 
+/* guarded() for the other translation units of the host library (multi.cpp) */
+int amvpt_host_guarded_call(int (*fn)(void *), void *ctx) {
+    return guarded([&] { return fn(ctx); });
+}
+
 static std::map<std::string, std::string> defines_of(const char *const *k, const char *const *v, int n) {
     std::map<std::string, std::string> d;
     for (int i = 0; i < n; ++i) d[k[i]] = v[i];

@@ -113,3 +113,15 @@ def test_shard_arithmetic(amvpt_mod):
             assert max(e - b for b, e in spans) - min(e - b for b, e in spans) <= 1
     with pytest.raises(ValueError):
         adist.lane_shard(10, 2, 2)
+
+
+def test_host_lane_shard_matches_dist(amvpt_mod):
+    """The C++ host's multi-GPU partition (amvpt_host_lane_shard, used by amvpt_host_render_multi)
+    is the same contiguous lane_shard as the torch.distributed path's (amvpt.dist)."""
+    from amvpt import dist
+    for lanes in (0, 1, 7, 100, 4096 * 2048 * 16, 2 ** 27 + 13):
+        for world in (1, 2, 3, 8):
+            shards = [amvpt_mod.host_lane_shard(lanes, r, world) for r in range(world)]
+            assert shards == [dist.lane_shard(lanes, r, world) for r in range(world)]
+            assert shards[0][0] == 0 and shards[-1][1] == lanes
+            assert all(shards[r][1] == shards[r + 1][0] for r in range(world - 1))
