@@ -205,8 +205,10 @@ def main():
             "rmse_vs_oracle": rmse,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (Cornell box of util.py:551-685 on a %dx%d grid sensor; no external assets)"
-                    % (p.grid_x, p.grid_y),
+            "data": "synthetic (%s on a %dx%d grid sensor; no external assets)" % (
+                {"veach_grid.xml": "Veach-MIS-class scene: 4 GGX rough-conductor plates, 4 sphere lights",
+                 "cbox_mesh.xml": "Cornell box of util.py:551-685 as OBJ/PLY meshes (3.6 k triangles)"}.get(
+                    cfg["scene"], "Cornell box of util.py:551-685"), p.grid_x, p.grid_y),
             "config": {
                 "workload": "%s: %s, %d-view %dx%d per view (quilt %dx%d), %d spp%s (%d passes x %d), G=%d, sa_mis, "
                             "adaptive %d, max_depth 8, rr_depth 5, seed 0"
@@ -290,16 +292,19 @@ def kernel_bytes(c, G, C):
     pushed = min(lanes, suffix)           # paths that left the primary vertex (= paths that terminate)
     rec = c["record_bytes"] or 16         # lane records (4 x 16 B) + lane_out + view records (amvpt_counters)
     adapt = c["adaptive_lanes"]
-    nee = 64                              # NEE record (shadow ray 28 B + destination + throughput + contribution)
+    state = 80                            # path state: 5 float4 planes (store_state)
+    nee = 52                              # NEE record: origin + destination, light point + thr, thr + contribution
+    fused = c["kernel_launches"]["k_shadow"] == 0   # NEE traced inside k_bounce (brute-force scenes)
     return {
         "k_prim_hit": 16 * lanes,                                   # hit record out
         "k_prim_req": (16 + 48) * lanes,                            # hit in, visibility requests out
         "k_vis": (48 + G / 8.0) * lanes,                            # requests in (once), ballots out
-        "k_mv_primary": (16 + G / 8.0 + rec) * lanes + 96 * pushed,  # hit + ballots in, records + paths out
-        "k_raygen": 96 * (lanes if G == 1 else adapt),              # path state out
+        "k_mv_primary": (16 + G / 8.0 + rec) * lanes + state * pushed,  # hit + ballots in, records + paths out
+        "k_raygen": state * (lanes if G == 1 else adapt),           # path state out
         "k_extend": 48 * suffix,                                    # ray in, hit out
-        "k_bounce": 112 * suffix + 96 * (suffix - pushed) + 64 * shadow + 16 * pushed,
-        "k_shadow": 96 * shadow,                                    # NEE record in, result read-modify-write
+        # state + hit in; survivors' state out; terminated paths' result out; NEE records out (split)
+        "k_bounce": (state + 16) * suffix + state * (suffix - pushed) + 16 * pushed + (0 if fused else nee * shadow),
+        "k_shadow": (nee + 32) * shadow,                            # NEE record in, result read-modify-write
         "k_splat": rec * lanes + 16 * adapt,                        # records in (film: PMC WRITE_SIZE)
     }
 
