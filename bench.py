@@ -208,7 +208,7 @@ def main():
             "data": "synthetic (%s on a %dx%d grid sensor; no external assets)" % (
                 {"veach_grid.xml": "Veach-MIS-class scene: 4 GGX rough-conductor plates, 4 sphere lights",
                  "cbox_mesh.xml": "Cornell box of util.py:551-685 as OBJ/PLY meshes (3.6 k triangles)"}.get(
-                    cfg["scene"], "Cornell box of util.py:551-685"), p.grid_x, p.grid_y),
+                    scene_file, "Cornell box of util.py:551-685"), p.grid_x, p.grid_y),
             "config": {
                 "workload": "%s: %s, %d-view %dx%d per view (quilt %dx%d), %d spp%s (%d passes x %d), G=%d, sa_mis, "
                             "adaptive %d, max_depth 8, rr_depth 5, seed 0"

@@ -61,7 +61,7 @@ struct Box {
 struct BuildPrim { Box box; float c[3]; uint32_t idx; };
 
 /* Binary SAH tree as built (children of inner node i at left, left + 1). */
-struct BNode { Box box; uint32_t left_or_first, count; };
+struct BNode { Box box; uint32_t left_or_first, count, axis = 0; };
 
 /* SAH shape: leaves of up to g_bvh_max_leaf primitives are kept when the split is
  * not cheaper; a split costs g_bvh_trav_cost primitive tests per unit of area on top
@@ -128,7 +128,7 @@ struct Builder {
                 uint32_t mid = begin + n / 2;
                 uint32_t l = (uint32_t) nodes.size();
                 nodes.resize(nodes.size() + 2);
-                nodes[ni].left_or_first = l; nodes[ni].count = 0;
+                nodes[ni].left_or_first = l; nodes[ni].count = 0; nodes[ni].axis = 0;
                 build(l, begin, mid, depth + 1);
                 build(l + 1, mid, end, depth + 1);
                 return;
@@ -145,12 +145,17 @@ struct Builder {
         if (mid == begin || mid == end) mid = begin + n / 2;
         uint32_t l = (uint32_t) nodes.size();
         nodes.resize(nodes.size() + 2);
-        nodes[ni].left_or_first = l; nodes[ni].count = 0;
+        nodes[ni].left_or_first = l; nodes[ni].count = 0; nodes[ni].axis = (uint32_t) best_axis;
         build(l, begin, mid, depth + 1);
         build(l + 1, mid, end, depth + 1);
     }
-    /* depth-first pre-order with skip links (DNode) */
-    void flatten(uint32_t ni, std::vector<DNode> &out) const {
+    /*
+     * Depth-first pre-order with skip links (DNode), children in the order a ray of direction
+     * octant `oct` (bit a: negative along axis a) meets them: the lower child along the split
+     * axis first for a positive direction, the upper one first for a negative direction.  The
+     * skip links are local to the copy, so octant copy o is the array at o * n_nodes.
+     */
+    void flatten(uint32_t ni, std::vector<DNode> &out, uint32_t oct = 0, uint32_t base = 0) const {
         const BNode &bn = nodes[ni];
         const uint32_t at = (uint32_t) out.size();
         DNode d{};
@@ -158,10 +163,11 @@ struct Builder {
         d.first = bn.count ? bn.left_or_first : 0u;
         out.push_back(d);
         if (!bn.count) {
-            flatten(bn.left_or_first, out);
-            flatten(bn.left_or_first + 1, out);
+            const uint32_t near = (oct >> bn.axis) & 1u;
+            flatten(bn.left_or_first + near, out, oct, base);
+            flatten(bn.left_or_first + (near ^ 1u), out, oct, base);
         }
-        out[at].skip_count = ((uint32_t) out.size() & kNodeSkipMask) | (bn.count << kNodeCountShift);
+        out[at].skip_count = (((uint32_t) out.size() - base) & kNodeSkipMask) | (bn.count << kNodeCountShift);
     }
 };
 
@@ -488,6 +494,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
 
     std::vector<DNode> nodes;
     std::vector<DPrim> prims;
+    uint32_t oct_stride = 0;   /* nodes per octant copy (0: one copy) */
     if (bprims.empty()) {
         /* one inner node with an empty box: every ray misses it and skips to the end */
         DNode root{};
@@ -505,6 +512,17 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         if (nodes.size() > kNodeSkipMask) {
             set_error("BVH too large (more than 2^28 nodes)");
             return AMVPT_ERR_INVALID;
+        }
+        /* per-lane walks of BVHs that are neither wave-uniform nor LDS-staged read the copy of
+         * their ray's direction octant: nearest child first, so the closest hit shrinks the
+         * box-test range early (AMVPT_OCT_BVH=0: one copy, A/B) */
+        const char *e = std::getenv("AMVPT_OCT_BVH");
+        const uint32_t n0 = (uint32_t) nodes.size();
+        const uint64_t lds_b = (uint64_t) n0 * sizeof(DNode) + bprims.size() * sizeof(DPrim);
+        if (!(e && e[0] == '0') && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes && (uint64_t) n0 * 8 <= kNodeSkipMask) {
+            nodes.reserve((size_t) n0 * 8);
+            for (uint32_t o = 1; o < 8; ++o) b.flatten(0, nodes, o, o * n0);
+            oct_stride = n0;
         }
         prims.resize(bprims.size());
         for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
@@ -586,7 +604,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.vnrm = (const float *) p_vnrm;
     D.vuv = (const float *) p_vuv;
     D.faces = (const uint32_t *) p_faces;
-    D.n_nodes = (uint32_t) nodes.size();
+    D.n_nodes = oct_stride ? oct_stride : (uint32_t) nodes.size();
+    D.oct_stride = oct_stride;
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;
@@ -604,7 +623,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
                             tab_round(d->emitter_count * (uint32_t) sizeof(DEmitter));
         D.tab_bytes = tb <= kTabBytes ? tb : 0u;
     }
-    D.lds_bytes = (uint32_t) (nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim));
+    D.lds_bytes = (uint32_t) ((size_t) D.n_nodes * sizeof(DNode) + prims.size() * sizeof(DPrim));
     sc->n_nodes = D.n_nodes;
     sc->n_prims = (uint32_t) bprims.size();
     sc->all_diffuse = d->bsdf_count > 0;

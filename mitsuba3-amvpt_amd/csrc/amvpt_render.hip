@@ -125,13 +125,14 @@ struct Bufs {
     uint32_t *cnt_nee;
     float4 *vreq[3];      /* k_prim_req -> k_vis: (p, bits), (n, ap.x), (emitter point, ap.y) per lane */
     unsigned long long *occ; /* k_vis -> k_mv_primary: occlusion ballots, word (i >> 6) * G + slot */
+    uint4 *vreq_w;        /* groups > 16 views (G = 0 instances): request bits lo / hi, primary view per lane */
+    uint4 *lmask_w[2];    /* groups > 16 views: (valid lo, hi, indirect lo, hi), (wi.z > 0 lo, hi) per slot */
 };
 
 /* ------------------------------------------------------------------ */
 /* Scene staging                                                      */
 /* ------------------------------------------------------------------ */
 
-constexpr uint32_t kLdsSceneBytes = 48 * 1024;
 constexpr int kPrimBlock = 128;
 enum { F_PDF, F_JP, F_PDFM, F_WX, F_WY, F_WZ, VS_FIELDS };   /* k_mv_primary's per-view LDS state */
 constexpr int kVsFieldsDiff = 2;   /* all-diffuse scenes keep only F_PDF and F_JP in LDS */
@@ -187,6 +188,7 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
     sc.uniform = scene_uniform(S.n_nodes, mode);
+    sc.oct_stride = sc.uniform ? 0u : S.oct_stride;
     sc.nodes = S.nodes;
     sc.prims = S.prims;
     char *dst = lds;
@@ -198,6 +200,7 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
         for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) d4[i] = sn[i];
         for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) d4[nn + i] = spr[i];
         sc.nodes = (const DNode *) lds;
+        sc.oct_stride = 0;   /* only the first ordering is staged */
         sc.prims = (const DPrim *) (lds + (size_t) nn * 16);
         dst = lds + scene_lds_bytes(S, mode);
         sync = true;
@@ -1673,14 +1676,25 @@ AD PrimRay primary_raygen(const KParams &P, const DView *V, uint32_t i) {
     r.ray = sample_ray_idx(P, V, fmadd(r.sx, P.inv_w, -0.f), fmadd(r.sy, P.inv_h, -0.f), r.p_idx, r.apx, r.apy);
     return r;
 }
+/*
+ * Group sizes.  G = 2..16 are compile-time instances; G = 0 is the runtime instance for groups
+ * of 17..64 views (KParams::G): 64-bit per-view masks kept in their own planes (vreq_w,
+ * lmask_w), 64-thread primary blocks (the per-view LDS state grows with G), k_vis waves that
+ * walk several slots.
+ */
+constexpr uint32_t kMaxGWide = 64;
+template <int G> AD int group_size(const KParams &P) { return G ? G : (int) P.G; }
+template <int G> using VMask = typename std::conditional<G == 0, unsigned long long, uint32_t>::type;
+template <int G> AD VMask<G> vbit(int k) { return (VMask<G>) 1 << k; }
 /* view index of group slot k of a lane whose primary view is p_idx (mvpath_multi.h:31-38) */
-template <int G> AD uint32_t group_view(uint32_t p_idx, int k) {
-    const uint32_t max_idx = (uint32_t) G * (p_idx / (uint32_t) G + 1u), id = p_idx + (uint32_t) k;
-    return id < max_idx ? id : id - (uint32_t) G;
+AD uint32_t group_view_n(uint32_t Gn, uint32_t p_idx, int k) {
+    const uint32_t max_idx = Gn * (p_idx / Gn + 1u), id = p_idx + (uint32_t) k;
+    return id < max_idx ? id : id - Gn;
 }
+template <int G> AD uint32_t group_view(uint32_t p_idx, int k) { return group_view_n((uint32_t) G, p_idx, k); }
 /* k_vis's verdict for slot k of lane-order thread i (0: emitter shadow ray, k >= 1: view k) */
-template <int G> AD bool occluded(const Bufs &B, uint32_t i, int k) {
-    return (B.occ[(size_t) (i >> 6) * G + (uint32_t) k] >> (i & 63u)) & 1ull;
+AD bool occluded_n(const Bufs &B, uint32_t Gn, uint32_t i, int k) {
+    return (B.occ[(size_t) (i >> 6) * Gn + (uint32_t) k] >> (i & 63u)) & 1ull;
 }
 
 /*
@@ -1715,7 +1729,8 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.chunk_n) return;
     PrimRay pr = primary_raygen(P, V, i);
-    uint32_t bits = 0;
+    const int Gn = group_size<G>(P);
+    VMask<G> bits = 0;
     f3 p = mk(0.f, 0.f, 0.f), n = p, dsp = p;
     if (P.max_depth != 0) {
         const SI si = compute_si(sc, pr.ray, hit_of(B.hit[i]));
@@ -1736,38 +1751,60 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
         const bool reuse = !direct_em && !delta && p_hit && bsdf_smooth;
         const bool p_face = si.wi.z > 0.f;
 #pragma unroll 1
-        for (int k = 1; k < G; ++k) {
-            const Surf r = camera_sample_surface(V[group_view<G>(pr.p_idx, k)], si, reuse, pr.apx, pr.apy);
-            if (r.valid && (r.face == p_face) && r.Jp > 0.f) bits |= 1u << k;
+        for (int k = 1; k < Gn; ++k) {
+            const Surf r = camera_sample_surface(V[group_view_n((uint32_t) Gn, pr.p_idx, k)], si, reuse, pr.apx, pr.apy);
+            if (r.valid && (r.face == p_face) && r.Jp > 0.f) bits |= vbit<G>(k);
         }
         p = si.p; n = si.n; dsp = ds.p;
     }
-    bits |= pr.p_idx << 16;
-    B.vreq[0][i] = make_float4(p.x, p.y, p.z, bitsf(bits));
+    if (G == 0) {
+        B.vreq_w[i] = make_uint4((uint32_t) bits, (uint32_t) ((unsigned long long) bits >> 32), pr.p_idx, 0u);
+        bits = 0;
+    } else {
+        bits |= (VMask<G>) pr.p_idx << 16;
+    }
+    B.vreq[0][i] = make_float4(p.x, p.y, p.z, bitsf((uint32_t) bits));
     B.vreq[1][i] = make_float4(n.x, n.y, n.z, pr.apx);
     B.vreq[2][i] = make_float4(dsp.x, dsp.y, dsp.z, pr.apy);
 }
 
-/* one block = 64 lanes x G slots, wave k traces slot k of the block's 64 lanes */
+/* one block = 64 lanes x G slots, wave k traces slot k of the block's 64 lanes (G = 0: 16 waves,
+ * wave w traces slots w, w + 16, ... of the runtime group size) */
+template <int G> constexpr int vis_waves() { return G ? G : 16; }
 template <int G, bool kUni>
-__global__ void __launch_bounds__(64 * G) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+__global__ void __launch_bounds__(64 * vis_waves<G>()) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
-    const int k = (int) (threadIdx.x >> 6);
+    const int Gn = group_size<G>(P);
     const uint32_t i = blockIdx.x * 64u + (threadIdx.x & 63u);
-    bool occ = false;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), nn = a, d = a;
+    VMask<G> bits = 0;
+    uint32_t p_idx = 0;
     if (i < P.chunk_n) {
-        const float4 a = B.vreq[0][i];
-        const uint32_t bits = fbits(a.w);
-        if ((bits >> k) & 1u) {
-            const float4 nn = B.vreq[1][i], d = B.vreq[2][i];
-            const f3 target = k == 0 ? mk(d.x, d.y, d.z) : camera_point(V[group_view<G>(bits >> 16, k)], nn.w, d.w);
-            occ = trace_any<kUni>(sc, spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target));
+        a = B.vreq[0][i];
+        if (G == 0) {
+            const uint4 w = B.vreq_w[i];
+            bits = (VMask<G>) (((unsigned long long) w.y << 32) | w.x);
+            p_idx = w.z;
+        } else {
+            bits = fbits(a.w);
+            p_idx = (uint32_t) bits >> 16;
         }
     }
-    const unsigned long long m = __ballot(occ);
-    if ((threadIdx.x & 63u) == 0u) B.occ[(size_t) blockIdx.x * G + (uint32_t) k] = m;
+    /* G > 0: exactly one slot per wave (block = 64 x G threads), a straight-line body */
+#pragma unroll 1
+    for (int k = (int) (threadIdx.x >> 6); G ? true : k < Gn; k += vis_waves<G>()) {
+        bool occ = false;
+        if (i < P.chunk_n && ((bits >> k) & 1u)) {
+            nn = B.vreq[1][i]; d = B.vreq[2][i];
+            const f3 target = k == 0 ? mk(d.x, d.y, d.z) : camera_point(V[group_view_n((uint32_t) Gn, p_idx, k)], nn.w, d.w);
+            occ = trace_any<kUni>(sc, spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target));
+        }
+        const unsigned long long m = __ballot(occ);
+        if ((threadIdx.x & 63u) == 0u) B.occ[(size_t) blockIdx.x * Gn + (uint32_t) k] = m;
+        if (G) break;
+    }
 }
 
 /* ------------------------------------------------------------------ */
@@ -1835,15 +1872,18 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * own (cosine_hemisphere(rand_2) whatever wi), so the per-view state reduces to F_PDF,
  * F_JP and one sign bit per view -- same values, a third of the LDS per thread.
  */
+template <int G> constexpr int prim_block() { return G ? kPrimBlock : 64; }   /* G = 0: LDS state grows with G */
 template <int G, bool kTab, bool kDiff>
-__global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+__global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    constexpr int kPB = prim_block<G>();
+    const int Gn = group_size<G>(P);
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     const uint32_t vs_off = kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u;
     SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
-    /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPrimBlock] */
+    /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPB] */
     float *const vs = reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
-#define VSF(f, k) vs[((f) * G + (k)) * kPrimBlock]
+#define VSF(f, k) vs[((f) * Gn + (k)) * kPB]
 #if AMVPT_PRIM_SLOT_ORDER
     /* threads run in slot order (a wave = 64 pixels of one sample, see slot_lane), so every
      * record store of a wave is 64 contiguous slots; the hit and the ballots are read at the
@@ -1865,9 +1905,9 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         /* every global load first: a load issued after the record stores would wait
          * for them (vmcnt counts loads and stores in issue order) */
         const float4 hitv = B.hit[i];
-        uint32_t occm = 0;   /* bit k: k_vis found slot k occluded */
+        VMask<G> occm = 0;   /* bit k: k_vis found slot k occluded */
 #pragma unroll
-        for (int k = 0; k < G; ++k) occm |= occluded<G>(B, i, k) ? (1u << k) : 0u;
+        for (int k = 0; k < Gn; ++k) occm |= occluded_n(B, (uint32_t) Gn, i, k) ? vbit<G>(k) : 0u;
         const uint32_t n = P.chunk_n;
         const PrimRay pr = primary_raygen(P, V, i);
         Pcg rng = pr.rng;
@@ -1878,8 +1918,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
          * (bsdf value, flags) per view.  Splat positions are not stored: k_splat_multi recomputes
          * them from the hit point (camera_uv) and the lane's jitter. */
         float *const vw = reinterpret_cast<float *>(B.vrec);
-        float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) G * n;
-        auto view_of = [&](int k) -> uint32_t { return group_view<G>(p_idx, k); };
+        float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
+        auto view_of = [&](int k) -> uint32_t { return group_view_n((uint32_t) Gn, p_idx, k); };
         auto put_view = [&](int k, float w, C3 res, C3 bv, uint32_t vf) {
             const size_t o = (size_t) k * n + slot;
             if (kDiff) {
@@ -1889,14 +1929,15 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 vB[o] = make_float4(bv.r, bv.g, bv.b, bitsf(vf));
             }
         };
-        uint32_t vmask = 0, imask = 0;   /* bit k: view k valid / indirect */
+        VMask<G> vmask = 0, imask = 0;   /* bit k: view k valid / indirect */
         float w0 = 1.f;                  /* slot 0's splat weight */
         C3 R0 = c3(0.f);                 /* slot 0's result: emission + direct light */
         C3 Dp = c3(0.f);                 /* kDiff: direct light through a valid view k >= 1 */
         C3 Bv = c3(0.f);                 /* kDiff: BSDF value of every indirect view */
         f3 hp = mk(0.f, 0.f, 0.f);       /* primary hit point (reprojection in the splat) */
         bool records_done = false, reuse_l = false, direct_l = false;
-        uint32_t nf_bits = 0, smask = 0;   /* kDiff: non-finite emis_mis channels, wi_k.z > 0 views */
+        uint32_t nf_bits = 0;   /* kDiff: non-finite emis_mis channels */
+        VMask<G> smask = 0;     /* kDiff: wi_k.z > 0 views */
 
         /* ---- sample_multi (mvpath_multi.h:130-369) ---- */
         bool valid_ray = P.valid_ray0 != 0 && P.max_depth != 0, adapt_mask = false;
@@ -1952,7 +1993,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 vmask |= p_hit ? 1u : 0u;
                 imask |= p_hit ? 1u : 0u;
                 const f3 wo_r0 = reflect_l(si.wi);
-                uint32_t wpos = p_face ? 1u : 0u;   /* kDiff: bit k = (wi_k.z > 0) */
+                VMask<G> wpos = p_face ? 1u : 0u;   /* kDiff: bit k = (wi_k.z > 0) */
                 if (!kDiff) {
                     VSF(F_WX, 0) = si.wi.x; VSF(F_WY, 0) = si.wi.y; VSF(F_WZ, 0) = si.wi.z;
                     VSF(F_PDFM, 0) = bd.diffuse ? 1.f : (P.fast_mis ? sqr(normalize(si.wi + wo_r0).z)
@@ -1971,7 +2012,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                 };
                 float n_direct = 1.f, n_indir = 2.f;
 #pragma unroll 1
-                for (int k = 1; k < G; ++k) {
+                for (int k = 1; k < Gn; ++k) {
                     Surf r = camera_sample_surface(V[view_of(k)], si, bd.reuse, apx, apy);
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
@@ -1988,7 +2029,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                         VSF(F_PDFM, k) = pdfM;
                         pdf_Mat = mat_pdf(wik, pdfM, valid);
                     } else {
-                        wpos |= wik.z > 0.f ? (1u << k) : 0u;
+                        wpos |= wik.z > 0.f ? vbit<G>(k) : 0u;
                     }
                     float J = r.Jp * iJp0;
                     float pdf_J = J > 1.f ? rcp(J) : J;
@@ -2014,8 +2055,8 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     /* kDiff: a valid view's sample is the primary's (same type, same wo) */
                     (void) replace;
                     n_indir += (float) indirect;
-                    vmask |= valid ? (1u << k) : 0u;
-                    imask |= indirect ? (1u << k) : 0u;
+                    vmask |= valid ? vbit<G>(k) : 0u;
+                    imask |= indirect ? vbit<G>(k) : 0u;
                 }
                 direct_pdf /= n_direct;
                 const float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
@@ -2044,7 +2085,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                  *      the multi-view mixture pdf (mvpath_multi.h:245-317) ---- */
                 float n_ind = 0.f, pdf = 0.f;
 #pragma unroll 1
-                for (int k = 0; k < G; ++k) {
+                for (int k = 0; k < Gn; ++k) {
                     const bool vk = (vmask >> k) & 1u;
                     const float Jpk = VSF(F_JP, k);
                     const float iJpk = k == 0 ? iJp0 : (vk ? rcp(Jpk) : 0.f);
@@ -2062,7 +2103,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     float acc = 0.f;
                     if (!kDiff && cond && !bd.diffuse) {
 #pragma unroll 1
-                        for (int j = 1; j < G; ++j) {
+                        for (int j = 1; j < Gn; ++j) {
                             if (j == k) continue;
                             float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
                             f3 worj = reflect_l(mk(VSF(F_WX, j), VSF(F_WY, j), VSF(F_WZ, j)));
@@ -2073,7 +2114,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                         }
                     } else {
 #pragma unroll 1
-                        for (int j = 1; j < G; ++j) {
+                        for (int j = 1; j < Gn; ++j) {
                             if (j == k) continue;
                             float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
                             acc = fmadd(VSF(F_PDF, j), pdf_J, acc);
@@ -2112,7 +2153,7 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
                     bv = csel(valid, bv, c3(0.f));
                     pdf += bp;
                     n_ind += (float) valid;
-                    if (!valid) imask &= ~(1u << k);
+                    if (!valid) imask &= ~vbit<G>(k);
                     if (k == 0) w0 = wk;
                     else put_view(k, wk, res, bv, (vk ? VF_VALID : 0u) | (valid ? VF_INDIRECT : 0u));
                     if (k == 0 && !kDiff) Bv = bv;   /* slot 0's (bsdf value), stored with slot 0 below */
@@ -2123,14 +2164,14 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
             } else {
                 vmask |= p_hit ? 1u : 0u;
 #pragma unroll 1
-                for (int k = 1; k < G; ++k) {
+                for (int k = 1; k < Gn; ++k) {
                     Surf r = camera_sample_surface(V[view_of(k)], si, reuse, apx, apy);
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
                         valid = !((occm >> k) & 1u);
                     }
-                    vmask |= valid ? (1u << k) : 0u;
+                    vmask |= valid ? vbit<G>(k) : 0u;
                 }
                 float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
                 R0 = emitted;
@@ -2172,16 +2213,21 @@ __global__ void __launch_bounds__(kPrimBlock, AMVPT_PRIM_WAVES) k_mv_primary(KPa
         }
         const uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) |
                                 (should_mis ? LF_MIS : 0u) | (reuse_l ? LF_REUSE : 0u) | (direct_l ? LF_DIRECT : 0u) |
-                                (nf_bits << 8) | (smask << 16);
+                                (nf_bits << 8) | (G ? (uint32_t) smask << 16 : 0u);
         B.lrec[0][slot] = make_float4(R0.r, R0.g, R0.b, pdfW);
         B.lrec[1][slot] = make_float4(Dp.r, Dp.g, Dp.b, bitsf(lflags));
-        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(vmask | (imask << 16)));
+        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(G ? (uint32_t) (vmask | (imask << 16)) : 0u));
+        if (G == 0) {
+            const unsigned long long vm = vmask, im = imask, sm = smask;
+            B.lmask_w[0][slot] = make_uint4((uint32_t) vm, (uint32_t) (vm >> 32), (uint32_t) im, (uint32_t) (im >> 32));
+            B.lmask_w[1][slot] = make_uint4((uint32_t) sm, (uint32_t) (sm >> 32), 0u, 0u);
+        }
         B.lrec[3][slot] = make_float4(hp.x, hp.y, hp.z, 0.f);
         /* slot 0 (generic: its bsdf value rides in L2), and the views the MIS loop did not write */
         put_view(0, w0, R0, Bv, (vmask & 1u ? VF_VALID : 0u) | (imask & 1u ? VF_INDIRECT : 0u));
         if (!records_done) {
 #pragma unroll 1
-            for (int k = 1; k < G; ++k)
+            for (int k = 1; k < Gn; ++k)
                 put_view(k, P.max_depth != 0 ? 1.f : 0.f, c3(0.f), c3(0.f), ((vmask >> k) & 1u) ? VF_VALID : 0u);
         }
     }
@@ -2221,8 +2267,15 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     const uint32_t n = P.chunk_n;
     float4 l0 = make_float4(0.f, 0.f, 0.f, 0.f), l1 = l0, l2 = l0, l3 = l0, lo = l0;
     if (ok) { l0 = B.lrec[0][slot]; l1 = B.lrec[1][slot]; l2 = B.lrec[2][slot]; l3 = B.lrec[3][slot]; lo = B.lane_out[slot]; }
-    const uint32_t lflags = fbits(l1.w), vmask = fbits(l2.w) & 0xffffu, imask = fbits(l2.w) >> 16;
-    const uint32_t smask = lflags >> 16;
+    const int Gn = group_size<G>(P);
+    const uint32_t lflags = fbits(l1.w);
+    VMask<G> vmask = fbits(l2.w) & 0xffffu, imask = fbits(l2.w) >> 16, smask = lflags >> 16;
+    if (G == 0 && ok) {
+        const uint4 m0 = B.lmask_w[0][slot], m1 = B.lmask_w[1][slot];
+        vmask = (VMask<G>) (((unsigned long long) m0.y << 32) | m0.x);
+        imask = (VMask<G>) (((unsigned long long) m0.w << 32) | m0.z);
+        smask = (VMask<G>) (((unsigned long long) m1.y << 32) | m1.x);
+    }
     const float qnan = __builtin_nanf("");
     /* cfma(0, emis_mis, 0) of a valid view whose wi.z <= 0 (kDiff, see k_mv_primary) */
     const C3 Dn = {(lflags & 0x100u) ? qnan : 0.f, (lflags & 0x200u) ? qnan : 0.f, (lflags & 0x400u) ? qnan : 0.f};
@@ -2252,10 +2305,10 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         p_idx = sensor_index(P, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f));
     }
     const float *const vw = reinterpret_cast<const float *>(B.vrec);
-    const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) G * n;
+    const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
     unsigned long long splats = 0, fallback = 0, nonfinite = 0, negative = 0;
 #pragma unroll 1
-    for (int k = 0; k < G; ++k) {
+    for (int k = 0; k < Gn; ++k) {
         const size_t o = (size_t) k * n + slot;
         float weight = 0.f;
         bool valid = false;
@@ -2263,7 +2316,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         float x = sx, y = sy;
         if (k > 0) {
             /* reprojected position in view k (camera_sample_surface, inactive -> 0) + quilt offset */
-            const uint32_t id = group_view<G>(p_idx, k);
+            const uint32_t id = group_view_n((uint32_t) Gn, p_idx, k);
             float ux = 0.f, uy = 0.f;
             view_uv(V, id, hp, apx, apy, ux, uy);
             x = reuse ? ux : 0.f;
@@ -2311,7 +2364,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         put(x, y, vals, valid, k == 0, k & 1, &fallback);
         splats += valid ? 1 : 0;
         if (ok && P.record) {
-            float *rr = B.records + ((size_t) i * G + k) * 8;
+            float *rr = B.records + ((size_t) i * Gn + k) * 8;
             rr[0] = x; rr[1] = y; rr[2] = v.r; rr[3] = v.g; rr[4] = v.b; rr[5] = alpha; rr[6] = weight;
             rr[7] = valid ? 1.f : 0.f;
         }
@@ -2545,12 +2598,14 @@ static void launch_bounce(bool tab, bool diff, int nee_walk, dim3 grid, size_t l
 #undef AMVPT_BOUNCE
 }
 
+template <int G> static int group_size_host(const KParams &P) { return G ? G : (int) P.G; }
 /* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
 template <int G>
 static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
                            const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T) {
-    const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPrimBlock - 1) / kPrimBlock);
-    const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * G * kPrimBlock * sizeof(float);
+    constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
+    const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
+    const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
     T.begin(AMVPT_K_PRIM_HIT, st);
     if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
@@ -2562,14 +2617,14 @@ static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStrea
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
     T.end(st);
     T.begin(AMVPT_K_VIS, st);
-    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * G), lds_bvh, st, P, S, V, B);
+    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     T.end(st);
     T.begin(AMVPT_K_MV_PRIMARY, st);
-    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
-    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
-    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPrimBlock), lds_tab + lds_view, st, P, S, V, B);
+    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
     T.end(st);
 }
 template <int G>
@@ -2587,16 +2642,18 @@ typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams 
                            const Bufs &, bool, bool, bool, KTimer &);
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const DView *, const Bufs &, bool);
 /* group sizes 2..16: the per-view bit masks (k_prim_req's request bits below the view index at
- * bit 16, k_mv_primary's valid / indirect flags at bits k and 16 + k) hold 16 views */
-static const primary_fn kPrimary[] = {nullptr, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
+ * bit 16, k_mv_primary's valid / indirect flags at bits k and 16 + k) hold 16 views; entry 0 is
+ * the runtime instance for 17..64 views (64-bit masks in vreq_w / lmask_w) */
+static const primary_fn kPrimary[] = {launch_primary<0>, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>,
                                       launch_primary<9>, launch_primary<10>, launch_primary<11>, launch_primary<12>,
                                       launch_primary<13>, launch_primary<14>, launch_primary<15>, launch_primary<16>};
-static const splat_fn kSplat[] = {nullptr, nullptr, launch_splat<2>, launch_splat<3>, launch_splat<4>,
+static const splat_fn kSplat[] = {launch_splat<0>, nullptr, launch_splat<2>, launch_splat<3>, launch_splat<4>,
                                   launch_splat<5>, launch_splat<6>, launch_splat<7>, launch_splat<8>,
                                   launch_splat<9>, launch_splat<10>, launch_splat<11>, launch_splat<12>,
                                   launch_splat<13>, launch_splat<14>, launch_splat<15>, launch_splat<16>};
 constexpr uint32_t kMaxG = 16;
+static uint32_t dispatch_g(uint32_t G) { return G > kMaxG ? 0u : G; }
 constexpr uint64_t kSelectChunk = 1ull << 30;
 
 amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
@@ -2623,7 +2680,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool is_mv = Pp.integrator == AMVPT_INTEGRATOR_MVPATH;
     const bool reuse = is_mv && Pp.sa_reuse && Pp.n_views > 1 && Pp.reuse_count != 1;
     const uint32_t G = reuse ? group_size(Pp) : 1;
-    if (G > kMaxG) { set_error("amvpt_render: group size > 16 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+    if (G > kMaxGWide) { set_error("amvpt_render: group size > 64 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
     if (!is_mv && n_passes > 1) { set_error("path: more than 2^32 lanes per frame"); return AMVPT_ERR_UNSUPPORTED; }
     if (Pp.multisensor && (Pp.grid_x == 0 || Pp.grid_y == 0 || Pp.film_width % Pp.grid_x || Pp.film_height % Pp.grid_y)) {
@@ -2725,8 +2782,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
     const uint64_t span = lane_end - lane_begin;
     const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
-    const bool diff_rec = scene->all_diffuse && diffuse_spec && G <= 16;   /* kDiff instances, compact view records */
-    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8;
+    const bool wide = G > kMaxG;   /* the runtime group-size instance (64-bit view masks) */
+    const bool diff_rec = scene->all_diffuse && diffuse_spec && !wide;   /* kDiff instances, compact view records */
+    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8 +
+                            (wide ? 48 : 0);
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
@@ -2791,6 +2850,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     B.cnt_nee = cntN;
     B.qcap = qcap;
     B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : 32) * G * chunk);
+    if (wide) {
+        B.vreq_w = (uint4 *) carve(16 * chunk);
+        for (int k = 0; k < 2; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
+    }
     B.film = film;
     B.records = records;
     B.stats = dstats;
@@ -2814,6 +2877,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
+    if (wide && lds_prim + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 163840) {
+        set_error("amvpt_render: per-view LDS state of this group size exceeds 160 KB");
+        return AMVPT_ERR_UNSUPPORTED;
+    }
     KTimer T;
     T.init(counters != nullptr);
     HIPCHK(T.err);
@@ -2886,7 +2953,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                     hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
                     T.end(st);
                 } else {
-                    kPrimary[G](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, diff, T);
+                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, diff, T);
                 }
             }
             HIPCHK(hipGetLastError());
@@ -2904,7 +2971,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             T.begin(AMVPT_K_SPLAT, st);
             if (G == 1 && P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
             else if (G == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_single<4>), sgrid, dim3(kSplatBlock), 0, st, P, B);
-            else kSplat[G](sgrid, st, P, dviews, B, diff_rec);
+            else kSplat[dispatch_g(G)](sgrid, st, P, dviews, B, diff_rec);
             T.end(st);
             T.mark(st);
             HIPCHK(hipGetLastError());

@@ -31,11 +31,10 @@ struct SceneRef {
     const DPrim *gprims;
     const DScene *g;
     uint32_t n_nodes;
+    uint32_t oct_stride;      /* per-lane walks: octant copy o of the nodes at nodes + o * oct_stride (0: one copy) */
     bool uniform;             /* small BVH: the kernels run their kUni = true instance (see trace_closest) */
 };
 
-/* BVHs up to this many nodes are traversed wave-uniformly. */
-constexpr uint32_t kUniformNodeLimit = 255;
 
 struct Hit { float t, u, v; int32_t prim; };
 
@@ -130,6 +129,13 @@ AD f3 safe_inv(f3 d) {
 
 AD uint32_t ufirst(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+/* the node array of the ray's direction octant (bit a = sign of d[a]; -0 counts as negative,
+ * any order gives the same hit) */
+AD const DNode *octant_nodes(const SceneRef &sc, f3 d) {
+    const uint32_t o = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+    return sc.nodes + (size_t) o * sc.oct_stride;
+}
+
 /* Scalar (s_load) reads of read-only scene records at a wave-uniform index: the
  * constant address space tells the backend the bytes are not written by the kernel. */
 template <typename T> AD T load_uniform(const T *base, uint32_t idx) {
@@ -200,9 +206,10 @@ template <bool kUni> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
         }
         return best;
     }
+    const DNode *const nodes = octant_nodes(sc, ray.d);
     uint32_t node = 0;
     while (node < sc.n_nodes) {
-        const DNode n = sc.nodes[node];
+        const DNode n = nodes[node];
         float tn;
         const bool hit = box_hit(n, ray.o, inv_d, tmax_box, tn);
         const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
@@ -252,6 +259,9 @@ template <bool kUni> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
         }
         return found;
     }
+    /* the first ordering: an any-hit walk gains nothing from near-first order (an unoccluded
+     * ray visits every box it crosses either way) and one copy keeps the cache footprint small
+     * (k_shadow on the 3.6 k-triangle mesh: 280 ms with it, 301 ms with the octant copies) */
     uint32_t node = 0;
     while (node < sc.n_nodes) {
         const DNode n = sc.nodes[node];

@@ -32,6 +32,9 @@ struct alignas(16) DNode {
     uint32_t skip_count;     /* bits 0..27: skip node index; bits 28..31: prim count (0 = inner node) */
 };
 constexpr uint32_t kNodeSkipMask = 0x0fffffffu, kNodeCountShift = 28, kMaxLeafPrims = 15;
+/* BVHs up to this many nodes are traversed wave-uniformly; per-lane walks stage nodes + prims
+ * in LDS up to kLdsSceneBytes. */
+constexpr uint32_t kUniformNodeLimit = 255, kLdsSceneBytes = 48 * 1024;
 
 struct alignas(16) DPrim {
     /* rect: rows 0..2 of to_object; tri: p0, p1 - p0, p2 - p0 (xyz); sphere: a = (center, radius) */
@@ -104,6 +107,7 @@ struct DScene {
     uint32_t lds_bytes;     /* nodes+prims footprint (LDS staging when small) */
     uint32_t n_bsdfs;
     uint32_t tab_bytes;     /* shapes+bsdfs+emitters footprint if <= kTabBytes (staged in LDS), else 0 */
+    uint32_t oct_stride;    /* != 0: nodes[] holds 8 direction-octant orderings of n_nodes each (amvpt_capi.cpp) */
 };
 
 } // namespace amvpt

@@ -309,6 +309,21 @@ def test_large_view_groups(gpu_ready, amvpt_mod, oracle, gx, gy, reuse):
     _check(amvpt_mod, oracle, s)
 
 
+@pytest.mark.parametrize("scene,gx,gy,reuse,res", [
+    ("cbox_grid.xml", 8, 4, 32, 12),    # the C5 light-field array as ONE group of 32 views
+    ("cbox_grid.xml", 8, 8, 64, 8),     # the largest group (64-bit view masks)
+    ("veach_grid.xml", 5, 4, 20, 12),   # glossy: per-view BSDF sampling + G x (G-1) BSDF pdfs
+], ids=["cbox_g32", "cbox_g64", "veach_g20"])
+def test_groups_above_16_views(gpu_ready, amvpt_mod, oracle, scene, gx, gy, reuse, res):
+    """Groups of 17..64 views (the reference has no cap, mvpath.cpp:192-217):
+    the runtime group-size instance with 64-bit view masks (vreq_w / lmask_w planes), 16-wave
+    k_vis blocks walking several slots each, 64-thread k_mv_primary blocks."""
+    s = amvpt_mod.load_file(os.path.join(SCENES, scene), res=res, spp=16, gx=gx, gy=gy, reuse=reuse)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert oracle.plan(p)["group"] == reuse
+    _check(amvpt_mod, oracle, s)
+
+
 CBOX_ENV = os.path.join(SCENES, "cbox_env.xml")
 VEACH_W = os.path.join(SCENES, "veach_grid.xml")
 
