@@ -179,6 +179,7 @@ def main():
                    "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
                    "k_prim_req": "k_prim_req<%d," % G}.get(dom, dom + "<")
     traffic, traffic_src = pmc_traffic(kernel_name, headline)
+    valu = pmc_valu(kms, kl, G, headline)
     # SURVEY 8(d) whole-pipeline byte model
     P = p.film_width * p.film_height
     B_sample = 336.0 * vbar + 120.0 * (G - 1) * hbar + 32.0 * P / samples_per_rank
@@ -238,6 +239,9 @@ def main():
                 "kernel_ms": {k: round(v, 3) for k, v in kms.items() if kl[k]},
                 "kernel_launches": {k: v for k, v in kl.items() if v},
                 "kernel_bytes": {k: int(v) for k, v in bytes_kernel.items() if kl[k]},
+                # VALU issue (the kernels are VALU/latency-bound, not HBM-bound): committed SQ PMC
+                # wave-instruction counts per launch / this run's launch time, vs 1228.8 G/s
+                "valu_issue": valu,
                 "pipeline_model": {"B_sample": round(B_sample, 1), "vbar": round(vbar, 4), "hbar": round(hbar, 4),
                                    "achieved_GBs": round(pipeline_gbs, 2),
                                    "frac": round(pipeline_gbs / HBM_PEAK_GBS, 5)},
@@ -324,6 +328,33 @@ def pmc_traffic(kernel_name, full_size):
         if key in k.replace(" ", ""):
             return int(v["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
     return None, os.path.relpath(files[-1], REPO)
+
+
+def pmc_valu(kms, kl, G, full_size):
+    """Per kernel: VALU wave-instructions per launch (newest profiles/r*_valu.json, made by
+    tools/pmc_valu.py from a SQ PMC pass of this bench at config M) over this run's mean launch
+    time, as a fraction of the chip's VALU issue peak.  None off config M."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_valu.json")))
+    if not files or not full_size:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    peak = d["peak_valu_ginst_s"]
+    sym = {"k_splat": "k_splat_multi<%d," % G, "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
+           "k_prim_req": "k_prim_req<%d," % G}
+    out = {"peak_Ginst_s": peak, "source": os.path.relpath(files[-1], REPO), "kernels": {}}
+    for k in kms:
+        if not kl[k]:
+            continue
+        key = sym.get(k, k + "<")
+        hit = [v for n, v in d["kernels"].items() if key in n]
+        if not hit:
+            continue
+        ginst = hit[0]["valu_insts_per_launch"] / (kms[k] / kl[k] * 1e-3) / 1e9
+        out["kernels"][k] = {"valu_per_wave": round(hit[0]["valu_per_wave"], 1), "achieved_Ginst_s": round(ginst, 1),
+                             "frac": round(ginst / peak, 4)}
+    return out
 
 
 def cpu_baseline(sd, vd, p, target_seconds):

@@ -66,11 +66,11 @@ void *g_exchange_ctx = nullptr;
 enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */ };
 template <int kWalk> AD Hit walk_closest(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_closest<kWalk == WALK_BRUTE>(sc, r);
-    return trace_closest<kWalk == WALK_UNI>(sc, r);
+    return trace_closest<kWalk == WALK_UNI, AMVPT_WALK_WW>(sc, r);
 }
 template <int kWalk> AD bool walk_any(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_any<kWalk == WALK_BRUTE>(sc, r);
-    return trace_any<kWalk == WALK_UNI>(sc, r);
+    return trace_any<kWalk == WALK_UNI, AMVPT_WALK_WW>(sc, r);
 }
 
 struct KParams {
@@ -1052,27 +1052,46 @@ AD int wave_max_dpp(int v) {
 }
 
 /* the wave's window flush: one global float atomic per touched film float, re-zeroing the
- * window (wave-local, in LDS order after the wave's own adds) */
+ * window (wave-local, in LDS order after the wave's own adds).  Four cells per lane per round:
+ * the four LDS reads go out together (one wait instead of four), and a cell's row comes from a
+ * float reciprocal with a one-step correction (e < 2^24), not an integer division. */
 template <int C>
 AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int rowlen = w.ww * C;
     const int n_elems = rowlen * w.wh;
+    const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
-    for (int e = (int) __lane_id(); e < n_elems; e += 64) {
-        const int cy = e / rowlen, r = e - cy * rowlen, cx = r / C, k = r - cx * C;
-        WinT *src = win + k * w.plane + cy * w.rs + cx;
-        const WinT d = *src;
+    const uint32_t film_row = P.W * (uint32_t) C;
+    constexpr int kU = 4;
+    for (int base = (int) __lane_id(); base < n_elems; base += 64 * kU) {
+        WinT d[kU];
+        WinT *src[kU];
+        uint32_t off[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            const int e = base + 64 * j;
+            int cy = (int) ((float) e * inv_rowlen);
+            cy -= (cy * rowlen > e) ? 1 : 0;
+            cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
+            const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
+            src[j] = win + k * w.plane + cy * w.rs + cx;
+            off[j] = (uint32_t) cy * film_row + (uint32_t) r;
+            d[j] = e < n_elems ? *src[j] : (WinT) 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
 #if AMVPT_WIN_FIXED
-        if (d != 0) {
-            *src = 0;
-            const float v = from_fixed(d);
+            if (d[j] != 0) {
+                *src[j] = 0;
+                const float v = from_fixed(d[j]);
 #else
-        if (__double_as_longlong(d) != 0ll) {
-            *src = 0.0;
-            const float v = (float) d;
+            if (__double_as_longlong(d[j]) != 0ll) {
+                *src[j] = 0.0;
+                const float v = (float) d[j];
 #endif
-            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + (size_t) cy * P.W * C + r, v);
+                if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + off[j], v);
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1476,8 +1495,10 @@ __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Buf
     }
 }
 
+/* waves per SIMD k_bounce's register allocation must allow: 5 (<= 96 VGPRs, from 101 at 4) hides
+ * more of the state loads and the fused NEE walk (109.7 vs 118.3 ms per config-M frame, A/B r02z) */
 #ifndef AMVPT_BOUNCE_WAVES
-#define AMVPT_BOUNCE_WAVES 4
+#define AMVPT_BOUNCE_WAVES 5
 #endif
 /*
  * kNee >= 0: the NEE shadow ray is traced inside k_bounce with walk kNee (the brute-force walks of
@@ -2246,9 +2267,9 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
 /* ------------------------------------------------------------------ */
 
 /* waves per SIMD the register allocation must allow: the 30-KB window admits 5 blocks (20 waves)
- * per CU */
+ * per CU, and 5 (<= 96 VGPRs) no longer spills (113.8 vs 117.9 ms per config-M frame, A/B r02z) */
 #ifndef AMVPT_SPLAT_WAVES
-#define AMVPT_SPLAT_WAVES 4
+#define AMVPT_SPLAT_WAVES 5
 #endif
 /* kRow: the row-reduced splat with wave windows (P.row_splat, RGBW), else the block window */
 template <int G, int C, bool kDiff, bool kRow>

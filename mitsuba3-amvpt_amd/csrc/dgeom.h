@@ -110,21 +110,50 @@ AD bool prim_hit(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
     return sphere_hit(p, r, t);
 }
 
-/* Slab test with inclusive bounds; boxes carry a relative pad from the builder. */
-AD bool box_hit(const DNode &n, f3 o, f3 inv_d, float tmax, float &tnear) {
-    float tx0 = (n.lo[0] - o.x) * inv_d.x, tx1 = (n.hi[0] - o.x) * inv_d.x;
-    float ty0 = (n.lo[1] - o.y) * inv_d.y, ty1 = (n.hi[1] - o.y) * inv_d.y;
-    float tz0 = (n.lo[2] - o.z) * inv_d.z, tz1 = (n.hi[2] - o.z) * inv_d.z;
+/*
+ * Slab test with inclusive bounds; boxes carry a relative pad from the builder (1e-4 of the
+ * scene's coordinate magnitude).  The test only has to be conservative -- it decides which
+ * primitives get the exact test, never a hit -- so it runs on a 1-ulp reciprocal and the fused
+ * form t = lo * inv - o * inv (one rounding of o * inv: an error far below the pad in t units
+ * for origins within 1000x the scene's extent); a NaN slab (0 * inf) drops out of the min/max
+ * and only widens the box.  AMVPT_EXACT_BOX=1 restores (lo - o) / d (A/B).
+ */
+#ifndef AMVPT_EXACT_BOX
+#define AMVPT_EXACT_BOX 0
+#endif
+struct BoxRay { f3 o, inv, oinv; };
+/* per-lane walk of the suffix kernels (k_extend, k_shadow): 2 speculative while-while, 1 plain
+ * while-while, 0 one loop (A/B) */
+#ifndef AMVPT_WALK_WW
+#define AMVPT_WALK_WW 2
+#endif
+AD float box_rcp(float d) {
+#if AMVPT_EXACT_BOX
+    return 1.f / (d != 0.f ? d : mulsign(1e-30f, d));
+#else
+    return __builtin_amdgcn_rcpf(fabs_(d) >= 1e-30f ? d : mulsign(1e-30f, d));
+#endif
+}
+AD BoxRay box_ray(const Ray &r) {
+    BoxRay b;
+    b.o = r.o;
+    b.inv = mk(box_rcp(r.d.x), box_rcp(r.d.y), box_rcp(r.d.z));
+    b.oinv = mk(r.o.x * b.inv.x, r.o.y * b.inv.y, r.o.z * b.inv.z);
+    return b;
+}
+AD bool box_hit(const DNode &n, const BoxRay &b, float tmax) {
+#if AMVPT_EXACT_BOX
+    float tx0 = (n.lo[0] - b.o.x) * b.inv.x, tx1 = (n.hi[0] - b.o.x) * b.inv.x;
+    float ty0 = (n.lo[1] - b.o.y) * b.inv.y, ty1 = (n.hi[1] - b.o.y) * b.inv.y;
+    float tz0 = (n.lo[2] - b.o.z) * b.inv.z, tz1 = (n.hi[2] - b.o.z) * b.inv.z;
+#else
+    float tx0 = fmaf(n.lo[0], b.inv.x, -b.oinv.x), tx1 = fmaf(n.hi[0], b.inv.x, -b.oinv.x);
+    float ty0 = fmaf(n.lo[1], b.inv.y, -b.oinv.y), ty1 = fmaf(n.hi[1], b.inv.y, -b.oinv.y);
+    float tz0 = fmaf(n.lo[2], b.inv.z, -b.oinv.z), tz1 = fmaf(n.hi[2], b.inv.z, -b.oinv.z);
+#endif
     float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
     float tm = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tnear = tmin;
     return tmin <= tm;
-}
-
-/* 1/d with zero components replaced by +-1e-30 so that (bound - o) * inv never is 0*inf */
-AD f3 safe_inv(f3 d) {
-    return {1.f / (d.x != 0.f ? d.x : mulsign(1e-30f, d.x)), 1.f / (d.y != 0.f ? d.y : mulsign(1e-30f, d.y)),
-            1.f / (d.z != 0.f ? d.z : mulsign(1e-30f, d.z))};
 }
 
 AD uint32_t ufirst(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -172,18 +201,17 @@ AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float 
  * Testing a primitive for a lane whose own box test failed cannot change that
  * lane's result (its box is padded and inclusive), so both walks are exact.
  */
-template <bool kUni> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
+template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
-    const f3 inv_d = safe_inv(ray.d);
+    const BoxRay br = box_ray(ray);
     float tmax_box = ray.maxt;
     if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
         uint32_t node = 0;
         while (node < nn) {
             const DNode n = load_uniform(sc.gnodes, node);
-            float tn;
-            const bool enter = wave_any(box_hit(n, ray.o, inv_d, tmax_box, tn));
+            const bool enter = wave_any(box_hit(n, br, tmax_box));
             const uint32_t skc = ufirst(n.skip_count);
             const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
             if (enter && count) {
@@ -207,42 +235,71 @@ template <bool kUni> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
         return best;
     }
     const DNode *const nodes = octant_nodes(sc, ray.d);
-    uint32_t node = 0;
-    while (node < sc.n_nodes) {
-        const DNode n = nodes[node];
-        float tn;
-        const bool hit = box_hit(n, ray.o, inv_d, tmax_box, tn);
-        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-        if (hit && count) {
-            for (uint32_t i = 0; i < count; ++i) {
-                const uint32_t pi = n.first + i;
-                const DPrim p = sc.prims[pi];
-                float t, u, v;
-                if (prim_hit(p, ray, t, u, v)) {
-                    if (t < best.t || (t == best.t && p.pad < best_orig)) {
-                        best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
-                        best_orig = p.pad;
-                        tmax_box = t;
-                    }
+    auto leaf_test = [&](uint32_t first, uint32_t count) {
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t pi = first + i;
+            const DPrim p = sc.prims[pi];
+            float t, u, v;
+            if (prim_hit(p, ray, t, u, v)) {
+                if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                    best_orig = p.pad;
+                    tmax_box = t;
                 }
             }
         }
+    };
+    const uint32_t nn = sc.n_nodes;
+    uint32_t node = 0;
+    if constexpr (kWW != 0) {
+    /* while-while (per-lane walks of large BVHs): the node loop runs until every lane holds a hit
+     * leaf or has finished, then the wave tests its leaves together -- the primitive code runs
+     * once per round for all lanes instead of once per divergent leaf visit.  kWW = 2: a lane
+     * that holds a leaf keeps stepping speculatively until the others have one (it stops at a
+     * second leaf and keeps it for the next round).  Incoherent rays only (the suffix walks):
+     * coherent primary / visibility waves lose with it (mesh k_vis 122 -> 138 ms). */
+    for (;;) {
+        uint32_t lf = 0, lc = 0;
+        bool stop = false;
+        for (;;) {
+            if (!wave_any(lc == 0u && node < nn)) break;
+            if (node < nn && !stop && (kWW == 2 || lc == 0u)) {
+                const DNode n = nodes[node];
+                const bool hit = box_hit(n, br, tmax_box);
+                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                if (hit && count) {
+                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                    else stop = true;   /* the second leaf: revisit it next round */
+                } else {
+                    node = hit ? node + 1 : skip;
+                }
+            }
+        }
+        if (!wave_any(lc != 0u)) break;
+        leaf_test(lf, lc);
+    }
+    return best;
+    }
+    while (node < nn) {
+        const DNode n = nodes[node];
+        const bool hit = box_hit(n, br, tmax_box);
+        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+        if (hit && count) leaf_test(n.first, count);
         node = (hit && !count) ? node + 1 : skip;
     }
     return best;
 }
 
 /* Any hit in [0, maxt] (Scene::ray_test); same two walks as trace_closest. */
-template <bool kUni> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
-    const f3 inv_d = safe_inv(ray.d);
+template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
+    const BoxRay br = box_ray(ray);
     if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
         bool found = false;
         uint32_t node = 0;
         while (node < nn) {
             const DNode n = load_uniform(sc.gnodes, node);
-            float tn;
-            const bool enter = wave_any(!found && box_hit(n, ray.o, inv_d, ray.maxt, tn));
+            const bool enter = wave_any(!found && box_hit(n, br, ray.maxt));
             const uint32_t skc = ufirst(n.skip_count);
             const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
             if (enter && count) {
@@ -262,19 +319,46 @@ template <bool kUni> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
     /* the first ordering: an any-hit walk gains nothing from near-first order (an unoccluded
      * ray visits every box it crosses either way) and one copy keeps the cache footprint small
      * (k_shadow on the 3.6 k-triangle mesh: 280 ms with it, 301 ms with the octant copies) */
+    auto leaf_any = [&](uint32_t first, uint32_t count) {
+        bool f = false;
+        for (uint32_t i = 0; i < count && !f; ++i) {
+            const DPrim p = sc.prims[first + i];
+            float t, u, v;
+            f = prim_hit(p, ray, t, u, v);
+        }
+        return f;
+    };
+    const uint32_t nn = sc.n_nodes;
     uint32_t node = 0;
-    while (node < sc.n_nodes) {
-        const DNode n = sc.nodes[node];
-        float tn;
-        const bool hit = box_hit(n, ray.o, inv_d, ray.maxt, tn);
-        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-        if (hit && count) {
-            for (uint32_t i = 0; i < count; ++i) {
-                const DPrim p = sc.prims[n.first + i];
-                float t, u, v;
-                if (prim_hit(p, ray, t, u, v)) return true;
+    if constexpr (kWW != 0) {
+    bool found = false;
+    for (;;) {
+        uint32_t lf = 0, lc = 0;
+        bool stop = false;
+        for (;;) {
+            if (!wave_any(!found && lc == 0u && node < nn)) break;
+            if (!found && node < nn && !stop && (kWW == 2 || lc == 0u)) {
+                const DNode n = sc.nodes[node];
+                const bool hit = box_hit(n, br, ray.maxt);
+                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                if (hit && count) {
+                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                    else stop = true;
+                } else {
+                    node = hit ? node + 1 : skip;
+                }
             }
         }
+        if (!wave_any(lc != 0u)) break;
+        if (lc) found = found || leaf_any(lf, lc);
+    }
+    return found;
+    }
+    while (node < nn) {
+        const DNode n = sc.nodes[node];
+        const bool hit = box_hit(n, br, ray.maxt);
+        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+        if (hit && count && leaf_any(n.first, count)) return true;
         node = (hit && !count) ? node + 1 : skip;
     }
     return false;
