@@ -876,7 +876,7 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
  * body would set the register allocation of the whole splat kernel) */
 template <int C, bool kRolled = false>
 AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, const float *wx,
-                 const float *wy, const float *vals, bool coalesce, unsigned long long *fallback) {
+                 const float *wy, const float *vals, bool coalesce, uint32_t *fallback) {
     const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
     const int plane = wn.plane;
     const bool in_win = cx0 >= wn.bx0 && cy0 >= wn.by0 && f.x0 + f.nx <= wn.bx0 + wn.ww && f.y0 + f.ny <= wn.by0 + wn.wh;
@@ -970,7 +970,7 @@ AD float union_weight(const KParams &P, float r, int x0, int cell, int lo, int h
 
 template <int C>
 AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, bool act,
-                    const float *vals, bool coalesce, unsigned long long *fallback) {
+                    const float *vals, bool coalesce, uint32_t *fallback) {
     const int x0c = max(f.x0, 0), y0c = max(f.y0, 0), x1 = f.x0 + f.nx, y1 = f.y0 + f.ny;
     const bool inw = x0c >= wn.bx0 && y0c >= wn.by0 && x1 <= wn.bx0 + wn.ww && y1 <= wn.by0 + wn.wh;
     const bool good = inw && win_fits<C>(vals);
@@ -1052,9 +1052,10 @@ AD int wave_max_dpp(int v) {
 }
 
 /* the wave's window flush: one global float atomic per touched film float, re-zeroing the
- * window (wave-local, in LDS order after the wave's own adds).  Four cells per lane per round:
- * the four LDS reads go out together (one wait instead of four), and a cell's row comes from a
- * float reciprocal with a one-step correction (e < 2^24), not an integer division. */
+ * window (wave-local, in LDS order after the wave's own adds).  A cell's row comes from a float
+ * reciprocal with a one-step correction (e < 2^24), not an integer division.  (Batching four
+ * cells per lane -- four LDS reads, one wait -- measured no faster and its live pointers pushed
+ * the 5-wave register budget into scratch.) */
 template <int C>
 AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1063,35 +1064,23 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
     const uint32_t film_row = P.W * (uint32_t) C;
-    constexpr int kU = 4;
-    for (int base = (int) __lane_id(); base < n_elems; base += 64 * kU) {
-        WinT d[kU];
-        WinT *src[kU];
-        uint32_t off[kU];
-#pragma unroll
-        for (int j = 0; j < kU; ++j) {
-            const int e = base + 64 * j;
-            int cy = (int) ((float) e * inv_rowlen);
-            cy -= (cy * rowlen > e) ? 1 : 0;
-            cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
-            const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
-            src[j] = win + k * w.plane + cy * w.rs + cx;
-            off[j] = (uint32_t) cy * film_row + (uint32_t) r;
-            d[j] = e < n_elems ? *src[j] : (WinT) 0;
-        }
-#pragma unroll
-        for (int j = 0; j < kU; ++j) {
+    for (int e = (int) __lane_id(); e < n_elems; e += 64) {
+        int cy = (int) ((float) e * inv_rowlen);
+        cy -= (cy * rowlen > e) ? 1 : 0;
+        cy += ((cy + 1) * rowlen <= e) ? 1 : 0;
+        const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
+        WinT *src = win + k * w.plane + cy * w.rs + cx;
+        const WinT d = *src;
 #if AMVPT_WIN_FIXED
-            if (d[j] != 0) {
-                *src[j] = 0;
-                const float v = from_fixed(d[j]);
+        if (d != 0) {
+            *src = 0;
+            const float v = from_fixed(d);
 #else
-            if (__double_as_longlong(d[j]) != 0ll) {
-                *src[j] = 0.0;
-                const float v = (float) d[j];
+        if (__double_as_longlong(d) != 0ll) {
+            *src = 0.0;
+            const float v = (float) d;
 #endif
-                if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + off[j], v);
-            }
+            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1100,7 +1089,7 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
 /* ImageBlock::put of a wave's samples through its own window (AMVPT_WAVE_WIN, row_splat) */
 template <int C>
 AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float py, const float *vals, bool valid,
-                 bool coalesce, unsigned long long *fallback) {
+                 bool coalesce, uint32_t *fallback) {
     Foot f;
     f.ok = false;
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
@@ -1138,7 +1127,7 @@ AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float p
  */
 template <int C>
 AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float px, float py, const float *vals,
-                  bool valid, bool coalesce, unsigned long long *fallback = nullptr) {
+                  bool valid, bool coalesce, uint32_t *fallback = nullptr) {
     Foot f;
     f.ok = false;
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
@@ -1200,8 +1189,7 @@ AD uint32_t lane_slot(const KParams &P, uint32_t lane) {
 /* ImageBlock::put's sample check (imageblock.cpp:180-204: warn_invalid / warn_negative): an active
  * sample with a non-finite channel, or (finite) with a channel below -1e-5, is counted
  * (amvpt_counters.nonfinite_samples / negative_samples) -- the reference logs a warning. */
-AD void check_sample(const KParams &P, const float *vals, bool active, unsigned long long &nf,
-                     unsigned long long &neg) {
+template <typename N> AD void check_sample(const KParams &P, const float *vals, bool active, N &nf, N &neg) {
     bool fin = true, nonneg = true;
     for (uint32_t k = 0; k < P.C; ++k) {
         fin = fin && finite_(vals[k]);
@@ -1790,14 +1778,56 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
 }
 
 /* one block = 64 lanes x G slots, wave k traces slot k of the block's 64 lanes (G = 0: 16 waves,
- * wave w traces slots w, w + 16, ... of the runtime group size) */
+ * wave w traces slots w, w + 16, ... of the runtime group size).  Wave-uniform walks with G > 0
+ * (vis_pairs): one block = 128 lanes, wave k traces slot k of both 64-lane groups at once
+ * (trace_any2_uni).  AMVPT_VIS_PAIRS = 0 turns that off (A/B). */
+#ifndef AMVPT_VIS_PAIRS
+#define AMVPT_VIS_PAIRS 1
+#endif
 template <int G> constexpr int vis_waves() { return G ? G : 16; }
+template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS && kUni && G != 0; }
+/* waves per SIMD the paired walk's register allocation must allow (0: no bound).  Measured at
+ * config M (r02ac): unbounded 96 VGPRs / 5 waves 69.3 ms, 6 waves (80 VGPRs, 12 B scratch)
+ * 63.5 ms, 8 waves (64 VGPRs, 52 B scratch) 74.1 ms; one ray per lane, 8 waves: 72.3 ms */
+#ifndef AMVPT_VIS_WAVES
+#define AMVPT_VIS_WAVES 6
+#endif
+template <int G, bool kUni> constexpr int vis_min_waves() { return vis_pairs<G, kUni>() ? AMVPT_VIS_WAVES : 0; }
 template <int G, bool kUni>
-__global__ void __launch_bounds__(64 * vis_waves<G>()) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+__global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>())) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
     const int Gn = group_size<G>(P);
+    if constexpr (vis_pairs<G, kUni>()) {
+        const int k = (int) (threadIdx.x >> 6);
+        Ray r[2];
+        bool act[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t i = blockIdx.x * 128u + 64u * (uint32_t) h + (threadIdx.x & 63u);
+            act[h] = false;
+            r[h] = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f};
+            if (i < P.chunk_n) {
+                const float4 a = B.vreq[0][i];
+                const uint32_t bits = fbits(a.w);
+                if ((bits >> k) & 1u) {
+                    const float4 nn = B.vreq[1][i], d = B.vreq[2][i];
+                    const f3 target = k == 0 ? mk(d.x, d.y, d.z) : camera_point(V[group_view<G>(bits >> 16, k)], nn.w, d.w);
+                    r[h] = spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target);
+                    act[h] = true;
+                }
+            }
+        }
+        bool occ0, occ1;
+        trace_any2_uni(sc, r[0], act[0], r[1], act[1], occ0, occ1);
+        const unsigned long long m0 = __ballot(occ0), m1 = __ballot(occ1);
+        if ((threadIdx.x & 63u) == 0u) {
+            B.occ[(size_t) (2u * blockIdx.x) * Gn + (uint32_t) k] = m0;
+            if ((2u * blockIdx.x + 1u) * 64u < P.chunk_n) B.occ[(size_t) (2u * blockIdx.x + 1u) * Gn + (uint32_t) k] = m1;
+        }
+        return;
+    }
     const uint32_t i = blockIdx.x * 64u + (threadIdx.x & 63u);
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), nn = a, d = a;
     VMask<G> bits = 0;
@@ -2278,7 +2308,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     if (kRow) wave_lds_init(reinterpret_cast<WaveLds<C> &>(L));
     else splat_lds_init(reinterpret_cast<SplatLds<C> &>(L));
     /* one put of this kernel's kind */
-    auto put = [&](float x, float y, const float *vals, bool valid, bool coalesce, int buf, unsigned long long *fb) {
+    auto put = [&](float x, float y, const float *vals, bool valid, bool coalesce, int buf, uint32_t *fb) {
         if constexpr (kRow) wave_put<C>(P, B.film, L, x, y, vals, valid, coalesce, fb);
         else block_put<C>(P, B.film, L, buf, x, y, vals, valid, coalesce, fb);
     };
@@ -2327,7 +2357,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     }
     const float *const vw = reinterpret_cast<const float *>(B.vrec);
     const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
-    unsigned long long splats = 0, fallback = 0, nonfinite = 0, negative = 0;
+    uint32_t splats = 0, fallback = 0, nonfinite = 0, negative = 0;   /* per lane, <= G each */
 #pragma unroll 1
     for (int k = 0; k < Gn; ++k) {
         const size_t o = (size_t) k * n + slot;
@@ -2638,7 +2668,9 @@ static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStrea
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
     T.end(st);
     T.begin(AMVPT_K_VIS, st);
-    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    constexpr bool kVisPairs = vis_pairs<G, true>();
+    const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
+    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     T.end(st);
     T.begin(AMVPT_K_MV_PRIMARY, st);

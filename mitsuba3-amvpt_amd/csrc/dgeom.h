@@ -365,6 +365,42 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
 }
 
 /*
+ * Two any-hit rays per lane on the wave-uniform walk (k_vis: the same view's visibility rays of
+ * two adjacent 64-lane groups, near-identical paths through the tree): the wave enters a node if
+ * any lane's first or second ray hits its box, so every node record is loaded and waited for
+ * once per two rays.  Lanes without a ray pass act = false (they count as found).  Exact for the
+ * same reason as trace_any: a primitive tested for a ray whose box test failed cannot hit it.
+ */
+AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
+    const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
+    const uint32_t nn = ufirst(sc.n_nodes);
+    f0 = !act0; f1 = !act1;
+    uint32_t node = 0;
+    while (node < nn) {
+        const DNode n = load_uniform(sc.gnodes, node);
+        const bool enter = wave_any((!f0 && box_hit(n, b0, r0.maxt)) || (!f1 && box_hit(n, b1, r1.maxt)));
+        const uint32_t skc = ufirst(n.skip_count);
+        const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
+        if (enter && count) {
+            const uint32_t first = ufirst(n.first);
+            for (uint32_t i = 0; i < count; ++i) {
+                const DPrim p = load_uniform(sc.gprims, first + i);
+                const uint32_t type = ufirst(p.type);
+                float t, u, v;
+                const bool h0 = prim_hit_u(p, type, r0, t, u, v);
+                const bool h1 = prim_hit_u(p, type, r1, t, u, v);
+                f0 = f0 || h0;
+                f1 = f1 || h1;
+            }
+            if (!wave_any(!f0 || !f1)) break;
+        }
+        node = (enter && !count) ? node + 1 : skip;
+    }
+    f0 = f0 && act0;
+    f1 = f1 && act1;
+}
+
+/*
  * Brute-force walks for tiny scenes (n_prims <= kBrutePrims, wave-uniform kernels only):
  * every primitive is tested in BVH order with the next record's scalar load issued
  * before the current test, so there are no dependent node loads and no box tests.
