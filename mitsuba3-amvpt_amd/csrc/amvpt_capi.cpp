@@ -289,10 +289,10 @@ static amvpt_status validate_scene(const amvpt_scene_desc *d) {
     }
     for (uint32_t i = 0; i < d->bsdf_count; ++i) {
         const amvpt_bsdf_desc &b = d->bsdfs[i];
-        if (b.type == AMVPT_BSDF_ROUGHCONDUCTOR &&
-            (b.distribution != AMVPT_MICROFACET_GGX || (!b.sample_visible && b.alpha_u != b.alpha_v))) {
-            set_error("roughconductor: only the GGX distribution (isotropic, or with visible-normal sampling) is implemented");
-            return AMVPT_ERR_UNSUPPORTED;
+        if (b.type == AMVPT_BSDF_ROUGHCONDUCTOR && b.distribution != AMVPT_MICROFACET_GGX &&
+            b.distribution != AMVPT_MICROFACET_BECKMANN) {
+            set_error("roughconductor: unknown microfacet distribution");
+            return AMVPT_ERR_INVALID;
         }
         if (b.type == AMVPT_BSDF_TWOSIDED) {
             for (int k = 0; k < 2; ++k) {

@@ -34,8 +34,8 @@
 #include <mutex>
 #include <type_traits>
 
+#include "internal.h"   /* the C-ABI enums (amvpt.h) before the device headers use them */
 #include "dbsdf.h"
-#include "internal.h"
 
 /* non-template kernels get internal linkage in the k_shadow translation unit (amvpt_shadow.hip) */
 #ifdef AMVPT_SHADOW_TU

@@ -44,32 +44,97 @@ AD C3 csel(bool m, C3 a, C3 b) { return {m ? a.r : b.r, m ? a.g : b.g, m ? a.b :
 struct BSample { f3 wo; float pdf, eta; uint32_t type; };
 AD BSample bs_zero() { return BSample{mk(0.f, 0.f, 0.f), 0.f, 0.f, 0u}; }
 
-/* ---------------- microfacet (GGX; Beckmann rejected at scene upload) ---------------- */
+/* ---------------- microfacet (microfacet.h:185-431): GGX and Beckmann ---------------- */
+constexpr float kInvSqrtPi = 0.56418958354775628695f;
 struct Mf {
     float au, av;
-    bool visible;
-    AD Mf(const DBsdf &b) : au(vmax(b.alpha_u, 1e-4f)), av(vmax(b.alpha_v, 1e-4f)), visible(b.sample_visible != 0) {}
+    bool visible, beckmann;
+    AD Mf(const DBsdf &b)
+        : au(vmax(b.alpha_u, 1e-4f)), av(vmax(b.alpha_v, 1e-4f)), visible(b.sample_visible != 0),
+          beckmann(b.distribution == AMVPT_MICROFACET_BECKMANN) {}
     AD float eval(f3 m) const {
-        float alpha_uv = au * av, ct = m.z;
-        float result = rcp(kPi * alpha_uv * sqr(sqr(m.x / au) + sqr(m.y / av) + sqr(m.z)));
+        float alpha_uv = au * av, ct = m.z, result;
+        if (beckmann) {
+            const float ct2 = sqr(ct);
+            result = exp_(-(sqr(m.x / au) + sqr(m.y / av)) / ct2) / (kPi * alpha_uv * sqr(ct2));
+        } else {
+            result = rcp(kPi * alpha_uv * sqr(sqr(m.x / au) + sqr(m.y / av) + sqr(m.z)));
+        }
         return result * ct > 1e-20f ? result : 0.f;
     }
     AD float smith_g1(f3 v, f3 m) const {
-        float xy = sqr(au * v.x) + sqr(av * v.y), ta2 = xy / sqr(v.z);
-        float result = 2.f / (1.f + dsqrt(1.f + ta2));
+        float xy = sqr(au * v.x) + sqr(av * v.y), ta2 = xy / sqr(v.z), result;
+        if (beckmann) {
+            /* rational approximation of the shadowing-masking function (microfacet.h:332-339) */
+            float a = rsqrt_(ta2), a_sqr = sqr(a);
+            result = a >= 1.6f ? 1.f : (3.535f * a + 2.181f * a_sqr) / (1.f + 2.276f * a + 2.577f * a_sqr);
+        } else {
+            result = 2.f / (1.f + dsqrt(1.f + ta2));
+        }
         if (xy == 0.f) result = 1.f;
         if (dot(v, m) * v.z <= 0.f) result = 0.f;
         return result;
     }
+    /* sample_visible_11 (microfacet.h:362-420) */
+    AD void visible_11(float cti, float u1, float u2, float &slx, float &sly) const {
+        if (beckmann) {
+            /* numerical inversion, three Newton steps */
+            float tan_theta_i = safe_sqrt(fnmadd(cti, cti, 1.f)) / cti;
+            float cot_theta_i = rcp(tan_theta_i);
+            float maxval = erf_(cot_theta_i);
+            u1 = vmax(vmin(u1, 1.f - 1e-6f), 1e-6f);
+            u2 = vmax(vmin(u2, 1.f - 1e-6f), 1e-6f);
+            float x = maxval - (maxval + 1.f) * erf_(dsqrt(-log_(u1)));
+            u1 *= 1.f + maxval + kInvSqrtPi * tan_theta_i * exp_(-sqr(cot_theta_i));
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                float slope = erfinv_(x),
+                      value = 1.f + x + kInvSqrtPi * tan_theta_i * exp_(-sqr(slope)) - u1,
+                      derivative = 1.f - slope * tan_theta_i;
+                x -= value / derivative;
+            }
+            slx = erfinv_(x);
+            sly = erfinv_(fmsub(2.f, u2, 1.f));
+            return;
+        }
+        float px, py;
+        disk_concentric(u1, u2, px, py);
+        float s = 0.5f * (1.f + cti);
+        py = lerp_(safe_sqrt(1.f - sqr(px)), py, s);
+        float x = px, y = py, z = safe_sqrt(1.f - fmadd(py, py, px * px));
+        float sti = safe_sqrt(1.f - sqr(cti));
+        float nrm = rcp(fmadd(sti, y, cti * z));
+        slx = fmsub(cti, y, sti * z) * nrm;
+        sly = x * nrm;
+    }
     AD void sample(f3 wi, float u1, float u2, f3 &m, float &pdf) const {
         if (!visible) {
-            float sin_phi, cos_phi;
-            sincos_c((2.f * kPi) * u2, sin_phi, cos_phi);
-            float alpha_2 = au * au;
-            float tan2 = alpha_2 * u1 / (1.f - u1);
-            float ct = rsqrt_(1.f + tan2), ct2 = sqr(ct);
-            float temp = 1.f + tan2 / alpha_2, ct3 = vmax(ct2 * ct, 1e-20f);
-            pdf = rcp(kPi * au * av * ct3 * sqr(temp));
+            /* azimuth: uniform (isotropic) or the tan inversion (anisotropic), then the
+             * distribution's elevation (microfacet.h:244-300) */
+            float sin_phi, cos_phi, alpha_2;
+            if (au == av) {
+                sincos_c((2.f * kPi) * u2, sin_phi, cos_phi);
+                alpha_2 = au * au;
+            } else {
+                float ratio = av / au, tmp = ratio * tan_((2.f * kPi) * u2);
+                cos_phi = rsqrt_(fmadd(tmp, tmp, 1.f));
+                cos_phi = mulsign(cos_phi, fabs_(u2 - .5f) - .25f);
+                sin_phi = cos_phi * tmp;
+                alpha_2 = rcp(sqr(cos_phi / au) + sqr(sin_phi / av));
+            }
+            float ct, ct2;
+            if (beckmann) {
+                ct = rsqrt_(fnmadd(alpha_2, log_(1.f - u1), 1.f));
+                ct2 = sqr(ct);
+                float ct3 = vmax(ct2 * ct, 1e-20f);
+                pdf = (1.f - u1) / (kPi * au * av * ct3);
+            } else {
+                float tan2 = alpha_2 * u1 / (1.f - u1);
+                ct = rsqrt_(1.f + tan2);
+                ct2 = sqr(ct);
+                float temp = 1.f + tan2 / alpha_2, ct3 = vmax(ct2 * ct, 1e-20f);
+                pdf = rcp(kPi * au * av * ct3 * sqr(temp));
+            }
             float st = dsqrt(1.f - ct2);
             m = mk(cos_phi * st, sin_phi * st, ct);
             return;
@@ -80,15 +145,8 @@ struct Mf {
         if (fabs_(st2) <= 4.f * kEps) { rx = 1.f; ry = 0.f; }
         else { rx = vmin(vmax(rx, -1.f), 1.f); ry = vmin(vmax(ry, -1.f), 1.f); }
         float sin_phi = ry, cos_phi = rx, cti = wp.z;
-        /* sample_visible_11, GGX branch */
-        float px, py;
-        disk_concentric(u1, u2, px, py);
-        float s = 0.5f * (1.f + cti);
-        py = lerp_(safe_sqrt(1.f - sqr(px)), py, s);
-        float x = px, y = py, z = safe_sqrt(1.f - fmadd(py, py, px * px));
-        float sti = safe_sqrt(1.f - sqr(cti));
-        float nrm = rcp(fmadd(sti, y, cti * z));
-        float slx = fmsub(cti, y, sti * z) * nrm, sly = x * nrm;
+        float slx, sly;
+        visible_11(cti, u1, u2, slx, sly);
         float sx = fmsub(cos_phi, slx, sin_phi * sly) * au, sy = fmadd(sin_phi, slx, cos_phi * sly) * av;
         m = normalize(mk(-sx, -sy, 1.f));
         pdf = eval(m) * smith_g1(wi, m) * absdot(wi, m) / wi.z;

@@ -69,6 +69,122 @@ AD void sincos_c(float x, float &s_out, float &c_out) {
     if (!(xa < kInf)) { s_out = __builtin_nanf(""); c_out = __builtin_nanf(""); }
 }
 
+/*
+ * exp / log / erf / erfinv / tan for the Beckmann distribution and anisotropic microfacet
+ * sampling (microfacet.h:185-431): Cephes expf / logf, a fitted erf (|x| < 1: x P(x^2), below 4:
+ * 1 - exp(-x^2) Q(1/x^2) / |x|, |error| < 2.1e-7), M. Giles' single-precision erfinv and
+ * tan = sin / cos -- the same operation sequences as the CPU parity checker's restatements, so
+ * the two agree bit for bit.
+ */
+AD float ldexp_(float y, int n) {
+    const int h = n / 2, l = n - h;
+    return (y * bitsf((uint32_t) (h + 127) << 23)) * bitsf((uint32_t) (l + 127) << 23);
+}
+AD float exp_(float x) {
+    if (x != x) return x;
+    if (x > 88.3762626647949f) return kInf;
+    if (x < -88.3762626647949f) return 0.f;
+    const float n = __builtin_floorf(fmadd(1.44269504088896341f, x, .5f));
+    float r = fnmadd(n, 0.693359375f, x);
+    r = fnmadd(n, -2.12194440e-4f, r);
+    float p = fmadd(r, 1.9875691500e-4f, 1.3981999507e-3f);
+    p = fmadd(p, r, 8.3334519073e-3f);
+    p = fmadd(p, r, 4.1665795894e-2f);
+    p = fmadd(p, r, 1.6666665459e-1f);
+    p = fmadd(p, r, 5.0000001201e-1f);
+    const float y = fmadd(p, r * r, r + 1.f);
+    return ldexp_(y, (int) n);
+}
+AD float log_(float x) {
+    if (x != x || x < 0.f) return __builtin_nanf("");
+    if (x == 0.f) return -kInf;
+    if (x == kInf) return kInf;
+    int e_adj = 0;
+    if (x < 1.17549435e-38f) { x *= 8388608.f; e_adj = -23; }
+    const uint32_t u = fbits(x);
+    int e = (int) ((u >> 23) & 0xffu) - 126 + e_adj;
+    float m = bitsf((u & 0x007fffffu) | 0x3f000000u);   /* [0.5, 1) */
+    if (m < 0.707106781186547524f) { e -= 1; m = m + m - 1.f; }
+    else m = m - 1.f;
+    const float z = m * m;
+    float p = fmadd(m, 7.0376836292e-2f, -1.1514610310e-1f);
+    p = fmadd(p, m, 1.1676998740e-1f);
+    p = fmadd(p, m, -1.2420140846e-1f);
+    p = fmadd(p, m, 1.4249322787e-1f);
+    p = fmadd(p, m, -1.6668057665e-1f);
+    p = fmadd(p, m, 2.0000714765e-1f);
+    p = fmadd(p, m, -2.4999993993e-1f);
+    p = fmadd(p, m, 3.3333331174e-1f);
+    const float fe = (float) e;
+    float y = (p * m) * z;
+    y = fmadd(fe, -2.12194440e-4f, y);
+    y = fmadd(z, -0.5f, y);
+    return fmadd(fe, 0.693359375f, m + y);
+}
+AD float erf_(float x) {
+    const float a = fabs_(x);
+    float r;
+    if (a < 1.f) {
+        const float t = x * x;
+        float p = fmadd(t, 7.93334984e-05f, -0.000803480507f);
+        p = fmadd(p, t, 0.00519121392f);
+        p = fmadd(p, t, -0.026855398f);
+        p = fmadd(p, t, 0.112836257f);
+        p = fmadd(p, t, -0.376126289f);
+        p = fmadd(p, t, 1.12837923f);
+        return p * x;
+    }
+    if (a < 4.f) {
+        const float s = 1.f / (a * a);
+        float q = fmadd(s, 0.208238602f, -1.215765f);
+        q = fmadd(q, s, 3.14549613f);
+        q = fmadd(q, s, -4.78043795f);
+        q = fmadd(q, s, 4.79150534f);
+        q = fmadd(q, s, -3.40518451f);
+        q = fmadd(q, s, 1.84398246f);
+        q = fmadd(q, s, -0.850101471f);
+        q = fmadd(q, s, 0.407034457f);
+        q = fmadd(q, s, -0.281359404f);
+        q = fmadd(q, s, 0.564175129f);
+        r = 1.f - exp_(-(a * a)) * q / a;
+    } else {
+        r = a == a ? 1.f : a;
+    }
+    return mulsign(r, x);
+}
+AD float erfinv_(float x) {
+    float w = -log_((1.f - x) * (1.f + x)), p;
+    if (w < 5.f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = fmadd(p, w, 3.43273939e-07f);
+        p = fmadd(p, w, -3.5233877e-06f);
+        p = fmadd(p, w, -4.39150654e-06f);
+        p = fmadd(p, w, 0.00021858087f);
+        p = fmadd(p, w, -0.00125372503f);
+        p = fmadd(p, w, -0.00417768164f);
+        p = fmadd(p, w, 0.246640727f);
+        p = fmadd(p, w, 1.50140941f);
+    } else {
+        w = __builtin_sqrtf(w) - 3.f;
+        p = -0.000200214257f;
+        p = fmadd(p, w, 0.000100950558f);
+        p = fmadd(p, w, 0.00134934322f);
+        p = fmadd(p, w, -0.00367342844f);
+        p = fmadd(p, w, 0.00573950773f);
+        p = fmadd(p, w, -0.0076224613f);
+        p = fmadd(p, w, 0.00943887047f);
+        p = fmadd(p, w, 1.00167406f);
+        p = fmadd(p, w, 2.83297682f);
+    }
+    return p * x;
+}
+AD float tan_(float x) {
+    float s, c;
+    sincos_c(x, s, c);
+    return s / c;
+}
+
 struct f3 { float x, y, z; };
 AD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 AD f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }

@@ -598,7 +598,7 @@ struct Microfacet {
     float eval(V3 m) const {
         float alpha_uv = au * av, ct = m.z, ct2 = sqr(ct), result;
         if (type == AMVPT_MICROFACET_BECKMANN) {
-            result = std::exp(-(sqr(m.x / au) + sqr(m.y / av)) / ct2) / (Pi * alpha_uv * sqr(ct2));
+            result = exp_(-(sqr(m.x / au) + sqr(m.y / av)) / ct2) / (Pi * alpha_uv * sqr(ct2));
         } else {
             result = rcp(Pi * alpha_uv * sqr(sqr(m.x / au) + sqr(m.y / av) + sqr(m.z)));
         }
@@ -617,6 +617,23 @@ struct Microfacet {
         return result;
     }
     V2 sample_visible_11(float cos_theta_i, V2 s) const {
+        if (type == AMVPT_MICROFACET_BECKMANN) {
+            /* numerical inversion with three Newton steps (microfacet.h:372-403) */
+            float tan_theta_i = safe_sqrt(fnmadd(cos_theta_i, cos_theta_i, 1.f)) / cos_theta_i;
+            float cot_theta_i = rcp(tan_theta_i);
+            float maxval = erf_(cot_theta_i);
+            s.x = fmaxf_(fminf_(s.x, 1.f - 1e-6f), 1e-6f);
+            s.y = fmaxf_(fminf_(s.y, 1.f - 1e-6f), 1e-6f);
+            float x = maxval - (maxval + 1.f) * erf_(std::sqrt(-log_(s.x)));
+            s.x *= 1.f + maxval + InvSqrtPi * tan_theta_i * exp_(-sqr(cot_theta_i));
+            for (int i = 0; i < 3; ++i) {
+                float slope = erfinv_(x),
+                      value = 1.f + x + InvSqrtPi * tan_theta_i * exp_(-sqr(slope)) - s.x,
+                      derivative = 1.f - slope * tan_theta_i;
+                x -= value / derivative;
+            }
+            return {erfinv_(x), erfinv_(fmsub(2.f, s.y, 1.f))};
+        }
         /* GGX branch (microfacet.h:404-418) */
         V2 p = square_to_uniform_disk_concentric(s);
         float ss = 0.5f * (1.f + cos_theta_i);
@@ -628,14 +645,32 @@ struct Microfacet {
     }
     void sample(V3 wi, V2 s, V3 &m, float &pdf) const {
         if (!visible) {
-            /* isotropic GGX, non-visible sampling (microfacet.h:256-300) */
-            float sin_phi, cos_phi;
-            sincos_((2.f * Pi) * s.y, sin_phi, cos_phi);
-            float alpha_2 = au * au;
-            float tan_theta_m_2 = alpha_2 * s.x / (1.f - s.x);
-            float cos_theta = rsqrt(1.f + tan_theta_m_2), cos_theta_2 = sqr(cos_theta);
-            float temp = 1.f + tan_theta_m_2 / alpha_2, cos_theta_3 = fmaxf_(cos_theta_2 * cos_theta, 1e-20f);
-            pdf = rcp(Pi * au * av * cos_theta_3 * sqr(temp));
+            /* microfacet.h:244-300: azimuth (isotropic: uniform; anisotropic: tan inversion),
+             * then the elevation of the distribution */
+            float sin_phi, cos_phi, alpha_2;
+            if (au == av) {
+                sincos_((2.f * Pi) * s.y, sin_phi, cos_phi);
+                alpha_2 = au * au;
+            } else {
+                float ratio = av / au, tmp = ratio * tan_((2.f * Pi) * s.y);
+                cos_phi = rsqrt(fmadd(tmp, tmp, 1.f));
+                cos_phi = mulsign(cos_phi, std::fabs(s.y - .5f) - .25f);
+                sin_phi = cos_phi * tmp;
+                alpha_2 = rcp(sqr(cos_phi / au) + sqr(sin_phi / av));
+            }
+            float cos_theta, cos_theta_2;
+            if (type == AMVPT_MICROFACET_BECKMANN) {
+                cos_theta = rsqrt(fnmadd(alpha_2, log_(1.f - s.x), 1.f));
+                cos_theta_2 = sqr(cos_theta);
+                float cos_theta_3 = fmaxf_(cos_theta_2 * cos_theta, 1e-20f);
+                pdf = (1.f - s.x) / (Pi * au * av * cos_theta_3);
+            } else {
+                float tan_theta_m_2 = alpha_2 * s.x / (1.f - s.x);
+                cos_theta = rsqrt(1.f + tan_theta_m_2);
+                cos_theta_2 = sqr(cos_theta);
+                float temp = 1.f + tan_theta_m_2 / alpha_2, cos_theta_3 = fmaxf_(cos_theta_2 * cos_theta, 1e-20f);
+                pdf = rcp(Pi * au * av * cos_theta_3 * sqr(temp));
+            }
             float sin_theta = std::sqrt(1.f - cos_theta_2);
             m = v3(cos_phi * sin_theta, sin_phi * sin_theta, cos_theta);
             return;
@@ -1438,10 +1473,6 @@ struct Renderer {
 
 bool build_scene(const amvpt_scene_desc *d, Scene &sc) {
     sc.bsdfs.assign(d->bsdfs, d->bsdfs + d->bsdf_count);
-    for (auto &b : sc.bsdfs)
-        if (b.type == AMVPT_BSDF_ROUGHCONDUCTOR &&
-            (b.distribution != AMVPT_MICROFACET_GGX || (!b.sample_visible && b.alpha_u != b.alpha_v)))
-            return false; /* Beckmann / anisotropic non-visible sampling: not on the implemented path */
     sc.emitters.assign(d->emitters, d->emitters + d->emitter_count);
     sc.emitter_pmf = sc.emitters.empty() ? 0.f : 1.f / (float) sc.emitters.size();
     /* Scene::update_emitter_sampling_distribution (scene.cpp:100-119) */
@@ -1808,6 +1839,11 @@ void oracle_sampler_1d(uint32_t seed_value, uint32_t lane, uint32_t n, float *ou
 }
 float oracle_gaussian_eval(float stddev, float x) { Gaussian g; g.init(stddev); return g.eval(x); }
 void oracle_sincos(float x, float *s, float *c) { sincos_(x, *s, *c); }
+/* the Beckmann path's transcendentals (oracle_math.h), checked against libm by the CPU tests */
+void oracle_math(uint32_t fn, const float *x, float *y, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i)
+        y[i] = fn == 0 ? exp_(x[i]) : fn == 1 ? log_(x[i]) : fn == 2 ? erf_(x[i]) : fn == 3 ? erfinv_(x[i]) : tan_(x[i]);
+}
 void oracle_square_to_cosine_hemisphere(float u, float v, float *out) {
     V3 r = square_to_cosine_hemisphere({u, v});
     out[0] = r.x; out[1] = r.y; out[2] = r.z;

@@ -63,6 +63,7 @@ def lib():
         L.oracle_square_to_cosine_hemisphere.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
         L.oracle_square_to_uniform_disk_concentric.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
         L.oracle_sincos.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_math.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.oracle_diffuse_eval_pdf.argtypes = [ctypes.c_void_p] * 5
         L.oracle_tea.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_tea_float32.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]

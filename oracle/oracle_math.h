@@ -46,6 +46,7 @@ static const float Pi = 3.14159265358979323846f;
 static const float InvPi = 0.31830988618379067154f;
 static const float InvTwoPi = 0.15915494309189533577f;
 static const float InvFourPi = 0.07957747154594766788f;
+static const float InvSqrtPi = 0.56418958354775628695f;
 static const float Epsilon = 5.9604644775390625e-08f;       /* 2^-24 */
 static const float RayEpsilon = Epsilon * 1500.f;            /* math.h:18-23 */
 static const float ShadowEpsilon = RayEpsilon * 10.f;
@@ -74,6 +75,129 @@ static inline void sincos_(float x, float &s_out, float &c_out) {
     s_out = u2f(f2u(rs) ^ (sign_sin & 0x80000000u));
     c_out = u2f(f2u(rc) ^ (sign_cos & 0x80000000u));
     if (!(xa < Infinity)) { s_out = NAN; c_out = NAN; }
+}
+
+/*
+ * exp / log / erf / erfinv / tan for the Beckmann distribution and anisotropic microfacet
+ * sampling (microfacet.h:185-431).  Dr.Jit's own single-precision versions are not vendored,
+ * so these are restatements of the published algorithms -- parity unpinned at the last ulp
+ * against the reference, pinned by tests/test_oracle_golden.py against libm / math.erf within
+ * a few ulp, and bit-identical between this oracle and the device (dmath.h, same operations).
+ *   exp    Cephes expf: n = floor(x log2 e + 1/2), two-constant Cody-Waite reduction, degree-5
+ *          polynomial, ldexp in two exact halves; 0 below -88.376, inf above +88.376
+ *   log    Cephes logf: frexp to [sqrt(1/2), sqrt 2), degree-8 polynomial, Cody-Waite ln 2
+ *   erf    |x| < 1: x P(x^2); 1 <= |x| < 4: 1 - exp(-x^2) Q(1/x^2) / |x|; else +-1
+ *          (least-squares fits, |error| < 2.1e-7)
+ *   erfinv M. Giles, "Approximating the erfinv function" (GPU Computing Gems, 2010), single
+ *   tan    sin / cos of the Cephes sincos above
+ */
+static inline float ldexp_(float y, int n) {
+    const int h = n / 2, l = n - h;
+    return (y * u2f((uint32_t) (h + 127) << 23)) * u2f((uint32_t) (l + 127) << 23);
+}
+static inline float exp_(float x) {
+    if (x != x) return x;
+    if (x > 88.3762626647949f) return Infinity;
+    if (x < -88.3762626647949f) return 0.f;
+    const float n = std::floor(fmadd(1.44269504088896341f, x, .5f));
+    float r = fnmadd(n, 0.693359375f, x);
+    r = fnmadd(n, -2.12194440e-4f, r);
+    float p = fmadd(r, 1.9875691500e-4f, 1.3981999507e-3f);
+    p = fmadd(p, r, 8.3334519073e-3f);
+    p = fmadd(p, r, 4.1665795894e-2f);
+    p = fmadd(p, r, 1.6666665459e-1f);
+    p = fmadd(p, r, 5.0000001201e-1f);
+    const float y = fmadd(p, r * r, r + 1.f);
+    return ldexp_(y, (int) n);
+}
+static inline float log_(float x) {
+    if (x != x || x < 0.f) return NAN;
+    if (x == 0.f) return -Infinity;
+    if (x == Infinity) return Infinity;
+    int e_adj = 0;
+    if (x < 1.17549435e-38f) { x *= 8388608.f; e_adj = -23; }
+    const uint32_t u = f2u(x);
+    int e = (int) ((u >> 23) & 0xffu) - 126 + e_adj;
+    float m = u2f((u & 0x007fffffu) | 0x3f000000u);   /* [0.5, 1) */
+    if (m < 0.707106781186547524f) { e -= 1; m = m + m - 1.f; }
+    else m = m - 1.f;
+    const float z = m * m;
+    float p = fmadd(m, 7.0376836292e-2f, -1.1514610310e-1f);
+    p = fmadd(p, m, 1.1676998740e-1f);
+    p = fmadd(p, m, -1.2420140846e-1f);
+    p = fmadd(p, m, 1.4249322787e-1f);
+    p = fmadd(p, m, -1.6668057665e-1f);
+    p = fmadd(p, m, 2.0000714765e-1f);
+    p = fmadd(p, m, -2.4999993993e-1f);
+    p = fmadd(p, m, 3.3333331174e-1f);
+    const float fe = (float) e;
+    float y = (p * m) * z;
+    y = fmadd(fe, -2.12194440e-4f, y);
+    y = fmadd(z, -0.5f, y);
+    return fmadd(fe, 0.693359375f, m + y);
+}
+static inline float erf_(float x) {
+    const float a = std::fabs(x);
+    float r;
+    if (a < 1.f) {
+        const float t = x * x;
+        float p = fmadd(t, 7.93334984e-05f, -0.000803480507f);
+        p = fmadd(p, t, 0.00519121392f);
+        p = fmadd(p, t, -0.026855398f);
+        p = fmadd(p, t, 0.112836257f);
+        p = fmadd(p, t, -0.376126289f);
+        p = fmadd(p, t, 1.12837923f);
+        return p * x;
+    }
+    if (a < 4.f) {
+        const float s = 1.f / (a * a);
+        float q = fmadd(s, 0.208238602f, -1.215765f);
+        q = fmadd(q, s, 3.14549613f);
+        q = fmadd(q, s, -4.78043795f);
+        q = fmadd(q, s, 4.79150534f);
+        q = fmadd(q, s, -3.40518451f);
+        q = fmadd(q, s, 1.84398246f);
+        q = fmadd(q, s, -0.850101471f);
+        q = fmadd(q, s, 0.407034457f);
+        q = fmadd(q, s, -0.281359404f);
+        q = fmadd(q, s, 0.564175129f);
+        r = 1.f - exp_(-(a * a)) * q / a;
+    } else {
+        r = a == a ? 1.f : a;
+    }
+    return mulsign(r, x);
+}
+static inline float erfinv_(float x) {
+    float w = -log_((1.f - x) * (1.f + x)), p;
+    if (w < 5.f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = fmadd(p, w, 3.43273939e-07f);
+        p = fmadd(p, w, -3.5233877e-06f);
+        p = fmadd(p, w, -4.39150654e-06f);
+        p = fmadd(p, w, 0.00021858087f);
+        p = fmadd(p, w, -0.00125372503f);
+        p = fmadd(p, w, -0.00417768164f);
+        p = fmadd(p, w, 0.246640727f);
+        p = fmadd(p, w, 1.50140941f);
+    } else {
+        w = std::sqrt(w) - 3.f;
+        p = -0.000200214257f;
+        p = fmadd(p, w, 0.000100950558f);
+        p = fmadd(p, w, 0.00134934322f);
+        p = fmadd(p, w, -0.00367342844f);
+        p = fmadd(p, w, 0.00573950773f);
+        p = fmadd(p, w, -0.0076224613f);
+        p = fmadd(p, w, 0.00943887047f);
+        p = fmadd(p, w, 1.00167406f);
+        p = fmadd(p, w, 2.83297682f);
+    }
+    return p * x;
+}
+static inline float tan_(float x) {
+    float s, c;
+    sincos_(x, s, c);
+    return s / c;
 }
 
 /* ---------------- vectors ---------------- */

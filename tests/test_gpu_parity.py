@@ -148,6 +148,22 @@ def test_veach_mis_g8(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
+@pytest.mark.parametrize("defines", [
+    dict(distr="beckmann"),                                            # the reference's default model
+    dict(distr="beckmann", vis="false"),
+    dict(distr="beckmann", a3u=0.02, a3v=0.1, a4u=0.05, a4v=0.25),    # anisotropic, visible normals
+    dict(distr="beckmann", vis="false", a3u=0.02, a3v=0.1, a4u=0.05, a4v=0.25),
+    dict(distr="ggx", vis="false", a3u=0.02, a3v=0.1, a4u=0.05, a4v=0.25),
+], ids=["beckmann_vis", "beckmann", "beckmann_vis_aniso", "beckmann_aniso", "ggx_aniso"])
+def test_veach_microfacet_models(gpu_ready, amvpt_mod, oracle, defines):
+    """roughconductor with Beckmann (exp eval, rational Smith G1, log elevation sampling, visible-normal
+    sampling by erf / erfinv Newton inversion) and anisotropic non-visible sampling (tan azimuth
+    inversion), microfacet.h:185-431: the device transcendentals are the oracle's operation for
+    operation, so records stay bit-identical."""
+    s = amvpt_mod.load_file(VEACH, res=24, spp=16, **defines)
+    _check(amvpt_mod, oracle, s)
+
+
 def test_veach_fast_mis_two_passes(gpu_ready, amvpt_mod, oracle):
     s = amvpt_mod.load_file(VEACH, res=16, spp=32, fast_mis="true")
     _check(amvpt_mod, oracle, s, seed=3)

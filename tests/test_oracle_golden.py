@@ -231,3 +231,71 @@ def test_fresnel_conductor_limits(oracle):
     assert np.isclose(L.oracle_fresnel_conductor(1.0, n, k), ((n - 1) ** 2 + k * k) / ((n + 1) ** 2 + k * k),
                       rtol=1e-5)
     assert np.isclose(L.oracle_fresnel_conductor(0.0, n, k), 1.0, rtol=1e-5)
+
+
+def test_beckmann_transcendentals_vs_libm(oracle):
+    """exp / log / erf / erfinv / tan of the Beckmann path (oracle_math.h restatements; Dr.Jit's own are
+    not vendored, so parity with the reference is unpinned at the last ulp): within a few ulp of libm /
+    math.erf / scipy's erfinv over the ranges the sampling code reaches."""
+    from scipy import special
+    L = oracle.lib()
+
+    def run(fn, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        y = np.zeros_like(x)
+        L.oracle_math(fn, x.ctypes.data, y.ctypes.data, len(x))
+        return y.astype(np.float64), x.astype(np.float64)
+
+    y, x = run(0, np.linspace(-87, 88, 20001))
+    assert np.max(np.abs(y / np.exp(x) - 1)) < 4e-7
+    y, x = run(0, np.array([-100.0, 100.0, np.nan]))
+    assert y[0] == 0 and np.isinf(y[1]) and np.isnan(y[2])
+    y, x = run(1, np.concatenate([np.geomspace(1e-40, 1e30, 20001), np.linspace(0.5, 2, 2001)]))
+    ref = np.log(x)
+    assert np.max(np.abs(y - ref) / np.maximum(np.abs(ref), 1e-3)) < 4e-7
+    y, x = run(1, np.array([0.0, -1.0, np.inf]))
+    assert np.isneginf(y[0]) and np.isnan(y[1]) and np.isposinf(y[2])
+    y, x = run(2, np.linspace(-5, 5, 40001))
+    assert np.max(np.abs(y - special.erf(x))) < 3e-7
+    y, x = run(3, np.linspace(-0.999999, 0.999999, 40001))
+    ref = special.erfinv(x)
+    assert np.max(np.abs(y - ref) / np.maximum(np.abs(ref), 1e-6)) < 2e-6
+    y, x = run(4, np.linspace(-6.2, 6.2, 40001))
+    ref = np.tan(x)
+    ok = np.abs(np.cos(x)) > 1e-3
+    assert np.max(np.abs(y - ref)[ok] / np.maximum(np.abs(ref[ok]), 1.0)) < 1e-5
+
+
+@pytest.mark.parametrize("kind,au,av,visible,theta_i", [
+    (BECKMANN, 0.3, 0.3, 1, 0.7), (BECKMANN, 0.2, 0.5, 1, 1.2), (BECKMANN, 0.3, 0.3, 0, 0.0),
+    (BECKMANN, 0.15, 0.45, 0, 0.0), (GGX, 0.15, 0.45, 0, 0.0), (GGX, 0.2, 0.5, 1, 1.0)],
+    ids=["beck_vis_iso", "beck_vis_aniso", "beck_iso", "beck_aniso", "ggx_aniso", "ggx_vis_aniso"])
+def test_microfacet_sampling_matches_its_pdf(oracle, kind, au, av, visible, theta_i):
+    """MicrofacetDistribution::sample (microfacet.h:244-360) draws normals distributed as its pdf(): the
+    returned pdf equals pdf(wi, m), and sample moments of m match the pdf's moments by quadrature.  Covers
+    the Beckmann elevation, the anisotropic azimuth inversion and the Beckmann visible-normal inversion."""
+    L = oracle.lib()
+    wi = oracle.f32(math.sin(theta_i), 0.0, math.cos(theta_i))
+    rng = np.random.default_rng(7)
+    n = 20000
+    ms = np.zeros((n, 3))
+    m = oracle.f32(0, 0, 0)
+    pdf = ctypes.c_float()
+    for i in range(n):
+        L.oracle_microfacet_sample(kind, au, av, visible, wi.ctypes.data, float(rng.uniform()), float(rng.uniform()),
+                                   m.ctypes.data, ctypes.byref(pdf))
+        ms[i] = m
+        if i < 300:
+            ref = L.oracle_microfacet_pdf(kind, au, av, visible, wi.ctypes.data, m.ctypes.data)
+            assert np.isclose(pdf.value, ref, rtol=2e-5, atol=1e-12)
+    # quadrature of pdf(m) dω over the upper hemisphere
+    th = (np.arange(600) + 0.5) * (np.pi / 2 / 600)
+    ph = (np.arange(600) + 0.5) * (2 * np.pi / 600)
+    T, Pp = np.meshgrid(th, ph, indexing="ij")
+    M = np.stack([np.sin(T) * np.cos(Pp), np.sin(T) * np.sin(Pp), np.cos(T)], -1).astype(np.float32).reshape(-1, 3)
+    w = np.array([L.oracle_microfacet_pdf(kind, au, av, visible, wi.ctypes.data, np.ascontiguousarray(v).ctypes.data)
+                  for v in M]) * (np.sin(T).reshape(-1)) * (np.pi / 2 / 600) * (2 * np.pi / 600)
+    assert abs(w.sum() - 1) < 0.01
+    for f in (lambda v: v[:, 0], lambda v: v[:, 2], lambda v: v[:, 0] ** 2, lambda v: v[:, 1] ** 2):
+        q, s = (f(M.astype(np.float64)) * w).sum() / w.sum(), f(ms).mean()
+        assert abs(q - s) < 4 * f(ms).std() / math.sqrt(n) + 2e-3, (q, s)
