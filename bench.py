@@ -300,7 +300,8 @@ def kernel_bytes(c, G, C):
     nee = 52                              # NEE record: origin + destination, light point + thr, thr + contribution
     fused = c["kernel_launches"]["k_shadow"] == 0   # NEE traced inside k_bounce (brute-force scenes)
     return {
-        "k_prim_hit": 16 * lanes,                                   # hit record out
+        # hit record out (+ the visibility requests when k_prim_req is fused into it)
+        "k_prim_hit": (16 + (48 if c["kernel_launches"]["k_prim_req"] == 0 else 0)) * lanes,
         "k_prim_req": (16 + 48) * lanes,                            # hit in, visibility requests out
         "k_vis": (48 + G / 8.0) * lanes,                            # requests in (once), ballots out
         "k_mv_primary": (16 + G / 8.0 + rec) * lanes + state * pushed,  # hit + ballots in, records + paths out

@@ -1730,19 +1730,15 @@ __global__ void __launch_bounds__(256) k_prim_hit(KParams P, const DScene *Sp, c
     }
 }
 
+/* k_prim_req's body for lane-order thread i: the primary vertex (pr, hit) -> visibility requests */
 template <int G, bool kTab, bool kDiff>
-__global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    DScene S = *Sp;
-    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.chunk_n) return;
-    PrimRay pr = primary_raygen(P, V, i);
+AD void prim_requests(const KParams &P, const SceneRef &sc, const DScene &S, const DView *V, const Bufs &B, uint32_t i,
+                      PrimRay pr, const Hit &hit) {
     const int Gn = group_size<G>(P);
     VMask<G> bits = 0;
     f3 p = mk(0.f, 0.f, 0.f), n = p, dsp = p;
     if (P.max_depth != 0) {
-        const SI si = compute_si(sc, pr.ray, hit_of(B.hit[i]));
+        const SI si = compute_si(sc, pr.ray, hit);
         const bool p_hit = si.valid();
         const bool direct_em = si_emitter(sc, si) >= 0;
         const int32_t b = p_hit ? S.shapes[si.shape].bsdf : -1;
@@ -1775,6 +1771,38 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
     B.vreq[0][i] = make_float4(p.x, p.y, p.z, bitsf((uint32_t) bits));
     B.vreq[1][i] = make_float4(n.x, n.y, n.z, pr.apx);
     B.vreq[2][i] = make_float4(dsp.x, dsp.y, dsp.z, pr.apy);
+}
+
+template <int G, bool kTab, bool kDiff>
+__global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.chunk_n) return;
+    const PrimRay pr = primary_raygen(P, V, i);
+    prim_requests<G, kTab, kDiff>(P, sc, S, V, B, i, pr, P.max_depth != 0 ? hit_of(B.hit[i]) : Hit{kInf, 0.f, 0.f, -1});
+}
+
+/*
+ * k_prim_hit + k_prim_req in one launch (wave-uniform BVHs, whose walk needs no LDS): the raygen
+ * is computed once and the hit goes straight into the request code (it is still stored for
+ * k_mv_primary).  AMVPT_FUSE_PRIM=0 keeps the two launches (A/B).
+ */
+template <int G, bool kTab, bool kDiff>
+__global__ void __launch_bounds__(256) k_prim_hit_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.chunk_n) return;
+    const PrimRay pr = primary_raygen(P, V, i);
+    Hit h{kInf, 0.f, 0.f, -1};
+    if (P.max_depth != 0) {
+        h = trace_closest<true>(sc, pr.ray);
+        B.hit[i] = hit_rec(h);
+    }
+    prim_requests<G, kTab, kDiff>(P, sc, S, V, B, i, pr, h);
 }
 
 /* one block = 64 lanes x G slots, wave k traces slot k of the block's 64 lanes (G = 0: 16 waves,
@@ -2657,16 +2685,26 @@ static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStrea
     constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
     const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
     const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
-    T.begin(AMVPT_K_PRIM_HIT, st);
-    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
-    T.end(st);
-    T.begin(AMVPT_K_PRIM_REQ, st);
-    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-    T.end(st);
+    static const bool fuse = [] { const char *e = std::getenv("AMVPT_FUSE_PRIM"); return !(e && e[0] == '0'); }();
+    if (uni && fuse) {
+        T.begin(AMVPT_K_PRIM_HIT, st);
+        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        T.end(st);
+    } else {
+        T.begin(AMVPT_K_PRIM_HIT, st);
+        if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
+        T.end(st);
+        T.begin(AMVPT_K_PRIM_REQ, st);
+        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        T.end(st);
+    }
     T.begin(AMVPT_K_VIS, st);
     constexpr bool kVisPairs = vis_pairs<G, true>();
     const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
