@@ -135,6 +135,23 @@ def main():
         adist.reduce_film(film, dst=0)
         return c
 
+    partition = "equal lane counts"
+    if lane_sharded and world > 1 and args.warmup > 0:
+        # load balance (outside the timed region): time this rank's range once, all-gather the
+        # times and move the range boundaries to equal cost (amvpt.dist.balanced_shards)
+        torch.cuda.synchronize()
+        t_b = time.perf_counter()
+        film.zero_()
+        dev.render(vd, p, film.data_ptr(), lane_begin, lane_end, stream)
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t_b], dtype=torch.float64, device="cuda")
+        ts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ts, t)
+        bounds = [adist.lane_shard(lanes_per_pass, r, world)[0] for r in range(world)] + [lanes_per_pass]
+        bounds = adist.balanced_shards(bounds, [float(x.item()) for x in ts], align=max(64, 16 * spp_pp))
+        lane_begin, lane_end = bounds[rank], bounds[rank + 1]
+        samples_per_rank = (lane_end - lane_begin) * n_passes
+        partition = "cost-balanced contiguous lane ranges (one timed warmup render per rank)"
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -154,7 +171,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    total_samples = samples_per_rank * world * args.steps
+    total_samples = lanes_per_pass * n_passes * args.steps if lane_sharded else samples_per_rank * world * args.steps
     value = total_samples / elapsed / 1e6
 
     # ---- one instrumented frame (outside the timed region): per-kernel HIP-event times + lane counters
@@ -217,6 +234,7 @@ def main():
                                p.film_height, spp, "" if lane_sharded else "/GPU", n_passes, spp_pp, G,
                                p.adaptive),
                 "samples_per_gpu_per_step": samples_per_rank,
+                "partition": partition if lane_sharded else "pass-sharded",
                 "adaptive_lanes_per_gpu_per_step": c["adaptive_lanes"],
                 "parallelism": ("lane-sharded x%d (+ one count all-gather per pass) + RCCL reduce of the RGBW "
                                 "ImageBlock" if lane_sharded else

@@ -125,3 +125,22 @@ def test_host_lane_shard_matches_dist(amvpt_mod):
             assert shards == [dist.lane_shard(lanes, r, world) for r in range(world)]
             assert shards[0][0] == 0 and shards[-1][1] == lanes
             assert all(shards[r][1] == shards[r + 1][0] for r in range(world - 1))
+
+
+def test_balanced_shards_equalise_measured_cost():
+    """amvpt.dist.balanced_shards: contiguous, ordered, aligned ranges that split a piecewise-uniform cost
+    into equal parts (the bench's one-measurement rebalance of the strong-scaling partition)."""
+    from amvpt import dist as adist
+    n, world = 1 << 20, 4
+    bounds = [adist.lane_shard(n, r, world)[0] for r in range(world)] + [n]
+    # shard 3 is twice as expensive per lane as the others
+    new = adist.balanced_shards(bounds, [1.0, 1.0, 1.0, 2.0], align=256)
+    assert new[0] == 0 and new[-1] == n and all(a <= b for a, b in zip(new, new[1:]))
+    assert all(x % 256 == 0 for x in new[1:-1])
+    dens = lambda x: 2.0 if x >= bounds[3] else 1.0
+    cost = [sum(dens(x) for x in range(a, b, 256)) for a, b in zip(new, new[1:])]
+    assert max(cost) / min(cost) < 1.01
+    # equal costs keep (aligned) equal ranges; one rank may own an empty range
+    assert adist.balanced_shards(bounds, [1.0] * 4, align=256) == bounds
+    with pytest.raises(ValueError):
+        adist.balanced_shards(bounds, [1.0] * 3)
