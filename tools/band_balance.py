@@ -33,21 +33,31 @@ def main():
     dev = amvpt.DeviceScene(sd)
     film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    out = {}
-    for w in sorted({1, 2, 4, args.world}):
+    def shard_times(bounds, reps):
         ms = []
-        for r in range(w):
-            b, e = adist.lane_shard(L, r, w)
+        for r in range(len(bounds) - 1):
+            b, e = bounds[r], bounds[r + 1]
             dev.render(vd, p, film.data_ptr(), b, e, stream)   # warm
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(args.reps):
+            for _ in range(reps):
                 dev.render(vd, p, film.data_ptr(), b, e, stream)
             torch.cuda.synchronize()
-            ms.append((time.perf_counter() - t0) * 1e3 / args.reps)
-        out[w] = {"shard_ms": [round(x, 2) for x in ms], "max_ms": round(max(ms), 2),
-                  "efficiency_bound": round(sum(ms) / (w * max(ms)), 4)}
-        print(json.dumps({"world": w, **out[w]}), flush=True)
+            ms.append((time.perf_counter() - t0) * 1e3 / reps)
+        return ms
+
+    for w in sorted({1, 2, 4, args.world}):
+        bounds = [adist.lane_shard(L, r, w)[0] for r in range(w)] + [L]
+        # equal lane counts, then bench.py's one-measurement rebalance (amvpt.dist.balanced_shards)
+        for kind in ("equal", "balanced"):
+            if kind == "balanced":
+                if w == 1:
+                    break
+                bounds = adist.balanced_shards(bounds, ms, align=256)
+            ms = shard_times(bounds, args.reps)
+            print(json.dumps({"world": w, "partition": kind, "shard_ms": [round(x, 2) for x in ms],
+                              "max_ms": round(max(ms), 2),
+                              "efficiency_bound": round(sum(ms) / (w * max(ms)), 4)}), flush=True)
 
 
 if __name__ == "__main__":
