@@ -194,7 +194,9 @@ def main():
     achieved = per_launch_bytes / (kms[dom] / launches * 1e-3) / 1e9
     kernel_name = {"k_splat": ("k_splat_multi<%d, %d>" % (G, C)) if G > 1 else "k_splat_single<%d>" % C,
                    "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
-                   "k_prim_req": "k_prim_req<%d," % G}.get(dom, dom + "<")
+                   "k_prim_req": "k_prim_req<%d," % G,
+                   "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1
+                   else "k_prim_hit<"}.get(dom, dom + "<")
     traffic, traffic_src = pmc_traffic(kernel_name, headline)
     valu = pmc_valu(kms, kl, G, headline)
     # SURVEY 8(d) whole-pipeline byte model
@@ -361,7 +363,8 @@ def pmc_valu(kms, kl, G, full_size):
         d = json.load(f)
     peak = d["peak_valu_ginst_s"]
     sym = {"k_splat": "k_splat_multi<%d," % G, "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
-           "k_prim_req": "k_prim_req<%d," % G}
+           "k_prim_req": "k_prim_req<%d," % G,
+           "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1 else "k_prim_hit<"}
     out = {"peak_Ginst_s": peak, "source": os.path.relpath(files[-1], REPO), "kernels": {}}
     for k in kms:
         if not kl[k]:
