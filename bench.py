@@ -194,7 +194,7 @@ def main():
     achieved = per_launch_bytes / (kms[dom] / launches * 1e-3) / 1e9
     kernel_name = {"k_splat": ("k_splat_multi<%d, %d>" % (G, C)) if G > 1 else "k_splat_single<%d>" % C,
                    "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
-                   "k_prim_req": "k_prim_req<%d," % G,
+                   "k_prim_req": "k_prim_req<%d," % G, "k_suffix": "k_suffix_fused<",
                    "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1
                    else "k_prim_hit<"}.get(dom, dom + "<")
     traffic, traffic_src = pmc_traffic(kernel_name, headline)
@@ -331,6 +331,9 @@ def kernel_bytes(c, G, C):
         "k_bounce": (state + 16) * suffix + state * (suffix - pushed) + 16 * pushed + (0 if fused else nee * shadow),
         "k_shadow": (nee + 32) * shadow,                            # NEE record in, result read-modify-write
         "k_splat": rec * lanes + 16 * adapt,                        # records in (film: PMC WRITE_SIZE)
+        # fused suffix (brute-force scenes): each path's state in once, its result out once; the
+        # vertices in between stay in registers
+        "k_suffix": (state + 16) * pushed,
     }
 
 
@@ -363,7 +366,7 @@ def pmc_valu(kms, kl, G, full_size):
         d = json.load(f)
     peak = d["peak_valu_ginst_s"]
     sym = {"k_splat": "k_splat_multi<%d," % G, "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
-           "k_prim_req": "k_prim_req<%d," % G,
+           "k_prim_req": "k_prim_req<%d," % G, "k_suffix": "k_suffix_fused<",
            "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1 else "k_prim_hit<"}
     out = {"peak_Ginst_s": peak, "source": os.path.relpath(files[-1], REPO), "kernels": {}}
     for k in kms:

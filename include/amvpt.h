@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 6
+#define AMVPT_ABI_VERSION 7
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -209,7 +209,8 @@ typedef enum amvpt_kernel_id {
     AMVPT_K_BOUNCE = 6,        /* suffix shading                          */
     AMVPT_K_SHADOW = 7,        /* suffix NEE any-hit                      */
     AMVPT_K_SPLAT = 8,         /* ImageBlock::put                         */
-    AMVPT_K_COUNT = 9
+    AMVPT_K_SUFFIX = 9,        /* ABI 7: the whole suffix in one launch (closest hit + shading + NEE, brute-force scenes) */
+    AMVPT_K_COUNT = 10
 } amvpt_kernel_id;
 
 typedef struct amvpt_scene amvpt_scene; /* opaque device-resident scene */

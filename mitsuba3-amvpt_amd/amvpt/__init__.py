@@ -86,7 +86,7 @@ class Counters(ctypes.Structure):
 
 # amvpt_kernel_id (include/amvpt.h): index -> name of Counters.kernel_ms / kernel_launches
 KERNELS = ("k_prim_hit", "k_prim_req", "k_vis", "k_mv_primary", "k_raygen", "k_extend", "k_bounce", "k_shadow",
-           "k_splat")
+           "k_splat", "k_suffix")
 
 
 INTEGRATOR_MVPATH, INTEGRATOR_PATH = 0, 1

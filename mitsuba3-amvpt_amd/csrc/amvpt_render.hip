@@ -38,7 +38,7 @@
 #include "dbsdf.h"
 
 /* non-template kernels get internal linkage in the k_shadow translation unit (amvpt_shadow.hip) */
-#ifdef AMVPT_SHADOW_TU
+#if defined(AMVPT_SHADOW_TU) || defined(AMVPT_GROUP_TU)
 #define AMVPT_TU_LOCAL static
 #else
 #define AMVPT_TU_LOCAL
@@ -46,7 +46,7 @@
 
 namespace amvpt {
 
-#ifndef AMVPT_SHADOW_TU
+#if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_GROUP_TU)
 uint64_t g_chunk_lanes = 1ull << 23;
 uint32_t g_traversal = 0;
 bool g_diffuse_spec = true;   /* all-diffuse kernel specialisation (AMVPT_NO_DIFFUSE_SPEC=1 turns it off) */
@@ -1489,6 +1489,70 @@ __global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Buf
 #define AMVPT_BOUNCE_WAVES 5
 #endif
 /*
+ * One suffix vertex (mvpath_multi.h:563-686 == mvpath_single.h:130-275): emitter-hit MIS at the
+ * ray's hit, emitter sample, BSDF eval/sample, Russian roulette.  s advances in place; returns
+ * whether the path continues; nee = the emitter sample's shadow ray shr (to nee_to) carries
+ * fma(nee_thr, nee_c, result) if unoccluded.  Shared by k_bounce and k_suffix_fused.
+ */
+template <bool kDiff>
+AD bool bounce_vertex(const KParams &P, const DScene &S, const SceneRef &sc, PathState &s, Pcg &rng, const Hit &hit,
+                      bool &nee, Ray &shr, f3 &nee_to, C3 &nee_thr, C3 &nee_c) {
+    SI si = compute_si(sc, s.ray, hit);
+    int32_t em = si_emitter(sc, si);
+    {
+        DSamp ds = ds_zero();
+        ds.p = si.p; ds.n = si.sh.n;
+        f3 rel = si.p - s.prev_p;
+        ds.dist = norm(rel);
+        ds.d = si.valid() ? rel / ds.dist : -si.wi;
+        ds.emitter = em;
+        float em_pdf = pdf_emitter_direction(sc, s.prev_p, ds, !s.prev_delta);
+        float mis_bsdf = mis_weight(s.prev_pdf, em_pdf);
+        s.res = cfma(s.thr, emitter_eval(sc, em, si, s.prev_pdf > 0.f) * mis_bsdf, s.res);
+    }
+    bool active_next = (s.depth + 1 < P.max_depth) && si.valid();
+    int32_t b = si.valid() ? S.shapes[si.shape].bsdf : -1;
+    bool active_em = active_next && (bsdf_flags(S.bsdfs, b) & BF_Smooth);
+    float e1 = rng.next_1d(), e2 = rng.next_1d();
+    DSamp ds;
+    C3 em_w;
+    sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
+    active_em = active_em && ds.pdf != 0.f;   /* ds.pdf != 0 <=> the reference traces the ray */
+    f3 wo = si.sh.to_local(ds.d);
+    float s1 = rng.next_1d();
+    float s2a = rng.next_1d(), s2b = rng.next_1d();
+    (void) s1;
+    C3 bval;
+    float bpdf;
+    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
+    BSample bs;
+    C3 bw;
+    bsdf_sample<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
+    if (active_em) {
+        float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
+        nee = true;
+        nee_thr = s.thr;
+        nee_c = bval * em_w * mis_em;
+        shr = spawn_ray_to(si.p, si.n, ds.p);
+        nee_to = ds.p;
+    }
+    s.ray = spawn_ray(si.p, si.n, si.sh.to_world(bs.wo));
+    s.thr = s.thr * bw;
+    s.eta *= bs.eta;
+    s.prev_p = si.p;
+    s.prev_pdf = bs.pdf;
+    s.prev_delta = (bs.type & BF_Delta) != 0;
+    if (si.valid()) s.depth += 1;
+    float tmax = cmax(s.thr);
+    float rr_prob = vmin(tmax * sqr(s.eta), .95f);
+    bool rractive = s.depth >= P.rr_depth;
+    bool rr_continue = rng.next_1d() < rr_prob;
+    s.valid_ray = s.valid_ray || (si.valid() && !(bs.type & BF_Null));
+    if (rractive) s.thr = s.thr * rcp(rr_prob);
+    return active_next && (!rractive || rr_continue) && (tmax != 0.f);
+}
+
+/*
  * kNee >= 0: the NEE shadow ray is traced inside k_bounce with walk kNee (the brute-force walks of
  * tiny scenes, which are ALU-bound and need no occupancy to hide node-load latency): no NEE
  * record goes through HBM, no k_shadow launch, and the visible light's contribution is added to
@@ -1517,59 +1581,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             rng.state = s.rng_state;
             rng.inc = (((uint64_t) path_seq(P, s.idx)) << 1) | 1u;
             ++verts;
-            SI si = compute_si(sc, s.ray, hit_of(B.hit[i]));
-            int32_t em = si_emitter(sc, si);
-            {
-                DSamp ds = ds_zero();
-                ds.p = si.p; ds.n = si.sh.n;
-                f3 rel = si.p - s.prev_p;
-                ds.dist = norm(rel);
-                ds.d = si.valid() ? rel / ds.dist : -si.wi;
-                ds.emitter = em;
-                float em_pdf = pdf_emitter_direction(sc, s.prev_p, ds, !s.prev_delta);
-                float mis_bsdf = mis_weight(s.prev_pdf, em_pdf);
-                s.res = cfma(s.thr, emitter_eval(sc, em, si, s.prev_pdf > 0.f) * mis_bsdf, s.res);
-            }
-            bool active_next = (s.depth + 1 < P.max_depth) && si.valid();
-            int32_t b = si.valid() ? S.shapes[si.shape].bsdf : -1;
-            bool active_em = active_next && (bsdf_flags(S.bsdfs, b) & BF_Smooth);
-            float e1 = rng.next_1d(), e2 = rng.next_1d();
-            DSamp ds;
-            C3 em_w;
-            sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
-            active_em = active_em && ds.pdf != 0.f;   /* ds.pdf != 0 <=> the reference traces the ray */
-            f3 wo = si.sh.to_local(ds.d);
-            float s1 = rng.next_1d();
-            float s2a = rng.next_1d(), s2b = rng.next_1d();
-            (void) s1;
-            C3 bval;
-            float bpdf;
-            bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
-            BSample bs;
-            C3 bw;
-            bsdf_sample<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
-            if (active_em) {
-                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
-                nee = true;
-                nee_thr = s.thr;
-                nee_c = bval * em_w * mis_em;
-                shr = spawn_ray_to(si.p, si.n, ds.p);
-                nee_to = ds.p;
-            }
-            s.ray = spawn_ray(si.p, si.n, si.sh.to_world(bs.wo));
-            s.thr = s.thr * bw;
-            s.eta *= bs.eta;
-            s.prev_p = si.p;
-            s.prev_pdf = bs.pdf;
-            s.prev_delta = (bs.type & BF_Delta) != 0;
-            if (si.valid()) s.depth += 1;
-            float tmax = cmax(s.thr);
-            float rr_prob = vmin(tmax * sqr(s.eta), .95f);
-            bool rractive = s.depth >= P.rr_depth;
-            bool rr_continue = rng.next_1d() < rr_prob;
-            s.valid_ray = s.valid_ray || (si.valid() && !(bs.type & BF_Null));
-            if (rractive) s.thr = s.thr * rcp(rr_prob);
-            keep = active_next && (!rractive || rr_continue) && (tmax != 0.f);
+            keep = bounce_vertex<kDiff>(P, S, sc, s, rng, hit_of(B.hit[i]), nee, shr, nee_to, nee_thr, nee_c);
             s.rng_state = rng.state;
             if (kNee < 0 && !keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
         }
@@ -1593,6 +1605,73 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             B.nee[1][ns] = make_float4(nee_to.x, nee_to.y, nee_to.z, nee_thr.r);
             B.nee[2][ns] = make_float4(nee_thr.g, nee_thr.b, nee_c.r, nee_c.g);
             B.nee_cb[ns] = nee_c.b;
+        }
+    }
+    if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
+}
+
+/*
+ * k_suffix_fused: the whole shared suffix of the brute-force-walk scenes in ONE launch, paths
+ * resident in registers.  Every wave iteration is one vertex for each of its lanes -- closest
+ * hit (brute force), bounce_vertex, the NEE any-hit walk -- whatever depth each lane's path is
+ * at; a lane whose path ended takes the partition's next queued path (the primary kernel's
+ * output queue, one returning atomic per wave on the partition's work counter).  No per-depth
+ * launches, no path state or hit through HBM (80 B in once per path, 16 B out): the walks are
+ * wave-uniform brute force, ALU-bound, so they need no occupancy of their own.  Lane results
+ * are the same operations in the same order as the k_extend / k_bounce wavefronts.
+ * The work counters (cnt_out of the queue pair) are zeroed by the host before the launch.
+ */
+#ifndef AMVPT_FUSED_BLOCKS
+/* blocks per queue partition (x kQParts blocks of 256 threads), more than are resident at once:
+ * blocks that start late find their partition partly drained, which evens out the tail
+ * (config M, suffix ms: 5 -> 163.7, 8 -> 149.0, 16 -> 144.8, 24..64 -> 144.8; r02fb) */
+#define AMVPT_FUSED_BLOCKS 16
+#endif
+#ifndef AMVPT_FUSED_WAVES
+/* 6 waves/SIMD (80 VGPRs, 24 B of spills): suffix 146.4 -> 143.2 ms per config-M frame; 4 waves 157.8 (r02fc) */
+#define AMVPT_FUSED_WAVES 6
+#endif
+template <bool kTab, bool kDiff, int kW>
+__global__ void __launch_bounds__(256, AMVPT_FUSED_WAVES) k_suffix_fused(KParams P, const DScene *Sp, Bufs B) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode);
+    const uint32_t part = blockIdx.x % kQParts;
+    const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
+    uint32_t *const work = B.cnt_out + part * kCntStride;
+    unsigned long long verts = 0, shadows = 0;
+    PathState s;
+    s.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), kLargest};
+    Pcg rng;
+    bool live = false, drained = false;
+    for (;;) {
+        if (!drained) {
+            const uint32_t j = queue_slot(!live, work);
+            const bool got = !live && j < count;
+            if (wave_any(!live && j >= count)) drained = true;   /* later entries are larger still */
+            if (got) {
+                s = load_state(B.q_in, pbase + j);
+                rng.state = s.rng_state;
+                rng.inc = (((uint64_t) path_seq(P, s.idx)) << 1) | 1u;
+                live = true;
+            }
+        }
+        if (!wave_any(live)) break;
+        const Hit h = walk_closest<kW>(sc, s.ray);
+        bool keep = false, nee = false;
+        Ray shr;
+        f3 nee_to;
+        C3 nee_thr, nee_c;
+        if (live) {
+            ++verts;
+            keep = bounce_vertex<kDiff>(P, S, sc, s, rng, h, nee, shr, nee_to, nee_thr, nee_c);
+        }
+        shadows += nee ? 1 : 0;
+        const bool occluded = brute_any<kW == WALK_BRUTE>(sc, shr, !nee);
+        if (nee && !occluded) s.res = cfma(nee_thr, nee_c, s.res);
+        if (live && !keep) {
+            B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
+            live = false;
         }
     }
     if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
@@ -2483,7 +2562,146 @@ void launch_shadow(int walk, dim3 grid, size_t lds, hipStream_t st, const KParam
 ;
 #endif
 
-#if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_KERNEL_PROBE)
+/* Per-kernel HIP-event timing of an instrumented render (amvpt_counters given): an
+ * event pair around every launch on the render stream, resolved in batches. */
+#ifndef AMVPT_FLUSH_MARKS
+#define AMVPT_FLUSH_MARKS 1
+#endif
+struct KTimer {
+    static constexpr size_t kPairs = 128;
+    bool on = false;
+    hipError_t err = hipSuccess;
+    hipEvent_t ev[2 * kPairs] = {};
+    int kid[kPairs] = {};
+    size_t n = 0;
+    double ms[AMVPT_K_COUNT] = {};
+    uint64_t launches[AMVPT_K_COUNT] = {};
+    void init(bool enable) {
+        on = enable;
+        if (!on) return;
+        for (auto &e : ev)
+            if (err == hipSuccess) err = hipEventCreate(&e);
+    }
+    void flush() {
+        if (!on || n == 0 || err != hipSuccess) return;
+        err = hipEventSynchronize(ev[2 * n - 1]);
+        for (size_t i = 0; i < n && err == hipSuccess; ++i) {
+            float t = 0.f;
+            err = hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
+            ms[kid[i]] += t;
+            launches[kid[i]] += 1;
+        }
+        n = 0;
+    }
+    void begin(int k, hipStream_t st) {
+        if (!on || err != hipSuccess) return;
+        if (n == kPairs) flush();
+        kid[n] = k;
+        err = hipEventRecord(ev[2 * n], st);
+    }
+    void end(hipStream_t st) {
+        if (!on || err != hipSuccess) return;
+        err = hipEventRecord(ev[2 * n + 1], st);
+        ++n;
+    }
+    /* stage markers when not timing: a timing-enabled event record after each stage
+     * (measured: a frame without them, or with hipEventDisableTiming markers, ran ~2 %
+     * slower; AMVPT_FLUSH_MARKS A/B) */
+    hipEvent_t mark_ev = nullptr;
+    void mark(hipStream_t st) {
+        if (on || !AMVPT_FLUSH_MARKS) return;
+        if (!mark_ev && hipEventCreate(&mark_ev) != hipSuccess) return;
+        (void) hipEventRecord(mark_ev, st);
+    }
+    ~KTimer() {
+        for (auto &e : ev)
+            if (e) (void) hipEventDestroy(e);
+        if (mark_ev) (void) hipEventDestroy(mark_ev);
+    }
+};
+
+/*
+ * Group-size instances.  The G-dependent launchers (and the ~20 kernels each pulls in) are
+ * explicitly instantiated in the translation units csrc/amvpt_group_*.hip (this file included
+ * with AMVPT_GROUP_TU and AMVPT_GROUP_LIST), so the instances compile in parallel; this unit
+ * only declares them.  k_prim_hit does not depend on G: its launcher lives here.
+ */
+void launch_prim_hit(bool uni, dim3 grid, size_t lds_bvh, hipStream_t st, const KParams &P, const DScene *S,
+                     const DView *V, const Bufs &B)
+#if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_GROUP_TU)
+{
+    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), grid, dim3(256), lds_bvh, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), grid, dim3(256), lds_bvh, st, P, S, V, B);
+}
+#else
+;
+#endif
+#ifdef AMVPT_GROUP_TU
+template <int G> inline int group_size_host(const KParams &P) { return G ? G : (int) P.G; }
+/* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
+template <int G>
+void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
+                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T) {
+    constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
+    const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
+    const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
+    static const bool fuse = [] { const char *e = std::getenv("AMVPT_FUSE_PRIM"); return !(e && e[0] == '0'); }();
+    if (uni && fuse) {
+        T.begin(AMVPT_K_PRIM_HIT, st);
+        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        T.end(st);
+    } else {
+        T.begin(AMVPT_K_PRIM_HIT, st);
+        launch_prim_hit(uni, g256, lds_bvh, st, P, S, V, B);
+        T.end(st);
+        T.begin(AMVPT_K_PRIM_REQ, st);
+        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        T.end(st);
+    }
+    T.begin(AMVPT_K_VIS, st);
+    constexpr bool kVisPairs = vis_pairs<G, true>();
+    const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
+    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    T.end(st);
+    T.begin(AMVPT_K_MV_PRIMARY, st);
+    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    T.end(st);
+}
+template <int G>
+void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff) {
+    const bool row = AMVPT_WAVE_WIN && P.row_splat && P.C == 4;
+    if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (diff && row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+}
+#define AMVPT_GROUP_INST(G_)                                                                                      \
+    template void launch_primary<G_>(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *,            \
+                                     const DView *, const Bufs &, bool, bool, bool, KTimer &);                          \
+    template void launch_splat<G_>(dim3, hipStream_t, const KParams &, const DView *, const Bufs &, bool);
+AMVPT_GROUP_LIST(AMVPT_GROUP_INST)
+#undef AMVPT_GROUP_INST
+#else
+template <int G>
+void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P, const DScene *S,
+                    const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T);
+template <int G>
+void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff);
+#endif
+
+#if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_GROUP_TU) && !defined(AMVPT_KERNEL_PROBE)
 /* ------------------------------------------------------------------ */
 /* Host orchestration                                                 */
 /* ------------------------------------------------------------------ */
@@ -2602,63 +2820,21 @@ static amvpt_status arena_reserve(DevArena &A, void *&buf, size_t &have, size_t 
     return AMVPT_OK;
 }
 
-/* Per-kernel HIP-event timing of an instrumented render (amvpt_counters given): an
- * event pair around every launch on the render stream, resolved in batches. */
-#ifndef AMVPT_FLUSH_MARKS
-#define AMVPT_FLUSH_MARKS 1
-#endif
-struct KTimer {
-    static constexpr size_t kPairs = 128;
-    bool on = false;
-    hipError_t err = hipSuccess;
-    hipEvent_t ev[2 * kPairs] = {};
-    int kid[kPairs] = {};
-    size_t n = 0;
-    double ms[AMVPT_K_COUNT] = {};
-    uint64_t launches[AMVPT_K_COUNT] = {};
-    void init(bool enable) {
-        on = enable;
-        if (!on) return;
-        for (auto &e : ev)
-            if (err == hipSuccess) err = hipEventCreate(&e);
-    }
-    void flush() {
-        if (!on || n == 0 || err != hipSuccess) return;
-        err = hipEventSynchronize(ev[2 * n - 1]);
-        for (size_t i = 0; i < n && err == hipSuccess; ++i) {
-            float t = 0.f;
-            err = hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
-            ms[kid[i]] += t;
-            launches[kid[i]] += 1;
-        }
-        n = 0;
-    }
-    void begin(int k, hipStream_t st) {
-        if (!on || err != hipSuccess) return;
-        if (n == kPairs) flush();
-        kid[n] = k;
-        err = hipEventRecord(ev[2 * n], st);
-    }
-    void end(hipStream_t st) {
-        if (!on || err != hipSuccess) return;
-        err = hipEventRecord(ev[2 * n + 1], st);
-        ++n;
-    }
-    /* stage markers when not timing: a timing-enabled event record after each stage
-     * (measured: a frame without them, or with hipEventDisableTiming markers, ran ~2 %
-     * slower; AMVPT_FLUSH_MARKS A/B) */
-    hipEvent_t mark_ev = nullptr;
-    void mark(hipStream_t st) {
-        if (on || !AMVPT_FLUSH_MARKS) return;
-        if (!mark_ev && hipEventCreate(&mark_ev) != hipSuccess) return;
-        (void) hipEventRecord(mark_ev, st);
-    }
-    ~KTimer() {
-        for (auto &e : ev)
-            if (e) (void) hipEventDestroy(e);
-        if (mark_ev) (void) hipEventDestroy(mark_ev);
-    }
-};
+
+static void launch_suffix_fused(bool tab, bool diff, int walk, dim3 grid, size_t lds, hipStream_t st, const KParams &P,
+                                const DScene *S, const Bufs &B) {
+#define AMVPT_FUSED(T_, D_)                                                                                           \
+    do {                                                                                                              \
+        if (walk == WALK_BRUTE_NS)                                                                                    \
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, S, B); \
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_BRUTE>), grid, dim3(256), lds, st, P, S, B); \
+    } while (0)
+    if (tab && diff) AMVPT_FUSED(true, true);
+    else if (tab) AMVPT_FUSED(true, false);
+    else if (diff) AMVPT_FUSED(false, true);
+    else AMVPT_FUSED(false, false);
+#undef AMVPT_FUSED
+}
 
 static void launch_bounce(bool tab, bool diff, int nee_walk, dim3 grid, size_t lds, hipStream_t st, const KParams &P,
                           const DScene *S, const Bufs &B) {
@@ -2677,57 +2853,6 @@ static void launch_bounce(bool tab, bool diff, int nee_walk, dim3 grid, size_t l
 #undef AMVPT_BOUNCE
 }
 
-template <int G> static int group_size_host(const KParams &P) { return G ? G : (int) P.G; }
-/* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
-template <int G>
-static void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
-                           const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T) {
-    constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
-    const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
-    const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
-    static const bool fuse = [] { const char *e = std::getenv("AMVPT_FUSE_PRIM"); return !(e && e[0] == '0'); }();
-    if (uni && fuse) {
-        T.begin(AMVPT_K_PRIM_HIT, st);
-        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        T.end(st);
-    } else {
-        T.begin(AMVPT_K_PRIM_HIT, st);
-        if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<true>), g256, dim3(256), lds_bvh, st, P, S, V, B);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit<false>), g256, dim3(256), lds_bvh, st, P, S, V, B);
-        T.end(st);
-        T.begin(AMVPT_K_PRIM_REQ, st);
-        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        T.end(st);
-    }
-    T.begin(AMVPT_K_VIS, st);
-    constexpr bool kVisPairs = vis_pairs<G, true>();
-    const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
-    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
-    T.end(st);
-    T.begin(AMVPT_K_MV_PRIMARY, st);
-    if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
-    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
-    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
-    T.end(st);
-}
-template <int G>
-static void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff) {
-    const bool row = AMVPT_WAVE_WIN && P.row_splat && P.C == 4;
-    if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else if (diff && row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else if (row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
-}
 
 typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams &, const DScene *, const DView *,
                            const Bufs &, bool, bool, bool, KTimer &);
@@ -2965,6 +3090,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* NEE traced inside k_bounce (brute-force walks; AMVPT_FUSE_NEE=0 keeps k_shadow, A/B) */
     bool fuse_nee = walk == WALK_BRUTE || walk == WALK_BRUTE_NS;
     { const char *e = std::getenv("AMVPT_FUSE_NEE"); if (e && e[0] == '0') fuse_nee = false; }
+    /* the whole suffix in one launch, paths in registers (brute-force walks with fused NEE;
+     * AMVPT_FUSE_SUFFIX=0 keeps the per-depth k_extend / k_bounce wavefronts, A/B) */
+    bool fuse_suffix = fuse_nee;
+    { const char *e = std::getenv("AMVPT_FUSE_SUFFIX"); if (e && e[0] == '0') fuse_suffix = false; }
+    uint32_t fused_blocks = AMVPT_FUSED_BLOCKS;
+    { const char *e = std::getenv("AMVPT_FUSED_BLOCKS"); if (e && e[0]) fused_blocks = std::max<uint32_t>(1, std::min<uint32_t>(64, (uint32_t) std::strtoul(e, nullptr, 0))); }
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
@@ -2981,6 +3112,19 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* the shared suffix (sample_suffix / sample_single loop) over the queue the raygen
      * or primary kernel filled: one k_bounce launch per depth, ping-pong A <-> B */
     auto run_suffix = [&](uint32_t cn) -> amvpt_status {
+        if (fuse_suffix) {
+            /* one k_suffix_fused launch over the primary queue (A); B's counters are its work counters */
+            for (int k = 0; k < kQPlanes; ++k) { B.q_in[k] = qa[k]; B.q_out[k] = qb[k]; }
+            B.cnt_in = cntA;
+            B.cnt_out = cntB;
+            HIPCHK(hipMemsetAsync(cntB, 0, (size_t) kQParts * kCntStride * 4, st));
+            T.begin(AMVPT_K_SUFFIX, st);
+            launch_suffix_fused(tab_b, diff, walk, dim3(kQParts * fused_blocks), lds, st, P, dS, B);
+            T.end(st);
+            HIPCHK(hipGetLastError());
+            HIPCHK(T.err);
+            return AMVPT_OK;
+        }
         /* a multiple of kQParts blocks: 1..16 per partition */
         const uint32_t bgrid = kQParts * std::max<uint32_t>(1, std::min<uint32_t>(16, (cn + 256 * kQParts - 1) / (256 * kQParts)));
         bool a_is_in = true;
@@ -3151,7 +3295,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }
         c.kernel_ms_primary = T.ms[AMVPT_K_PRIM_HIT] + T.ms[AMVPT_K_PRIM_REQ] + T.ms[AMVPT_K_VIS] +
                               T.ms[AMVPT_K_MV_PRIMARY] + T.ms[AMVPT_K_RAYGEN];
-        c.kernel_ms_bounce = T.ms[AMVPT_K_EXTEND] + T.ms[AMVPT_K_BOUNCE] + T.ms[AMVPT_K_SHADOW];
+        c.kernel_ms_bounce = T.ms[AMVPT_K_EXTEND] + T.ms[AMVPT_K_BOUNCE] + T.ms[AMVPT_K_SHADOW] + T.ms[AMVPT_K_SUFFIX];
         c.kernel_ms_splat = T.ms[AMVPT_K_SPLAT];
         c.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -3165,5 +3309,5 @@ amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h,
     return AMVPT_OK;
 }
 
-#endif /* !AMVPT_SHADOW_TU && !AMVPT_KERNEL_PROBE */
+#endif /* !AMVPT_SHADOW_TU && !AMVPT_GROUP_TU && !AMVPT_KERNEL_PROBE */
 } // namespace amvpt
