@@ -36,7 +36,6 @@ for _p in (REPO, PKG):
 
 METRIC = "Msamples/sec (whole node), 8-view 1024² 64spp; per-pixel RMSE vs llvm_rgb"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-CHUNK_LANES = 1 << 23  # amvpt_render's default lane chunk (g_chunk_lanes)
 
 
 # SURVEY 8 config table.  M = the metric's workload (the default bench line); the others are

@@ -264,7 +264,8 @@ amvpt_status amvpt_plan(const amvpt_params *params, uint32_t *spp, uint32_t *spp
 amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t width,
                            uint32_t height, uint32_t film_alpha, void *stream);
 
-/* Tuning knobs (0 keeps the default). chunk_lanes bounds the lane arena per launch. */
+/* Tuning knobs (0 keeps the default). chunk_lanes bounds the lane arena per launch; 0 restores the
+ * automatic chunk (2^25 lanes, halved down to 2^23 while the chunk's arena would exceed 24 GB). */
 amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes);
 /* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane; scenes of <= 48
  * primitives test every primitive in the suffix walks instead), 1 force the wave-uniform

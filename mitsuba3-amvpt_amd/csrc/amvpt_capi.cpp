@@ -209,7 +209,7 @@ amvpt_status amvpt_set_device(int device) {
 uint32_t amvpt_film_channels(const amvpt_params *p) { return p && p->film_alpha ? 5u : 4u; }
 
 amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes) {
-    if (chunk_lanes) g_chunk_lanes = std::max<uint64_t>(256, chunk_lanes);
+    g_chunk_lanes = chunk_lanes ? std::max<uint64_t>(256, chunk_lanes) : 0;   /* 0: automatic */
     return AMVPT_OK;
 }
 

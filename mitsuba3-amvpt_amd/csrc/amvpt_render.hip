@@ -3,7 +3,7 @@
  *
  * One frame = n_passes passes (mvpath.cpp:36-41,222-246); one pass = L lanes
  * (lane -> pixel = lane >> log2(spp_per_pass), mvpath.cpp:173-190), processed
- * in chunks of at most g_chunk_lanes lanes.  Per chunk:
+ * in chunks of at most g_chunk_lanes lanes (automatic: 2^23..2^25).  Per chunk:
  *
  *   k_mv_primary<G>  render_multisample + sample_multi up to the suffix
  *                    (jitter, sample_ray_idx, primary hit, emitter sample +
@@ -47,7 +47,10 @@
 namespace amvpt {
 
 #if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_GROUP_TU)
-uint64_t g_chunk_lanes = 1ull << 23;
+/* 0 = automatic: 2^25 lanes, halved (not below 2^23) while the chunk's arena would exceed 24 GB.
+ * Fewer, larger chunks mean fewer tails of the fused suffix and fewer kernel boundaries
+ * (config M: 2^22 386, 2^23 373, 2^24 364, 2^25 363 ms per frame; r02fd) */
+uint64_t g_chunk_lanes = 0;
 uint32_t g_traversal = 0;
 bool g_diffuse_spec = true;   /* all-diffuse kernel specialisation (AMVPT_NO_DIFFUSE_SPEC=1 turns it off) */
 amvpt_exchange_fn g_exchange = nullptr;
@@ -2997,11 +3000,16 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* lane arena: queues (2 x 5 x 16 B), lane_out + hit (32 B), NEE queue (52 B), visibility requests
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
     const uint64_t span = lane_end - lane_begin;
-    const uint64_t chunk = std::min<uint64_t>(g_chunk_lanes, span);
     const bool wide = G > kMaxG;   /* the runtime group-size instance (64-bit view masks) */
     const bool diff_rec = scene->all_diffuse && diffuse_spec && !wide;   /* kDiff instances, compact view records */
     const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8 +
                             (wide ? 48 : 0);
+    uint64_t chunk_max = g_chunk_lanes;
+    if (chunk_max == 0) {
+        chunk_max = 1ull << 25;
+        while (chunk_max > (1ull << 23) && chunk_max * per_lane > (24ull << 30)) chunk_max >>= 1;
+    }
+    const uint64_t chunk = std::min<uint64_t>(chunk_max, span);
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);

@@ -312,7 +312,7 @@ def test_many_chunks_per_pass(gpu_ready, amvpt_mod, oracle, chunk):
         assert oracle.plan(p)["lanes"] > 4 * chunk
         _check(amvpt_mod, oracle, s)
     finally:
-        amvpt_mod.set_chunk_lanes(1 << 23)
+        amvpt_mod.set_chunk_lanes(0)   # back to the automatic chunk
 
 
 @pytest.mark.parametrize("gx,gy,reuse", [(4, 4, 16), (4, 3, 12)], ids=["g16", "g12"])
