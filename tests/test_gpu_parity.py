@@ -375,3 +375,46 @@ def test_veach_weighted_emitter_sampling(gpu_ready, amvpt_mod, oracle):
     distr_1d.h:116-215): binary search over the float CDF, re-used sample, pmf = weight / sum."""
     s = amvpt_mod.load_file(VEACH_W, res=24, spp=16, w0=0.25, w1=1, w2=2.5, w3=4)
     _check(amvpt_mod, oracle, s)
+
+
+@pytest.mark.parametrize("adaptive", [0, 2])
+def test_fused_suffix_matches_wavefront_suffix(gpu_ready, amvpt_mod, oracle, monkeypatch, adaptive):
+    """k_suffix_fused (paths in registers, brute-force scenes) vs the per-depth k_extend / k_bounce
+    wavefronts (AMVPT_FUSE_SUFFIX=0) on the same lanes: records bit-identical, the same vertex and
+    shadow-ray counts, and each launch path actually taken (kernel launch counters)."""
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=32, spp=32, gx=4, gy=2, reuse=8, adaptive=adaptive)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("AMVPT_FUSE_SUFFIX", fused)
+        dev = amvpt_mod.DeviceScene(sd)
+        film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+        rec = torch.zeros((plan["lanes"], plan["group"], 8), dtype=torch.float32, device="cuda")
+        dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, 0, plan["lanes"])
+        cnt = amvpt_mod.Counters()
+        film2 = torch.zeros_like(film)
+        dev.render(vd, p, film2.data_ptr(), counters=cnt)
+        torch.cuda.synchronize()
+        out[fused] = (rec.cpu().numpy(), film2.cpu().numpy(), cnt.as_dict())
+    (r1, f1, c1), (r0, f0, c0) = out["1"], out["0"]
+    assert c1["kernel_launches"]["k_suffix"] > 0 and c1["kernel_launches"]["k_extend"] == 0
+    assert c0["kernel_launches"]["k_suffix"] == 0 and c0["kernel_launches"]["k_extend"] > 0
+    for k in ("vertices", "shadow_rays", "lanes", "adaptive_lanes", "view_splats"):
+        assert c1[k] == c0[k], k
+    assert _bit_equal(r1, r0).all()
+    assert np.abs(f1 - f0).max() <= 1e-5 * np.abs(f0).max()
+
+
+def test_mesh_scene_keeps_wavefront_suffix(gpu_ready, amvpt_mod):
+    """Scenes above the brute-force size (the 3.6 k-triangle mesh box) run the per-depth suffix."""
+    torch = _torch()
+    s = amvpt_mod.load_file(MESH, res=16, spp=16, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    cnt = amvpt_mod.Counters()
+    amvpt_mod.DeviceScene(sd).render(vd, p, film.data_ptr(), counters=cnt)
+    torch.cuda.synchronize()
+    d = cnt.as_dict()
+    assert d["kernel_launches"]["k_suffix"] == 0 and d["kernel_launches"]["k_extend"] > 0
