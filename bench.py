@@ -261,6 +261,10 @@ def main():
                 # VALU issue (the kernels are VALU/latency-bound, not HBM-bound): committed SQ PMC
                 # wave-instruction counts per launch / this run's launch time, vs 1228.8 G/s
                 "valu_issue": valu,
+                "note": ("the dominant kernel keeps its paths in registers (k_suffix_fused): its algorithmic "
+                         "HBM bytes are 96 B per path, so its HBM fraction is small by design; it is bound "
+                         "by VALU issue (valu_issue) -- pipeline_model is the metric's roofline")
+                        if dom == "k_suffix" else None,
                 "pipeline_model": {"B_sample": round(B_sample, 1), "vbar": round(vbar, 4), "hbar": round(hbar, 4),
                                    "achieved_GBs": round(pipeline_gbs, 2),
                                    "frac": round(pipeline_gbs / HBM_PEAK_GBS, 5)},

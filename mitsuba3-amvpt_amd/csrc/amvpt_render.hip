@@ -1627,8 +1627,9 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
 #ifndef AMVPT_FUSED_BLOCKS
 /* blocks per queue partition (x kQParts blocks of 256 threads), more than are resident at once:
  * blocks that start late find their partition partly drained, which evens out the tail
- * (config M, suffix ms: 5 -> 163.7, 8 -> 149.0, 16 -> 144.8, 24..64 -> 144.8; r02fb) */
-#define AMVPT_FUSED_BLOCKS 16
+ * (config M, 2^23-lane chunks, suffix ms: 5 -> 163.7, 8 -> 149.0, 16 -> 144.8, 24..64 -> 144.8,
+ * r02fb; 2^25-lane chunks: 12 -> 135.2, 16 -> 133.5, 24 -> 132.4, 32 -> 132.7, r02fm) */
+#define AMVPT_FUSED_BLOCKS 24
 #endif
 #ifndef AMVPT_FUSED_WAVES
 /* 6 waves/SIMD (80 VGPRs, 24 B of spills): suffix 146.4 -> 143.2 ms per config-M frame; 4 waves 157.8 (r02fc) */
@@ -2408,6 +2409,9 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
 
 /* waves per SIMD the register allocation must allow: the 30-KB window admits 5 blocks (20 waves)
  * per CU, and 5 (<= 96 VGPRs) no longer spills (113.8 vs 117.9 ms per config-M frame, A/B r02z) */
+#ifndef AMVPT_SPLAT_SKIP
+#define AMVPT_SPLAT_SKIP 1   /* skip views without a valid splat in the wave (0: off, A/B) */
+#endif
 #ifndef AMVPT_SPLAT_WAVES
 #define AMVPT_SPLAT_WAVES 5
 #endif
@@ -2470,6 +2474,9 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     uint32_t splats = 0, fallback = 0, nonfinite = 0, negative = 0;   /* per lane, <= G each */
 #pragma unroll 1
     for (int k = 0; k < Gn; ++k) {
+        /* a view no lane of the wave splats into: no reprojection, no put (all-diffuse records carry
+         * the valid bits in the lane record; records / debug mode write every view's entry) */
+        if (AMVPT_SPLAT_SKIP && kDiff && k > 0 && !P.record && !P.debug && !wave_any(ok && ((vmask >> k) & 1u))) continue;
         const size_t o = (size_t) k * n + slot;
         float weight = 0.f;
         bool valid = false;

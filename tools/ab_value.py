@@ -20,6 +20,8 @@ def child(steps=3, kernels=False):
     import amvpt
     if os.environ.get("AB_CHUNK"):
         amvpt.set_chunk_lanes(int(os.environ["AB_CHUNK"]))
+    if os.environ.get("AB_TRAV"):
+        amvpt.set_traversal(int(os.environ["AB_TRAV"]))
     s = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), res=1024, spp=64, gx=4, gy=2, reuse=8)
     sd, vd, p = s.describe(0, 0, 0)
     dev = amvpt.DeviceScene(sd)
