@@ -658,19 +658,22 @@ constexpr int kSplatSuper = 1024;   /* lanes per splat super-block (see slot_lan
 constexpr int kSplatBlock = AMVPT_SPLAT_BLOCK;   /* threads per splat block (see slot_lane) */
 constexpr int kWinCells = kWinW * kWinH;
 /*
- * Window cell format.  AMVPT_WIN_FIXED = 1 (default): signed 32.32 fixed point in an int64 word,
- * accumulated with ds_add_u64 -- 9.7 lane-ops/clk/CU against 7.5 for ds_add_f64 on gfx950
- * (tools/ubench_lds.hip, 8-B stride; profiles/r02a_ubench.log).  Integer adds are exact and
- * order-independent, so a block's window sum no longer depends on the order of its adds; each
- * contribution is truncated to 2^-32 (~2e-10, far below the f32 film's resolution at the film's
- * scale).  Samples with a non-finite channel or one of magnitude >= 2^20 bypass the window
- * (direct global float atomics), so a cell sum stays far from int64 overflow and NaN/Inf still
- * reach the film as in the reference.  AMVPT_WIN_FIXED = 0: fp64 cells with ds_add_f64.
+ * Window cell format.  AMVPT_WIN_FIXED = 0 (default): fp64 cells accumulated with ds_add_f64 --
+ * each f32 contribution is exact in f64 and a cell holds at most a few hundred of them, so the
+ * window sum is the exact sum to far below the f32 film's resolution.  AMVPT_WIN_FIXED = 1: signed
+ * 32.32 fixed point in an int64 word with ds_add_u64 (9.7 lane-ops/clk/CU against 7.5 for
+ * ds_add_f64 in isolation, tools/ubench_lds.hip, profiles/r02a_ubench.log; order-independent
+ * integer sums, values of magnitude >= 2^20 or non-finite bypass the window) -- but its six-VALU
+ * conversion per add costs more than the atomic rate gains now that the row splat is VALU-bound:
+ * config-M splat 105.0 ms fixed vs 99.8 ms fp64 (r02fo, r02fp).  AMVPT_WIN_FIXED = 2: fp32 cells
+ * with ds_add_f32: 142 ms (the 64-bit bank layout of the row adds no longer spreads).
  */
 #ifndef AMVPT_WIN_FIXED
-#define AMVPT_WIN_FIXED 1
+#define AMVPT_WIN_FIXED 0
 #endif
-#if AMVPT_WIN_FIXED
+#if AMVPT_WIN_FIXED == 2
+typedef float WinT;        /* fp32 cells, ds_add_f32 (A/B) */
+#elif AMVPT_WIN_FIXED
 typedef long long WinT;
 #else
 typedef double WinT;
@@ -783,10 +786,13 @@ AD void lds_add64(long long *p, long long v) {
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 AD void win_add(double *p, float x) { lds_add64(p, (double) x); }
+AD void win_add(float *p, float x) {
+    (void) __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 AD void win_add(long long *p, float x) { lds_add64(p, to_fixed(x)); }
 /* may the sample go through the window?  (fixed point: finite and below 2^20 in every channel) */
 template <int C> AD bool win_fits(const float *vals) {
-#if AMVPT_WIN_FIXED
+#if AMVPT_WIN_FIXED == 1
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < C; ++k) ok = ok && fabsf(vals[k]) < kFixMax;
@@ -860,7 +866,11 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
         const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
         WinT *src = win + k * plane + cy * w.rs + cx;
         const WinT d = *src;
-#if AMVPT_WIN_FIXED
+#if AMVPT_WIN_FIXED == 2
+        if (__float_as_int(d) != 0) {
+            *src = 0.f;
+            const float v = d;
+#elif AMVPT_WIN_FIXED
         if (d != 0) {
             *src = 0;
             const float v = from_fixed(d);
@@ -1074,7 +1084,11 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
         const int r = e - cy * rowlen, cx = r / C, k = r - cx * C;
         WinT *src = win + k * w.plane + cy * w.rs + cx;
         const WinT d = *src;
-#if AMVPT_WIN_FIXED
+#if AMVPT_WIN_FIXED == 2
+        if (__float_as_int(d) != 0) {
+            *src = 0.f;
+            const float v = d;
+#elif AMVPT_WIN_FIXED
         if (d != 0) {
             *src = 0;
             const float v = from_fixed(d);
