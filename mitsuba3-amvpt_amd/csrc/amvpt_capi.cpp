@@ -41,6 +41,14 @@ static inline void hcross(const float *a, const float *b, float *o) {
     o[1] = std::fmaf(a[2], b[0], -(a[0] * b[2]));
     o[2] = std::fmaf(a[0], b[1], -(a[1] * b[0]));
 }
+/* .5 * dr::norm(dr::cross(p1 - p0, p2 - p0)) (mesh.cpp:470) */
+static inline float tri_area(const float *p0, const float *p1, const float *p2) {
+    const float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+    const float e1[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};
+    float c[3];
+    hcross(e0, e1, c);
+    return .5f * std::sqrt(hdot(c, c));
+}
 
 /* ---------------------------------------------------------------- */
 /* Binned SAH BVH                                                    */
@@ -315,7 +323,6 @@ static amvpt_status validate_scene(const amvpt_scene_desc *d) {
         }
         if (e.type != AMVPT_EMITTER_AREA) { set_error("unknown emitter type"); return AMVPT_ERR_INVALID; }
         if (e.shape < 0 || (uint32_t) e.shape >= d->shape_count) { set_error("emitter without a valid shape"); return AMVPT_ERR_INVALID; }
-        if (d->shapes[e.shape].type == AMVPT_SHAPE_MESH) { set_error("area emitters on meshes are not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     }
 
     for (uint32_t i = 0; i < d->shape_count; ++i) {
@@ -334,6 +341,15 @@ static amvpt_status validate_scene(const amvpt_scene_desc *d) {
             if (!s.positions || !s.faces) { set_error("mesh without positions/faces"); return AMVPT_ERR_INVALID; }
             for (size_t f = 0; f < 3 * (size_t) s.face_count; ++f)
                 if (s.faces[f] >= s.vertex_count) { set_error("mesh face index >= vertex_count"); return AMVPT_ERR_INVALID; }
+            if (s.emitter >= 0) {
+                /* Mesh::build_pmf (mesh.cpp:448-449) / DiscreteDistribution::compute_cdf (distr_1d.h) */
+                if (s.face_count == 0) { set_error("Cannot create sampling table for an empty mesh"); return AMVPT_ERR_INVALID; }
+                float acc = 0.f;
+                for (uint32_t f = 0; f < s.face_count; ++f)
+                    acc += tri_area(s.positions + 3 * s.faces[3 * f], s.positions + 3 * s.faces[3 * f + 1],
+                                    s.positions + 3 * s.faces[3 * f + 2]);
+                if (!(acc > 0.f)) { set_error("DiscreteDistribution: no probability mass found!"); return AMVPT_ERR_INVALID; }
+            }
         } else if (s.type != AMVPT_SHAPE_RECTANGLE && s.type != AMVPT_SHAPE_SPHERE) {
             set_error("unknown shape type");
             return AMVPT_ERR_INVALID;
@@ -396,7 +412,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (!device_ok()) { set_error("amvpt_scene_create: no HIP device visible (the product path has no CPU fallback)"); return AMVPT_ERR_NO_DEVICE; }
     bool has_spheres = false;
     std::vector<DShape> shapes(d->shape_count);
-    std::vector<float> vpos, vnrm, vuv;
+    std::vector<float> vpos, vnrm, vuv, face_area;
     std::vector<uint32_t> faces;
     std::vector<BuildPrim> bprims;
     std::vector<DPrim> scene_prims; /* scene order */
@@ -454,6 +470,18 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
                 vuv.insert(vuv.end(), s.texcoords, s.texcoords + 2 * (size_t) s.vertex_count);
             }
             faces.insert(faces.end(), s.faces, s.faces + 3 * (size_t) s.face_count);
+            /* Mesh::build_pmf (mesh.cpp:444-485): face areas .5 |(p1 - p0) x (p2 - p0)|, float prefix sum */
+            float acc = 0.f;
+            for (uint32_t f = 0; f < s.face_count; ++f) {
+                const float a = tri_area(s.positions + 3 * s.faces[3 * f], s.positions + 3 * s.faces[3 * f + 1],
+                                         s.positions + 3 * s.faces[3 * f + 2]);
+                acc += a;
+                face_area.push_back(a);
+                face_area.push_back(acc);
+            }
+            o.n_faces = s.face_count;
+            o.area_sum = acc;
+            o.inv_area = acc != 0.f ? 1.f / acc : 0.f;
             for (uint32_t f = 0; f < s.face_count; ++f) {
                 DPrim p{};
                 const float *P0 = s.positions + 3 * s.faces[3 * f], *P1 = s.positions + 3 * s.faces[3 * f + 1],
@@ -572,6 +600,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (vnrm.empty()) vnrm.resize(3, 0.f);
     if (vuv.empty()) vuv.resize(2, 0.f);
     if (faces.empty()) faces.resize(3, 0);
+    if (face_area.empty()) face_area.resize(2, 0.f);
 
     amvpt_scene *sc = new amvpt_scene();
     sc->has_spheres = has_spheres;
@@ -584,7 +613,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", (int) e);
         return AMVPT_OK;
     };
-    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces;
+    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea;
     amvpt_status st;
 #define UP(vec, ptr)                                                                      \
     if ((st = upload(vec.data(), vec.size() * sizeof(vec[0]), &ptr)) != AMVPT_OK) {       \
@@ -592,7 +621,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         return st;                                                                        \
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
-    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces)
+    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -604,6 +633,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.vnrm = (const float *) p_vnrm;
     D.vuv = (const float *) p_vuv;
     D.faces = (const uint32_t *) p_faces;
+    D.face_area = (const float *) p_farea;
     D.n_nodes = oct_stride ? oct_stride : (uint32_t) nodes.size();
     D.oct_stride = oct_stride;
     D.n_prims = (uint32_t) prims.size();

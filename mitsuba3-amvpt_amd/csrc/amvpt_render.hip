@@ -280,6 +280,53 @@ AD uint32_t sample_emitter(const DScene &S, float &u, float &weight) {
 }
 
 /*
+ * Mesh::sample_position (mesh.cpp:765-816) + Shape::sample_direction (shape.cpp:360-377):
+ * the face from m_area_pmf.sample_reuse (distr_1d.h: JIT predicate of sample(), binary search
+ * over [0, n - 1]), a uniform point on it (warp::square_to_uniform_triangle), the interpolated
+ * shading normal when the mesh has vertex normals, else the face normal.
+ */
+AD DSamp mesh_sample_direction(const DScene &S, const DShape &s, f3 itp, float u1, float u2) {
+    DSamp ds = ds_zero();
+    const float2 *tab = reinterpret_cast<const float2 *>(S.face_area) + s.fbase;
+    const float sum = s.area_sum, norm_ = s.inv_area, sample = u2 * sum;
+    uint32_t start = 0, end = s.n_faces - 1u;
+    const uint32_t it = end ? 32u - (uint32_t) __builtin_clz(end) : 0u;
+    for (uint32_t k = 0; k < it; ++k) {
+        const uint32_t middle = (start + end) >> 1;
+        const float c = tab[middle].y;
+        const bool cond = ((c < sample) || c == 0.f) && c != sum;
+        start = cond ? min(middle + 1u, end) : start;
+        end = cond ? end : middle;
+    }
+    const float pmf = tab[start].x * norm_, cdf = start > 0 ? tab[start - 1].y * norm_ : 0.f;
+    u2 = (u2 - cdf) / pmf;
+    const uint32_t *fi = S.faces + 3 * (size_t) (s.fbase + start);
+    const uint32_t i0 = s.vbase + fi[0], i1 = s.vbase + fi[1], i2 = s.vbase + fi[2];
+    const f3 p0 = ld3(S.vpos + 3 * (size_t) i0), p1 = ld3(S.vpos + 3 * (size_t) i1), p2 = ld3(S.vpos + 3 * (size_t) i2);
+    const f3 e0 = p1 - p0, e1 = p2 - p0;
+    const float t = safe_sqrt(1.f - u1), bx = 1.f - t, by = t * u2;
+    ds.p = fma3(e0, bx, fma3(e1, by, p0));
+    f3 n;
+    if (s.has_normals) {
+        const f3 n0 = ld3(S.vnrm + 3 * (size_t) i0), n1 = ld3(S.vnrm + 3 * (size_t) i1),
+                 n2 = ld3(S.vnrm + 3 * (size_t) i2);
+        n = fma3(n0, 1.f - bx - by, fma3(n1, bx, n2 * by));
+    } else {
+        n = cross(e0, e1);
+    }
+    ds.n = normalize(n);
+    if (s.flip) ds.n = -ds.n;
+    ds.pdf = norm_;
+    ds.d = ds.p - itp;
+    const float d2 = sqnorm(ds.d);
+    ds.dist = dsqrt(d2);
+    ds.d = ds.d / ds.dist;
+    const float x = d2 / absdot(ds.d, ds.n);
+    ds.pdf *= finite_(x) ? x : 0.f;
+    return ds;
+}
+
+/*
  * Scene::sample_emitter_direction (scene.cpp:294-348) up to its ray_test: returns
  * true when the reference would trace the shadow ray spawn_ray_to(ref.p, ref.n,
  * ds.p).  The test itself runs in its own wavefront (k_vis slot 0 for primary
@@ -310,7 +357,7 @@ AD bool sample_emitter_direction(const SceneRef &sc, const SI &ref, float u1, fl
         spec = c3(em.radiance) / ds.pdf;
     } else {
         const DShape &s = S.shapes[em.shape];
-        ds = shape_sample_direction(s, ref.p, u1, u2);
+        ds = s.type == PRIM_TRI ? mesh_sample_direction(S, s, ref.p, u1, u2) : shape_sample_direction(s, ref.p, u1, u2);
         bool a = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
         spec = csel(a, c3(em.radiance) / ds.pdf, c3(0.f));
     }

@@ -52,6 +52,8 @@ struct DShape {
     float inv_area;
     uint32_t vbase, fbase, has_normals, has_uv;
     float center[3], radius;
+    uint32_t n_faces;       /* mesh: face count of its area distribution (Mesh::m_area_pmf) */
+    float area_sum;         /* mesh: m_area_pmf.sum(); inv_area holds its normalization() */
 };
 
 struct DBsdf {
@@ -98,6 +100,7 @@ struct DScene {
     const float *vnrm;
     const float *vuv;
     const uint32_t *faces;  /* 3 per face, indices relative to the shape's vbase */
+    const float *face_area; /* (pmf, inclusive cdf) per face at 2 * (fbase + f): Mesh::m_area_pmf */
     uint32_t n_nodes, n_prims, n_shapes, n_emitters;
     float emitter_pmf;
     int32_t environment;    /* the constant emitter's index, or -1 */

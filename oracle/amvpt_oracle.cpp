@@ -161,6 +161,9 @@ struct Shape {
     std::vector<uint32_t> faces;
     float center[3];
     float radius;
+    /* Mesh::m_area_pmf (mesh.cpp:444-485): face areas and their inclusive float prefix sums */
+    std::vector<float> area_pmf, area_cdf;
+    float area_sum = 0.f;
 };
 
 struct Scene {
@@ -499,7 +502,47 @@ static DS shape_sample_direction(const Shape &s, V3 itp, V2 sample) {
         if (s.flip) res.n = -res.n;
         return res;
     }
-    return ds; /* mesh emitters are rejected at scene creation */
+    /* Mesh::sample_position (mesh.cpp:765-816): DiscreteDistribution::sample_reuse over the face
+     * areas (JIT predicate of sample(), distr_1d.h:116-134), warp::square_to_uniform_triangle */
+    const uint32_t n = (uint32_t) s.area_pmf.size();
+    const float norm_ = s.inv_area, value = sample.y * s.area_sum;
+    uint32_t start = 0, end = n - 1u;
+    const uint32_t iters = end ? 32u - (uint32_t) __builtin_clz(end) : 0u;
+    for (uint32_t k = 0; k < iters; ++k) {
+        const uint32_t middle = (start + end) >> 1;
+        const float c = s.area_cdf[middle];
+        const bool cond = ((c < value) || c == 0.f) && c != s.area_sum;
+        start = cond ? std::min(middle + 1u, end) : start;
+        end = cond ? end : middle;
+    }
+    const float pmf = s.area_pmf[start] * norm_, cdf = start > 0 ? s.area_cdf[start - 1] * norm_ : 0.f;
+    sample.y = (sample.y - cdf) / pmf;
+    const uint32_t i0 = s.faces[3 * start], i1 = s.faces[3 * start + 1], i2 = s.faces[3 * start + 2];
+    V3 p0 = vtx(s, i0), p1 = vtx(s, i1), p2 = vtx(s, i2);
+    V3 e0 = p1 - p0, e1 = p2 - p0;
+    float t = safe_sqrt(1.f - sample.x), bx = 1.f - t, by = t * sample.y;
+    ds.p = fmadd(e0, bx, fmadd(e1, by, p0));
+    V3 n3;
+    if (!s.nrm.empty()) {
+        V3 n0{s.nrm[3 * i0], s.nrm[3 * i0 + 1], s.nrm[3 * i0 + 2]}, n1{s.nrm[3 * i1], s.nrm[3 * i1 + 1], s.nrm[3 * i1 + 2]},
+            n2{s.nrm[3 * i2], s.nrm[3 * i2 + 1], s.nrm[3 * i2 + 2]};
+        n3 = fmadd(n0, 1.f - bx - by, fmadd(n1, bx, n2 * by));
+    } else {
+        n3 = cross(e0, e1);
+    }
+    ds.n = normalize(n3);
+    if (s.flip) ds.n = -ds.n;
+    ds.pdf = norm_;
+    ds.uv = V2{bx, by};
+    ds.delta = false;
+    /* Shape::sample_direction (shape.cpp:360-377) */
+    ds.d = ds.p - itp;
+    float dist_squared = squared_norm(ds.d);
+    ds.dist = std::sqrt(dist_squared);
+    ds.d = ds.d / ds.dist;
+    float x = dist_squared / absdot(ds.d, ds.n);
+    ds.pdf *= isfinite_(x) ? x : 0.f;
+    return ds;
 }
 
 static float shape_pdf_direction(const Shape &s, V3 itp, const DS &ds) {
@@ -1505,6 +1548,16 @@ bool build_scene(const amvpt_scene_desc *d, Scene &sc) {
             if (s.normals) sh.nrm.assign(s.normals, s.normals + 3 * s.vertex_count);
             if (s.texcoords) sh.uv.assign(s.texcoords, s.texcoords + 2 * s.vertex_count);
             sh.faces.assign(s.faces, s.faces + 3 * s.face_count);
+            float acc = 0.f;
+            for (uint32_t f = 0; f < s.face_count; ++f) {
+                V3 p0 = vtx(sh, sh.faces[3 * f]), p1 = vtx(sh, sh.faces[3 * f + 1]), p2 = vtx(sh, sh.faces[3 * f + 2]);
+                const float a = .5f * norm(cross(p1 - p0, p2 - p0)); /* mesh.cpp:470 */
+                acc += a;
+                sh.area_pmf.push_back(a);
+                sh.area_cdf.push_back(acc);
+            }
+            sh.area_sum = acc;
+            sh.inv_area = acc != 0.f ? 1.f / acc : 0.f;
             for (uint32_t f = 0; f < s.face_count; ++f) sc.prims.push_back({AMVPT_SHAPE_MESH, i, f});
         } else {
             std::memcpy(sh.center, s.center, sizeof(sh.center));
@@ -1617,7 +1670,9 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
     Scene sc;
     if (!build_scene(sd, sc)) return 4;
     for (auto &e : sc.emitters)
-        if (e.type == AMVPT_EMITTER_AREA && sc.shapes[e.shape].type == AMVPT_SHAPE_MESH) return 4;
+        if (e.type == AMVPT_EMITTER_AREA && sc.shapes[e.shape].type == AMVPT_SHAPE_MESH &&
+            !(sc.shapes[e.shape].area_sum > 0.f))
+            return 4; /* Mesh::build_pmf: "no probability mass found" */
     amvpt_params P = *params;
     uint32_t spp, spp_pp, n_passes;
     uint64_t L;

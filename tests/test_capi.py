@@ -85,9 +85,9 @@ def test_product_modules_never_import_the_oracle():
                 assert not bad.search(txt), os.path.join(root, f)
 
 
-def _cbox_desc(amvpt_mod):
+def _cbox_desc(amvpt_mod, name="cbox_grid.xml"):
     from conftest import SCENES
-    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=8, spp=4)
+    s = amvpt_mod.load_file(os.path.join(SCENES, name), res=8, spp=4)
     sd, vd, p = s.describe(0, 0, 0)
     return s, sd, vd, p
 
@@ -105,13 +105,14 @@ def _copy_scene(amvpt_mod, sd):
 
 
 @pytest.mark.parametrize("breakage", ["emitter_range", "emitter_pair", "face_index", "bsdf_range",
-                                      "env_count", "env_shape", "negative_weight", "zero_weights"])
+                                      "env_count", "env_shape", "negative_weight", "zero_weights",
+                                      "mesh_light_no_area"])
 def test_scene_create_rejects_malformed_descriptors(amvpt_mod, breakage):
     """Malformed C-ABI input is refused with AMVPT_ERR_INVALID before any device work:
     shape.emitter outside [-1, emitter_count), emitter.shape / shape.emitter disagreeing, mesh face
     indices >= vertex_count, BSDF indices out of range."""
     L = amvpt_mod.hip_lib()
-    s, sd, vd, p = _cbox_desc(amvpt_mod)
+    s, sd, vd, p = _cbox_desc(amvpt_mod, "cbox_meshlight.xml" if breakage == "mesh_light_no_area" else "cbox_grid.xml")
     nd, shapes, bsdfs, ems = _copy_scene(amvpt_mod, sd)
     keep = []
     if breakage == "emitter_range":
@@ -127,6 +128,11 @@ def test_scene_create_rejects_malformed_descriptors(amvpt_mod, breakage):
         faces[n - 1] = shapes[mesh].vertex_count
         keep.append(faces)
         shapes[mesh].faces = ctypes.cast(faces, ctypes.POINTER(ctypes.c_uint32))
+    elif breakage == "mesh_light_no_area":
+        light = next(i for i in range(nd.shape_count) if shapes[i].type == 1 and shapes[i].emitter >= 0)
+        flat = (ctypes.c_float * (3 * shapes[light].vertex_count))()   # every vertex at the origin
+        keep.append(flat)
+        shapes[light].positions = ctypes.cast(flat, ctypes.POINTER(ctypes.c_float))
     elif breakage == "env_count":
         nd.has_environment = 1               # claims a constant emitter the table does not hold
     elif breakage == "env_shape":
@@ -150,10 +156,12 @@ def test_scene_create_rejects_malformed_descriptors(amvpt_mod, breakage):
     assert L.amvpt_last_error().decode()
 
 
-def test_scene_create_accepts_the_loaded_descriptor(amvpt_mod):
-    """The unmodified loader output passes validation (then needs a device)."""
+@pytest.mark.parametrize("name", ["cbox_grid.xml", "cbox_meshlight.xml"])
+def test_scene_create_accepts_the_loaded_descriptor(amvpt_mod, name):
+    """The unmodified loader output passes validation (then needs a device); area emitters on
+    meshes are accepted (mesh.cpp:765-816)."""
     L = amvpt_mod.hip_lib()
-    s, sd, vd, p = _cbox_desc(amvpt_mod)
+    s, sd, vd, p = _cbox_desc(amvpt_mod, name)
     nd, shapes, bsdfs, ems = _copy_scene(amvpt_mod, sd)
     h = ctypes.c_void_p()
     rc = L.amvpt_scene_create(ctypes.byref(nd), ctypes.byref(h))

@@ -418,3 +418,20 @@ def test_mesh_scene_keeps_wavefront_suffix(gpu_ready, amvpt_mod):
     torch.cuda.synchronize()
     d = cnt.as_dict()
     assert d["kernel_launches"]["k_suffix"] == 0 and d["kernel_launches"]["k_extend"] > 0
+
+
+MESHLIGHT = os.path.join(SCENES, "cbox_meshlight.xml")
+
+
+@pytest.mark.parametrize("defines", [
+    dict(res=32, spp=16),                               # G = 4, two mesh lights, uniform picking
+    dict(res=24, spp=16, gx=4, gy=2, reuse=8),          # G = 8
+    dict(res=24, spp=16, reuse=1),                      # G = 1 (render_sample)
+], ids=["g4", "g8", "g1"])
+def test_mesh_area_emitters(gpu_ready, amvpt_mod, oracle, defines):
+    """Area emitters on meshes: Mesh::sample_position (mesh.cpp:765-816) picks a face from the
+    float area CDF with DiscreteDistribution::sample_reuse and a uniform barycentric point
+    (interpolated vertex normal on the icosphere, face normal on the flat cube);
+    Shape::pdf_direction (shape.cpp:379-390) prices emitter hits by 1 / surface area."""
+    s = amvpt_mod.load_file(MESHLIGHT, **defines)
+    _check(amvpt_mod, oracle, s)

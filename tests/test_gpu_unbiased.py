@@ -39,6 +39,8 @@ pytestmark = pytest.mark.gpu
 
 CBOX = os.path.join(SCENES, "cbox_grid.xml")
 VEACH = os.path.join(SCENES, "veach_grid.xml")
+MESHLIGHT = os.path.join(SCENES, "cbox_meshlight.xml")
+RECTLIGHTS = os.path.join(SCENES, "cbox_cubelight_rects.xml")
 K = 24   # independent seeds per side
 
 
@@ -110,6 +112,25 @@ def test_amvpt_views_unbiased_against_single_view(gpu_ready, amvpt_mod, name, pa
           "per-view |z| max %.2f, mean ratio %s" % (
               name, frac, int(smooth.sum()) * 3, alpha, pmin, full, zv.max(),
               np.round(vt.mean(0) / vr.mean(0), 4).tolist()))
+    assert frac >= 0.9975, "Z-test rejects: only %.4f of smooth-footprint pixel channels pass" % frac
+    assert zv.max() < 4.5, "per-view mean differs: |z| = %s" % np.round(zv, 2).tolist()
+
+
+def test_mesh_light_matches_rectangle_lights(gpu_ready, amvpt_mod):
+    """Area emitter on a mesh (mesh.cpp:765-816: area-CDF face pick, barycentric point) against the
+    same flat box emitting as six rectangles (rectangle.cpp sampling): two different unbiased
+    estimators of one image, compared with the reference's Z-test (test_renders.py:159-230)."""
+    defines = dict(res=48, spp=64, gx=2, gy=2, reuse=4)
+    test = _frames(amvpt_mod, MESHLIGHT, range(K), **defines)
+    ref = _frames(amvpt_mod, RECTLIGHTS, range(1000, 1000 + K), **dict(defines, spp=256))
+    assert np.isfinite(test).all() and np.isfinite(ref).all()
+    res = defines["res"]
+    smooth = _smooth(ref.mean(0), res)
+    frac, pmin, alpha = _z_gate(test[:, smooth], ref[:, smooth])
+    vt, vr = _view_means(test, res), _view_means(ref, res)
+    zv = np.abs(vt.mean(0) - vr.mean(0)) / np.sqrt(vt.var(0, ddof=1) / K + vr.var(0, ddof=1) / K)
+    print("mesh light vs rectangles: gate %.4f (min p %.3g), per-view |z| max %.2f, mean ratio %s" % (
+        frac, pmin, zv.max(), np.round(vt.mean(0) / vr.mean(0), 4).tolist()))
     assert frac >= 0.9975, "Z-test rejects: only %.4f of smooth-footprint pixel channels pass" % frac
     assert zv.max() < 4.5, "per-view mean differs: |z| = %s" % np.round(zv, 2).tolist()
 
