@@ -92,7 +92,7 @@ typedef struct amvpt_bsdf_desc {
 } amvpt_bsdf_desc;
 
 enum {
-    AMVPT_EMITTER_AREA = 0,     /* src/emitters/area.cpp: attached to a rectangle / sphere shape */
+    AMVPT_EMITTER_AREA = 0,     /* src/emitters/area.cpp: attached to a rectangle / sphere / mesh shape */
     AMVPT_EMITTER_CONSTANT = 1  /* src/emitters/constant.cpp: environment, shape = -1 */
 };
 
