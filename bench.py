@@ -6,12 +6,17 @@ sa_reuse + sa_mis, reuse_count 8, max_depth 8, rr_depth 5, seed 0.
 One step = one full frame of that workload on every rank (scene upload, film
 allocation and plan are outside the timed region; inputs are resident in HBM).
 
-Multi-GPU (one process per GPU, RCCL over xGMI): strong scaling by lane sharding
-(SURVEY 8(e)).  Every rank renders the contiguous lane range lane_shard(L, r, N) of
-every pass of the SAME 64-spp frame (a band of quilt rows; lanes keep their global
-TEA seeds, so the image is the single-GPU one), and the RGBW ImageBlocks are summed
-on rank 0 with one RCCL reduce inside the timed region.  `--weak` instead renders
-passes [4r, 4r+4) of a (64*N)-spp frame (pass sharding; labelled "weak").
+Multi-GPU (one process per GPU, RCCL over xGMI): strong scaling; every rank
+renders its share of the SAME frame (lanes keep their global TEA seeds, so the image is the
+single-GPU one) inside the timed region, and rank 0 ends the step holding the whole ImageBlock:
+  * view groups (C5, "4 views per GPU"; the default whenever the groups divide among the ranks):
+    rank r renders the lanes of its groups' quilt tiles into a film window of those tiles + a
+    4-px filter border (amvpt_render_ex), and the windows are gathered on rank 0 (borders and the
+    few overflow cells summed) -- no full-quilt film per rank, no reduce;
+  * lane bands (M / C3 / C4: one group of 8 views): rank r renders the contiguous lane range of
+    a cost-balanced band of quilt rows of every pass, and the RGBW ImageBlocks are summed on
+    rank 0 with one RCCL reduce.
+`--weak` instead renders passes [4r, 4r+4) of a (64*N)-spp frame (pass sharding; labelled "weak").
 
 After the timed region rank 0 also reports `rmse_vs_oracle`: the per-pixel RMSE of
 the developed film of a stated lane window of the same workload, HIP pipeline vs the
@@ -82,6 +87,8 @@ def main():
     ap.add_argument("--gy", type=int, default=None)
     ap.add_argument("--reuse", type=int, default=None)
     ap.add_argument("--adaptive", type=int, default=None)
+    ap.add_argument("--partition", choices=("auto", "lanes", "view-groups"), default="auto",
+                    help="multi-GPU partition of the frame (auto: view groups when they divide among the ranks)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -89,7 +96,7 @@ def main():
     for k in ("res", "spp", "gx", "gy", "reuse", "adaptive"):
         if getattr(args, k) is not None:
             cfg[k] = getattr(args, k)
-    headline = cfg == CONFIGS["M"]   # PMC traffic in profiles/ was collected on exactly this workload
+    prof_config = args.config if cfg == CONFIGS[args.config] else "custom"   # workload key of the PMC summaries
     scene_file = cfg.pop("scene")
     lane_sharded = not args.weak
 
@@ -112,45 +119,82 @@ def main():
     sd, vd, p = scene.describe(0, 0, 0)
     plan = amvpt.plan(p)
     spp, spp_pp, n_passes, lanes_per_pass = plan
-    if lane_sharded:
-        # strong scaling: this rank's lanes of every pass of ONE frame; the adaptive fill's
-        # prefix/total come from one all-gather per pass (amvpt.dist.count_exchange)
-        lane_begin, lane_end = adist.lane_shard(lanes_per_pass, rank, world)
-        amvpt.set_adaptive_exchange(adist.count_exchange(device="cuda"))
-    else:
+    G = group_size(p)
+    exchange = adist.run_exchange(device="cuda")   # per-call adaptive count exchange (amvpt_render_opts)
+    groups = None
+    if lane_sharded and world > 1 and args.partition != "lanes":
+        groups = adist.view_group_partition(p, G, world)
+        if groups is None and args.partition == "view-groups":
+            raise SystemExit("view-group partition does not apply to this configuration / world size")
+    if not lane_sharded:
         # pass sharding: this rank's passes are [rank*n_passes, (rank+1)*n_passes) of a world*spp frame
-        lane_begin, lane_end = 0, 2 ** 64 - 1
         p = adist.pass_shard(p, rank, world, plan)
     dev = amvpt.DeviceScene(sd)
     C = 5 if p.film_alpha else 4
-    film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    samples_per_rank = (min(lane_end, lanes_per_pass) - lane_begin) * n_passes
-    G = group_size(p)
+    quilt_bytes = p.film_width * p.film_height * C * 4
+    if groups is not None:
+        # view groups: this rank's tiles (lanes) and film window (tiles + filter border); rank 0 also
+        # holds the whole quilt the windows are gathered into
+        rect, win = groups[rank]
+        wx0, wy0, ww, wh = win
+        film = torch.zeros((wh, ww, C), dtype=torch.float32, device="cuda")
+        ov_cap = 1 << 20
+        overflow = torch.zeros(4 * (ov_cap + 1), dtype=torch.int32, device="cuda")
+        quilt = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda") if rank == 0 else None
+        lanes = amvpt.LaneSet(0, 0, *rect)
+        samples_per_rank = rect[2] * rect[3] * spp_pp * n_passes
+        partition = "view groups: %d groups of %d views per GPU, tiles %dx%d px + %d-px border window, gather to rank 0" % (
+            p.n_views // G // world, G, rect[2], rect[3], adist.FILTER_BORDER)
+        film_bytes = ww * wh * C * 4
 
-    def step(counters=None):
-        film.zero_()
-        c = dev.render(vd, p, film.data_ptr(), lane_begin, lane_end, stream, counters)
-        adist.reduce_film(film, dst=0)
-        return c
+        def step(counters=None):
+            film.zero_()
+            overflow[:4].zero_()
+            c = dev.render_ex(vd, p, film.data_ptr(), lanes=lanes, window=win, overflow_ptr=overflow.data_ptr(),
+                              overflow_capacity=ov_cap, stream=stream, counters=counters, exchange=exchange)
+            adist.gather_windows(film, win, overflow, quilt, [g[1] for g in groups], dst=0)
+            return c
+    else:
+        if lane_sharded:
+            # lane bands: this rank's lanes of every pass of ONE frame
+            lane_begin, lane_end = adist.lane_shard(lanes_per_pass, rank, world)
+        else:
+            lane_begin, lane_end = 0, 2 ** 64 - 1
+        film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
+        samples_per_rank = (min(lane_end, lanes_per_pass) - lane_begin) * n_passes
+        partition = "equal lane counts" if lane_sharded else "pass-sharded"
+        film_bytes = quilt_bytes
+        band = [lane_begin, lane_end]
 
-    partition = "equal lane counts"
-    if lane_sharded and world > 1 and args.warmup > 0:
-        # load balance (outside the timed region): time this rank's range once, all-gather the
-        # times and move the range boundaries to equal cost (amvpt.dist.balanced_shards)
-        torch.cuda.synchronize()
-        t_b = time.perf_counter()
-        film.zero_()
-        dev.render(vd, p, film.data_ptr(), lane_begin, lane_end, stream)
-        torch.cuda.synchronize()
-        t = torch.tensor([time.perf_counter() - t_b], dtype=torch.float64, device="cuda")
-        ts = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(ts, t)
-        bounds = [adist.lane_shard(lanes_per_pass, r, world)[0] for r in range(world)] + [lanes_per_pass]
-        bounds = adist.balanced_shards(bounds, [float(x.item()) for x in ts], align=max(64, 16 * spp_pp))
-        lane_begin, lane_end = bounds[rank], bounds[rank + 1]
-        samples_per_rank = (lane_end - lane_begin) * n_passes
-        partition = "cost-balanced contiguous lane ranges (one timed warmup render per rank)"
+        def step(counters=None):
+            film.zero_()
+            c = dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt.LaneSet(band[0], band[1], 0, 0, 0, 0),
+                              stream=stream, counters=counters, exchange=exchange if world > 1 else None)
+            adist.reduce_film(film, dst=0)
+            return c
+
+        if lane_sharded and world > 1 and args.warmup > 0:
+            # load balance (outside the timed region): time this rank's range on a warm arena (one
+            # untimed render first: the arena allocation and module load are one-time costs), from
+            # the per-kernel HIP-event times (the adaptive exchange would synchronise the ranks'
+            # wall clocks), all-gather the times and move the boundaries to equal cost
+            dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt.LaneSet(band[0], band[1], 0, 0, 0, 0), stream=stream,
+                          exchange=exchange)
+            cb = amvpt.Counters()
+            dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt.LaneSet(band[0], band[1], 0, 0, 0, 0), stream=stream,
+                          counters=cb, exchange=exchange)
+            own_ms = sum(cb.as_dict()["kernel_ms"].values())
+            t = torch.tensor([own_ms], dtype=torch.float64, device="cuda")
+            ts = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(ts, t)
+            shard_ms = [float(x.item()) for x in ts]
+            bounds = [adist.lane_shard(lanes_per_pass, r, world)[0] for r in range(world)] + [lanes_per_pass]
+            bounds = adist.balanced_shards(bounds, shard_ms, align=max(64, 16 * spp_pp))
+            band[0], band[1] = bounds[rank], bounds[rank + 1]
+            samples_per_rank = (band[1] - band[0]) * n_passes
+            partition = ("cost-balanced bands of quilt rows (per-kernel time of a warm render per rank; measured "
+                         "balance before %.3f)" % (sum(shard_ms) / world / max(shard_ms)))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -196,11 +240,17 @@ def main():
                    "k_prim_req": "k_prim_req<%d," % G, "k_suffix": "k_suffix_fused<",
                    "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1
                    else "k_prim_hit<"}.get(dom, dom + "<")
-    traffic, traffic_src = pmc_traffic(kernel_name, headline)
-    valu = pmc_valu(kms, kl, G, headline)
+    rev = source_revision()
+    traffic, traffic_src = pmc_traffic(kernel_name, prof_config, rev)
+    valu = pmc_valu(kms, kl, G, prof_config, rev)
+    hbm_frac = achieved / HBM_PEAK_GBS
+    valu_dom = (valu or {}).get("kernels", {}).get(dom)
+    # the measured limiter of the dominant kernel: VALU issue (committed SQ counts of this code revision
+    # over this run's launch time) vs algorithmic HBM bytes over the same time
+    bound = "valu" if valu_dom and valu_dom["frac"] > hbm_frac else "hbm"
     # SURVEY 8(d) whole-pipeline byte model
     P = p.film_width * p.film_height
-    B_sample = 336.0 * vbar + 120.0 * (G - 1) * hbar + 32.0 * P / samples_per_rank
+    B_sample = 336.0 * vbar + 120.0 * (G - 1) * hbar + 32.0 * P / (lanes_per_pass * n_passes)
     pipeline_gbs = value / world * 1e6 * B_sample / 1e9
 
     cpu = None
@@ -236,21 +286,25 @@ def main():
                                p.adaptive),
                 "samples_per_gpu_per_step": samples_per_rank,
                 "partition": partition if lane_sharded else "pass-sharded",
+                "film_bytes_per_gpu": film_bytes,
                 "adaptive_lanes_per_gpu_per_step": c["adaptive_lanes"],
-                "parallelism": ("lane-sharded x%d (+ one count all-gather per pass) + RCCL reduce of the RGBW "
-                                "ImageBlock" if lane_sharded else
+                "parallelism": (("view groups x%d (+ one per-row count all-gather per pass) + gather of the film "
+                                 "windows to rank 0" if groups is not None else
+                                 "lane bands x%d (+ one count all-gather per pass) + RCCL reduce of the RGBW "
+                                 "ImageBlock") if lane_sharded else
                                 "pass-sharded x%d + RCCL reduce of the RGBW ImageBlock") % world,
             },
             "roofline": {
-                "bound": "hbm",
+                "bound": bound,
                 "kernel": dom,
                 "kernel_symbol": kernel_name,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "frac": round(hbm_frac, 5),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "source_revision": rev,
                 "algorithmic_bytes_per_launch": int(per_launch_bytes),
                 "avg_launch_ms": round(kms[dom] / launches, 4),
                 "launches_per_step": launches,
@@ -262,9 +316,9 @@ def main():
                 # wave-instruction counts per launch / this run's launch time, vs 1228.8 G/s
                 "valu_issue": valu,
                 "note": ("the dominant kernel keeps its paths in registers (k_suffix_fused): its algorithmic "
-                         "HBM bytes are 96 B per path, so its HBM fraction is small by design; it is bound "
-                         "by VALU issue (valu_issue) -- pipeline_model is the metric's roofline")
-                        if dom == "k_suffix" else None,
+                         "HBM bytes are 96 B per pushed path, so its HBM fraction is small by design; bound = "
+                         "the larger of its VALU-issue and HBM fractions -- pipeline_model is the metric's "
+                         "roofline") if dom == "k_suffix" else None,
                 "pipeline_model": {"B_sample": round(B_sample, 1), "vbar": round(vbar, 4), "hbar": round(hbar, 4),
                                    "achieved_GBs": round(pipeline_gbs, 2),
                                    "frac": round(pipeline_gbs / HBM_PEAK_GBS, 5)},
@@ -272,7 +326,7 @@ def main():
             "cpu_baseline": cpu,
             "counters": {k: c[k] for k in ("lanes", "vertices", "reuse_lanes", "visibility_rays", "view_splats",
                                              "nonfinite_samples", "negative_samples", "record_bytes",
-                                             "splat_fallback")},
+                                             "splat_fallback", "pushed_paths", "film_overflow")},
         }
         print(json.dumps(out))
     if world > 1:
@@ -316,7 +370,7 @@ def kernel_bytes(c, G, C):
     stream element is written once by its producer and read once by its consumer."""
     lanes, verts, shadow = c["lanes"], c["vertices"], c["shadow_rays"]
     suffix = max(0, verts - lanes)        # suffix vertices (k_extend / k_bounce entries)
-    pushed = min(lanes, suffix)           # paths that left the primary vertex (= paths that terminate)
+    pushed = c["pushed_paths"]            # paths that entered the suffix (device counter; = paths that terminate)
     rec = c["record_bytes"] or 16         # lane records (4 x 16 B) + lane_out + view records (amvpt_counters)
     adapt = c["adaptive_lanes"]
     state = 80                            # path state: 5 float4 planes (store_state)
@@ -340,38 +394,59 @@ def kernel_bytes(c, G, C):
     }
 
 
-def pmc_traffic(kernel_name, full_size):
-    """HBM bytes per launch of `kernel_name` from the newest committed rocprofv3 PMC summary
-    (profiles/r*_traffic.json, made by tools/pmc_traffic.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this bench at config M).  None when no summary matches."""
+def source_revision():
+    """Revision stamp of the kernel sources (sha256 over csrc/, first 16 hex digits): committed PMC
+    summaries carry the stamp of the code they were measured on, and the bench uses only matching ones."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(PKG, "csrc")
+    for n in sorted(os.listdir(d)):
+        if n.endswith((".hip", ".h", ".cpp")):
+            h.update(n.encode())
+            h.update(open(os.path.join(d, n), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _profile(pattern, config, rev):
+    """Newest committed profile summary (profiles/<pattern>) measured on this config and source revision;
+    (data, path) or (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_traffic.json")))
-    if not files or not full_size:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        if d.get("config", "M") == config and d.get("source_revision") == rev:
+            return d, os.path.relpath(f, REPO)
+    return None, "no profiles/%s for config %s at source revision %s (stale profiles refused)" % (pattern, config, rev)
+
+
+def pmc_traffic(kernel_name, config, rev):
+    """HBM bytes per launch of `kernel_name` from a committed rocprofv3 PMC summary (profiles/r*_traffic.json,
+    tools/pmc_traffic.py: separate FETCH_SIZE and WRITE_SIZE passes of this bench) of this config and
+    source revision; (None, reason) otherwise."""
+    d, src = _profile("r*_traffic.json", config, rev)
+    if d is None:
+        return None, src
     key = kernel_name.replace(" ", "")
     for k, v in d["kernels"].items():
         if key in k.replace(" ", ""):
-            return int(v["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
-    return None, os.path.relpath(files[-1], REPO)
+            return int(v["hbm_bytes_per_launch"]), src
+    return None, src
 
 
-def pmc_valu(kms, kl, G, full_size):
-    """Per kernel: VALU wave-instructions per launch (newest profiles/r*_valu.json, made by
-    tools/pmc_valu.py from a SQ PMC pass of this bench at config M) over this run's mean launch
-    time, as a fraction of the chip's VALU issue peak.  None off config M."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_valu.json")))
-    if not files or not full_size:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
+def pmc_valu(kms, kl, G, config, rev):
+    """Per kernel: VALU wave-instructions per launch (committed profiles/r*_valu.json of this config and source
+    revision, tools/pmc_valu.py) over this run's mean launch time, as a fraction of the chip's VALU issue peak."""
+    d, src = _profile("r*_valu.json", config, rev)
+    if d is None:
+        return {"source": src, "kernels": {}}
     peak = d["peak_valu_ginst_s"]
     sym = {"k_splat": "k_splat_multi<%d," % G, "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
            "k_prim_req": "k_prim_req<%d," % G, "k_suffix": "k_suffix_fused<",
            "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1 else "k_prim_hit<"}
-    out = {"peak_Ginst_s": peak, "source": os.path.relpath(files[-1], REPO), "kernels": {}}
+    out = {"peak_Ginst_s": peak, "source": src, "kernels": {}}
     for k in kms:
         if not kl[k]:
             continue

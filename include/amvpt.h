@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 7
+#define AMVPT_ABI_VERSION 8
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -196,6 +196,9 @@ typedef struct amvpt_counters {
     uint64_t record_bytes;     /* bytes of per-lane records k_mv_primary writes and the splat reads (lane + views) */
     uint64_t nonfinite_samples; /* splatted view samples with a NaN/Inf value (ImageBlock::put's check, imageblock.cpp:180-204) */
     uint64_t negative_samples;  /* splatted view samples with a negative RGB component (same check) */
+    /* ABI 8 */
+    uint64_t pushed_paths;      /* paths that left the primary vertex into the shared suffix (byte model of the suffix) */
+    uint64_t film_overflow;     /* film floats added to the overflow list (cells outside an amvpt_film_window) */
 } amvpt_counters;
 
 /* kernels of the pipeline, for amvpt_counters.kernel_ms */
@@ -291,6 +294,95 @@ amvpt_status amvpt_set_bvh_build(uint32_t max_leaf_prims, float traversal_cost);
  */
 typedef int (*amvpt_exchange_fn)(void *ctx, uint64_t local_count, uint64_t *prefix, uint64_t *total);
 amvpt_status amvpt_set_adaptive_exchange(amvpt_exchange_fn fn, void *ctx);
+
+/* ------------------------------------------------------------------ */
+/* ABI 8: one rank's share of a frame, with per-call options           */
+/* ------------------------------------------------------------------ */
+
+/*
+ * The lanes of one render (a rank's share of the frame).  Lane = global
+ * wavefront index (mvpath.cpp:173-190: pixel = lane / spp_per_pass, pixel = y * W + x).
+ *   rect_width == 0: the contiguous lanes [lane_begin, lane_end) of every pass (a band of
+ *                    quilt rows: the strong-scaling lane shards of configs M / C3 / C4);
+ *   rect_width  > 0: the lanes of the quilt pixels [rect_x0, rect_x0 + rect_width) x
+ *                    [rect_y0, rect_y0 + rect_height) -- one RUN of rect_width * spp_per_pass
+ *                    consecutive lanes per pixel row.  A view group's tiles (mvpath_multi.h:31-38,
+ *                    grid.cpp:269-297) form such a rectangle: the view-group partition of C5
+ *                    ("4 views per GPU"), whose reprojected splats stay inside the group's tiles.
+ */
+typedef struct amvpt_lane_set {
+    uint64_t lane_begin, lane_end;
+    uint32_t rect_x0, rect_y0, rect_width, rect_height;
+} amvpt_lane_set;
+
+/*
+ * The film of one render: a device RGBW (RGBAW) fp32 buffer of height x width pixels holding
+ * the quilt rectangle [x0, x0 + width) x [y0, y0 + height) (row-major, channel-minor, the
+ * ImageBlock layout; 0, 0, W, H = the whole ImageBlock).  Splats are clipped to the quilt as
+ * ImageBlock::put does (imageblock.cpp:265-558); a footprint cell of the quilt outside the
+ * window is appended to `overflow` (device): a 16-byte header whose first u64 counts the cells,
+ * then entries of 4 u32 {quilt float index lo, hi, f32 value bits, 0}, at most overflow_capacity
+ * of them (the count keeps counting past it: the caller checks count <= capacity).  A window
+ * smaller than the quilt needs an overflow buffer.  Summing every window into its rectangle and
+ * every overflow entry into its float gives the whole-quilt ImageBlock (float summation order aside).
+ */
+typedef struct amvpt_film_window {
+    float *film;
+    uint32_t x0, y0, width, height;
+    uint32_t *overflow;
+    uint64_t overflow_capacity;
+} amvpt_film_window;
+
+/*
+ * Adaptive fill over a lane set that is not the whole pass (ABI 8).  The fill re-traces the
+ * pass's flagged lanes in compressed order and seeds from the WHOLE pass's compressed array
+ * (mvpath_multi.h:79-115), so every run of every rank's lane set needs the number of flagged
+ * lanes of the whole pass below its first lane.  Called once per pass with this render's runs
+ * (ascending lane_begin; a contiguous lane set is one run) and their flagged-lane counts; fills
+ * run_prefix[i] = flagged lanes of the pass with a lane index < run_lane_begin[i] (all ranks)
+ * and *total = flagged lanes of the pass.  Runs of different ranks must not interleave.  Every
+ * rank calls it once per pass (an empty lane set with n_runs = 0).  Returns 0 on success.
+ */
+typedef int (*amvpt_run_exchange_fn)(void *ctx, uint32_t n_runs, const uint64_t *run_lane_begin,
+                                     const uint64_t *run_count, uint64_t *run_prefix, uint64_t *total);
+
+/* Per-call options (ABI 8; NULL = defaults): replace the process-global knobs above, so
+ * concurrent renders (two scenes, or several ranks in one process) do not share state. */
+enum {
+    /* amvpt_render_opts.flags: kernel-path selection for tests and A/B runs (results are identical) */
+    AMVPT_OPT_GENERIC_KERNELS = 1u,   /* no all-diffuse kernel instances (kDiff) */
+    AMVPT_OPT_WAVEFRONT_SUFFIX = 2u,  /* per-depth k_extend / k_bounce instead of k_suffix_fused */
+    AMVPT_OPT_SPLIT_NEE = 4u          /* suffix NEE rays in k_shadow instead of inside k_bounce */
+};
+typedef struct amvpt_render_opts {
+    uint64_t chunk_lanes;             /* 0: automatic (see amvpt_set_chunk_lanes) */
+    uint32_t traversal;               /* 0 auto, 1 wave-uniform, 2 per-lane (see amvpt_set_traversal) */
+    uint32_t flags;                   /* AMVPT_OPT_* */
+    amvpt_run_exchange_fn exchange;   /* adaptive fill over a partial lane set */
+    void *exchange_ctx;
+    float *records;                   /* test hook (parity), NULL: off -- as amvpt_render_records: [v * G + slot][8] */
+    uint32_t record_pass;             /*   of pass record_pass, v = the lane's index in the lane set (lane order) */
+    uint32_t reserved;
+} amvpt_render_opts;
+
+/*
+ * amvpt_render over a lane set into a film window, with per-call options.  amvpt_render(...,
+ * lane_begin, lane_end, film, ...) is amvpt_render_ex with the contiguous lane set, the
+ * whole-quilt window and the process-global knobs.
+ */
+amvpt_status amvpt_render_ex(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                             const amvpt_lane_set *lanes, const amvpt_film_window *film, void *stream,
+                             const amvpt_render_opts *opts, amvpt_counters *counters);
+
+/*
+ * The gather side of a windowed render (ABI 8): add a film window -- height x width x channels fp32
+ * holding quilt pixels [x0, x0 + width) x [y0, y0 + height) -- and n_entries overflow entries (the
+ * 16-byte entries that follow an overflow list's header) into a whole-quilt film of quilt_height x
+ * quilt_width x channels.  Device pointers; the adds are ordered on `stream`.
+ */
+amvpt_status amvpt_film_accumulate(float *quilt, uint32_t quilt_width, uint32_t quilt_height, uint32_t channels,
+                                   const float *window, uint32_t x0, uint32_t y0, uint32_t width, uint32_t height,
+                                   const uint32_t *overflow_entries, uint64_t n_entries, void *stream);
 
 #ifdef __cplusplus
 }

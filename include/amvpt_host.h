@@ -50,13 +50,16 @@ int amvpt_host_render(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t s
                       int raw, float *out_host, amvpt_counters *counters);
 
 /*
- * Integrator::render over n_devices GPUs of one node, one host thread per device:
- * device devices[r] renders the lane range amvpt_host_lane_shard(L, r, n_devices) of every pass
- * (L = lanes per pass, amvpt_plan) into its own RGBW ImageBlock; the blocks are summed onto
- * devices[0] with one RCCL reduce (ncclReduce, sum, fp32, communicators from ncclCommInitAll) and
- * developed there.  The adaptive fill's per-pass count exchange runs between the threads.  The
- * image equals amvpt_host_render's up to float summation order.  Counters: lane statistics summed,
- * times of the slowest device.
+ * Integrator::render over n_devices GPUs of one node, one host thread per device.
+ * View groups, when they divide among the devices (C5): devices[r] renders the lanes of its groups'
+ * quilt tiles into a film window (tiles + filter border), the windows and overflow cells go to
+ * devices[0] (ncclSend / ncclRecv) and are summed into the ImageBlock there (amvpt_film_accumulate).
+ * Otherwise lane bands: devices[r] renders amvpt_host_lane_shard(L, r, n_devices) of every pass into
+ * its own RGBW ImageBlock and the blocks are summed onto devices[0] with one ncclReduce.  Developed on
+ * devices[0].  The adaptive fill's per-run count exchange runs between the threads (per-call option).
+ * Communicators, per-device scenes and films are cached on the scene for the next frame.  The image
+ * equals amvpt_host_render's up to float summation order.  Counters: lane statistics summed, times of
+ * the slowest device.
  */
 int amvpt_host_render_multi(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t seed, uint32_t spp,
                             int raw, const int *devices, int n_devices, float *out_host,
@@ -64,6 +67,16 @@ int amvpt_host_render_multi(amvpt_host_scene *scene, uint32_t sensor_index, uint
 
 /* [begin, end) of rank's contiguous lane range (sizes differ by at most one; amvpt.dist.lane_shard) */
 void amvpt_host_lane_shard(uint64_t lanes, uint32_t rank, uint32_t world, uint64_t *begin, uint64_t *end);
+
+/* The view-group partition of amvpt_host_render_multi (amvpt.dist.view_group_partition): rank's lane
+ * rectangle and film window {x0, y0, width, height}; returns 1, or 0 when the view groups do not
+ * divide among `world` devices as rectangles of quilt tiles (lane bands are used then). */
+int amvpt_host_view_group_partition(const amvpt_params *params, uint32_t rank, uint32_t world, uint32_t *rect,
+                                    uint32_t *window);
+
+/* render_multi's per-scene cache (communicators, per-device scene copies, streams, films): how many
+ * scene creations, communicator initialisations and completed multi-GPU renders it has seen. */
+int amvpt_host_multi_stats(amvpt_host_scene *scene, uint64_t *scene_creates, uint64_t *comm_inits, uint64_t *renders);
 
 /*
  * The exact descriptors render() hands to the C-ABI (for the parity tests: the oracle

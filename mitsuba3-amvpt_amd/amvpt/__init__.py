@@ -75,13 +75,59 @@ class Counters(ctypes.Structure):
                 ("kernel_ms_primary", f64), ("kernel_ms_bounce", f64), ("kernel_ms_splat", f64),
                 ("total_ms", f64), ("splat_fallback", u64),
                 ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12),
-                ("record_bytes", u64), ("nonfinite_samples", u64), ("negative_samples", u64)]
+                ("record_bytes", u64), ("nonfinite_samples", u64), ("negative_samples", u64),
+                ("pushed_paths", u64), ("film_overflow", u64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         for k in ("kernel_ms", "kernel_launches"):
             d[k] = {name: d[k][i] for i, name in enumerate(KERNELS)}
         return d
+
+
+class LaneSet(ctypes.Structure):
+    """amvpt_lane_set: contiguous lanes [lane_begin, lane_end), or (rect_width > 0) the lanes of a
+    pixel rectangle of the quilt (one run of rect_width * spp_per_pass lanes per pixel row)."""
+    _fields_ = [("lane_begin", u64), ("lane_end", u64), ("rect_x0", u32), ("rect_y0", u32),
+                ("rect_width", u32), ("rect_height", u32)]
+
+
+class FilmWindow(ctypes.Structure):
+    """amvpt_film_window: device film holding quilt pixels [x0, x0+width) x [y0, y0+height), plus the
+    overflow list (device; 16-B header with the u64 cell count, then 16-B entries) for cells outside."""
+    _fields_ = [("film", ctypes.c_void_p), ("x0", u32), ("y0", u32), ("width", u32), ("height", u32),
+                ("overflow", ctypes.c_void_p), ("overflow_capacity", u64)]
+
+
+# amvpt_run_exchange_fn: (ctx, n_runs, *run_lane_begin, *run_count, *run_prefix, *total) -> 0 on success
+RunExchangeFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, u32, ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                 ctypes.POINTER(u64), ctypes.POINTER(u64))
+
+
+class RenderOpts(ctypes.Structure):
+    """amvpt_render_opts: per-call chunk size, traversal, path-selection flags, run exchange, records."""
+    _fields_ = [("chunk_lanes", u64), ("traversal", u32), ("flags", u32), ("exchange", RunExchangeFn),
+                ("exchange_ctx", ctypes.c_void_p), ("records", ctypes.c_void_p), ("record_pass", u32),
+                ("reserved", u32)]
+
+
+# amvpt_render_opts.flags (results are identical; kernel-path selection for tests / A/B)
+OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE = 1, 2, 4
+
+
+def wrap_run_exchange(fn):
+    """ctypes callback around `fn(run_lane_begin: list, run_count: list) -> (run_prefix: list, total)`
+    (exceptions -> status 1)."""
+    def cb(_ctx, n, begins, counts, prefix, total):
+        try:
+            pre, tot = fn([int(begins[i]) for i in range(n)], [int(counts[i]) for i in range(n)])
+            for i in range(n):
+                prefix[i] = int(pre[i])
+            total[0] = int(tot)
+            return 0
+        except Exception:   # noqa: BLE001 -- reported to the C side as a failed exchange
+            return 1
+    return RunExchangeFn(cb)
 
 
 # amvpt_kernel_id (include/amvpt.h): index -> name of Counters.kernel_ms / kernel_launches
@@ -109,11 +155,15 @@ def hip_lib():
         for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
                    "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
                    "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal",
-                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build"):
+                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build", "amvpt_render_ex"):
             if hasattr(L, fn):   # older variant builds (AMVPT_LIB_DIR A/B runs) may lack the newest knobs
                 getattr(L, fn).restype = ctypes.c_int
         L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Counters)]
+        if hasattr(L, "amvpt_render_ex"):
+            L.amvpt_render_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params),
+                                          ctypes.POINTER(LaneSet), ctypes.POINTER(FilmWindow), ctypes.c_void_p,
+                                          ctypes.POINTER(RenderOpts), ctypes.POINTER(Counters)]
         L.amvpt_render_records.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u32, u64,
                                            u64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.amvpt_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.POINTER(ctypes.c_void_p)]
@@ -156,6 +206,9 @@ def host_lib():
                                               ctypes.POINTER(Counters)]
         L.amvpt_host_lane_shard.argtypes = [u64, u32, u32, ctypes.POINTER(u64), ctypes.POINTER(u64)]
         L.amvpt_host_lane_shard.restype = None
+        L.amvpt_host_view_group_partition.argtypes = [ctypes.POINTER(Params), u32, u32, ctypes.POINTER(u32),
+                                                      ctypes.POINTER(u32)]
+        L.amvpt_host_multi_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(u64)] * 3
         L.amvpt_host_describe.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.POINTER(ctypes.POINTER(SceneDesc)),
                                           ctypes.POINTER(ctypes.POINTER(ViewDesc)), ctypes.POINTER(Params)]
         L.amvpt_host_integrator_string.argtypes = [ctypes.c_void_p]
@@ -265,6 +318,20 @@ def host_lane_shard(n_lanes, rank, world):
     b, e = u64(), u64()
     host_lib().amvpt_host_lane_shard(n_lanes, rank, world, ctypes.byref(b), ctypes.byref(e))
     return b.value, e.value
+
+
+def host_view_group_partition(params, rank, world):
+    """The C++ host's view-group partition (amvpt_host_view_group_partition): (rect, window) or None."""
+    r, w = (u32 * 4)(), (u32 * 4)()
+    ok = host_lib().amvpt_host_view_group_partition(ctypes.byref(params), rank, world, r, w)
+    return (tuple(r), tuple(w)) if ok else None
+
+
+def multi_stats(scene):
+    """render_multi's cache counters on this scene: scene creations, communicator inits, renders."""
+    a, b, c = u64(), u64(), u64()
+    _check(scene._lib.amvpt_host_multi_stats(scene._h, a, b, c), scene._lib)
+    return {"scene_creates": a.value, "comm_inits": b.value, "renders": c.value}
 
 
 def plan(params):
@@ -380,6 +447,24 @@ class DeviceScene:
                                       ctypes.c_void_p(film_ptr), ctypes.c_void_p(stream),
                                       ctypes.byref(counters) if counters is not None else None),
                self._lib)
+        return counters
+
+    def render_ex(self, views_ptr, params, film_ptr, lanes=None, window=None, overflow_ptr=None,
+                  overflow_capacity=0, stream=None, counters=None, chunk_lanes=0, traversal=0, flags=0,
+                  exchange=None, records_ptr=None, record_pass=0):
+        """amvpt_render_ex: `lanes` a LaneSet (None: the whole pass), `window` (x0, y0, width, height)
+        of the quilt the film holds (None: the whole quilt), per-call options; `exchange` is
+        `fn(run_lane_begin, run_count) -> (run_prefix, total)` (see amvpt.dist.run_exchange)."""
+        if lanes is None:
+            lanes = LaneSet(0, 2 ** 64 - 1, 0, 0, 0, 0)
+        x0, y0, w, h = window if window is not None else (0, 0, params.film_width, params.film_height)
+        fw = FilmWindow(ctypes.c_void_p(film_ptr), x0, y0, w, h, ctypes.c_void_p(overflow_ptr or 0),
+                        overflow_capacity)
+        cb = wrap_run_exchange(exchange) if exchange is not None else RunExchangeFn()
+        o = RenderOpts(chunk_lanes, traversal, flags, cb, None, ctypes.c_void_p(records_ptr or 0), record_pass, 0)
+        _check(self._lib.amvpt_render_ex(self.h, views_ptr, ctypes.byref(params), ctypes.byref(lanes),
+                                         ctypes.byref(fw), ctypes.c_void_p(stream), ctypes.byref(o),
+                                         ctypes.byref(counters) if counters is not None else None), self._lib)
         return counters
 
     def render_records(self, views_ptr, params, film_ptr, records_ptr, pass_index=0, lane_begin=0,

@@ -6,7 +6,13 @@ independent and seeds its own sampler from its global lane index
 data-path collective.  The only collective is the final sum of the RGBW
 ImageBlocks (an RCCL reduce of the film, ImageBlock::put is additive).
 
-Two partitions are provided:
+Three partitions are provided:
+  * view_groups -- C5's "4 views per GPU" (SURVEY 8(e)): rank r owns whole view groups
+    (mvpath_multi.h:31-38: a lane's reprojections stay inside its primary view's group), i.e. a
+    rectangle of quilt tiles; it renders the lanes of those pixels (amvpt_lane_set rect form) into a
+    film window of its tiles plus a 4-pixel filter border, and the frame is assembled on rank 0 by a
+    gather of the windows (borders summed) plus the few cells that fall outside (the overflow list).
+    The adaptive fill exchanges one count per pixel row of the rectangle (run_exchange).
   * pass_shard  -- weak scaling (bench.py): rank r renders the passes
     [r * P, (r + 1) * P) of a (world * spp)-spp frame by offsetting the seed by
     spp_per_pass * P * r -- exactly the seeds those passes get in a single
@@ -94,3 +100,171 @@ def reduce_film(film, dst=0):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.reduce(film, dst=dst)
     return film
+
+
+# ---------------------------------------------------------------------------------------------------
+# View-group partition (C5)
+# ---------------------------------------------------------------------------------------------------
+
+FILTER_BORDER = 4   # pixels around a rank's tiles its splats can reach (Gaussian radius 2 + jitter)
+
+
+def view_tile(params, v):
+    """Quilt tile (tx, ty) of view v: the inverse of GridSensor::sample_ray_idx's index
+    (grid.cpp:269-297; batch.cpp:163-181 is the grid_y = 1 case) -- the splat's tile offset."""
+    gx = max(1, params.grid_x)
+    gy = max(1, params.grid_y)
+    ix, iy = v % gx, v // gx
+    if params.reverse_x:
+        ix = gx - 1 - ix
+    if params.reverse_y:
+        iy = gy - 1 - iy
+    return ix, iy
+
+
+def tiles_rect(params, views):
+    """Pixel rectangle (x0, y0, w, h) of the quilt tiles of `views`, or None when they do not form one."""
+    gx, gy = max(1, params.grid_x), max(1, params.grid_y)
+    sx, sy = params.film_width // gx, params.film_height // gy
+    tiles = {view_tile(params, v) for v in views}
+    xs = sorted({t[0] for t in tiles})
+    ys = sorted({t[1] for t in tiles})
+    if len(tiles) != len(xs) * len(ys) or xs != list(range(xs[0], xs[-1] + 1)) or ys != list(range(ys[0], ys[-1] + 1)):
+        return None
+    return xs[0] * sx, ys[0] * sy, len(xs) * sx, len(ys) * sy
+
+
+def view_group_partition(params, group, world):
+    """Per rank: (lane rectangle, film window) of the view-group partition, or None when it does not
+    apply (fewer groups than ranks, groups not divisible among ranks, a grid without separate tiles,
+    or tiles that do not form rectangles).  Rank r owns groups [r * n / world, (r + 1) * n / world)."""
+    if not params.multisensor or group < 1 or params.n_views % group:
+        return None
+    n_groups = params.n_views // group
+    if world < 1 or n_groups < world or n_groups % world:
+        return None
+    per = n_groups // world
+    out = []
+    for r in range(world):
+        rect = tiles_rect(params, range(r * per * group, (r + 1) * per * group))
+        if rect is None:
+            return None
+        x0, y0, w, h = rect
+        wx0, wy0 = max(0, x0 - FILTER_BORDER), max(0, y0 - FILTER_BORDER)
+        wx1 = min(params.film_width, x0 + w + FILTER_BORDER)
+        wy1 = min(params.film_height, y0 + h + FILTER_BORDER)
+        out.append((rect, (wx0, wy0, wx1 - wx0, wy1 - wy0)))
+    return out
+
+
+def exclusive_prefix(all_begins, all_counts, begins):
+    """Flagged lanes below each run in `begins`, given every rank's runs (all_begins, all_counts)."""
+    import numpy as np
+    b = np.asarray(all_begins, dtype=np.int64)
+    c = np.asarray(all_counts, dtype=np.int64)
+    order = np.argsort(b, kind="stable")
+    b, c = b[order], c[order]
+    csum = np.concatenate([[0], np.cumsum(c)])
+    idx = np.searchsorted(b, np.asarray(begins, dtype=np.int64), side="left")
+    return [int(csum[i]) for i in idx], int(csum[-1])
+
+
+def run_exchange(device=None):
+    """`fn(run_lane_begin, run_count) -> (run_prefix, total)` over torch.distributed: the adaptive fill's
+    count exchange for any lane set (amvpt_run_exchange_fn, include/amvpt.h).  One all-gather of the
+    run counts and one of the padded (lane begin, count) pairs per pass; runs of different ranks are
+    disjoint, so each run's prefix is the count of every run (any rank) that starts below it."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(begins, counts):
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return exclusive_prefix(begins, counts, begins)
+        world = dist.get_world_size()
+        n = torch.tensor([len(begins)], dtype=torch.int64, device=device)
+        ns = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(ns, n)
+        m = max(1, max(int(x.item()) for x in ns))
+        buf = torch.zeros((m, 2), dtype=torch.int64)
+        buf[:, 0] = 2 ** 62
+        if begins:
+            buf[:len(begins), 0] = torch.tensor(begins, dtype=torch.int64)
+            buf[:len(begins), 1] = torch.tensor(counts, dtype=torch.int64)
+        buf = buf.to(device) if device else buf
+        outs = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(outs, buf)
+        allr = torch.cat(outs).cpu().numpy()
+        return exclusive_prefix(allr[:, 0], allr[:, 1], begins)
+    return fn
+
+
+def overflow_entries(overflow):
+    """(quilt float indices int64, values float32) of an overflow list (int32 tensor: 4 header words,
+    then 4 words per entry), as torch tensors on the list's device."""
+    import torch
+    cnt = int(overflow[:2].view(torch.int64)[0].item())
+    cap = overflow.numel() // 4 - 1
+    if cnt > cap:
+        raise RuntimeError("film overflow list full: %d > %d" % (cnt, cap))
+    e = overflow[4:4 + 4 * cnt].view(cnt, 4)
+    idx = (e[:, 0].to(torch.int64) & 0xffffffff) | (e[:, 1].to(torch.int64) << 32)
+    return idx, e[:, 2].contiguous().view(torch.float32)
+
+
+def gather_windows(window_film, window, overflow, quilt, windows, dst=0):
+    """Assemble the whole-quilt ImageBlock on `dst` from every rank's film window (their borders
+    overlap: summed) and overflow list (summed into their floats).  `windows` lists every rank's
+    (x0, y0, w, h); `quilt` (H, W, C) is written on dst only (zeroed first).  Point-to-point
+    sends to dst (RCCL over xGMI on GPUs, gloo on CPU); a single process just adds its own."""
+    import torch
+    import torch.distributed as dist
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    rank = dist.get_rank() if multi else 0
+    world = dist.get_world_size() if multi else 1
+    idx, val = overflow_entries(overflow)
+    if multi:
+        n = torch.tensor([idx.numel()], dtype=torch.int64, device=window_film.device)
+        ns = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(ns, n)
+        counts = [int(x.item()) for x in ns]
+    else:
+        counts = [idx.numel()]
+    if rank != dst:
+        ops = [dist.P2POp(dist.isend, window_film.contiguous(), dst)]
+        if counts[rank]:
+            ops.append(dist.P2POp(dist.isend, idx.contiguous(), dst))
+            ops.append(dist.P2POp(dist.isend, val.contiguous(), dst))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        return None
+    C = quilt.shape[2]
+    quilt.zero_()
+    recv = {}
+    ops = []
+    for r in range(world):
+        if r == rank:
+            continue
+        x0, y0, w, h = windows[r]
+        t = torch.empty((h, w, C), dtype=quilt.dtype, device=quilt.device)
+        recv[r] = [t]
+        ops.append(dist.P2POp(dist.irecv, t, r))
+        if counts[r]:
+            ti = torch.empty(counts[r], dtype=torch.int64, device=quilt.device)
+            tv = torch.empty(counts[r], dtype=torch.float32, device=quilt.device)
+            recv[r] += [ti, tv]
+            ops += [dist.P2POp(dist.irecv, ti, r), dist.P2POp(dist.irecv, tv, r)]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    flat = quilt.view(-1)
+    for r in range(world):
+        x0, y0, w, h = windows[r]
+        if r == rank:
+            quilt[y0:y0 + h, x0:x0 + w] += window_film
+            if idx.numel():
+                flat.index_add_(0, idx.to(quilt.device), val.to(quilt.device))
+        else:
+            quilt[y0:y0 + h, x0:x0 + w] += recv[r][0]
+            if counts[r]:
+                flat.index_add_(0, recv[r][1], recv[r][2])
+    return quilt

@@ -681,18 +681,74 @@ amvpt_status amvpt_scene_stats(const amvpt_scene *scene, uint32_t *n_nodes, uint
     return AMVPT_OK;
 }
 
+} // extern "C"
+
+namespace {
+/* amvpt_set_adaptive_exchange's one-count exchange as a run exchange: a contiguous lane set is
+ * one run (or none, for an empty range) */
+struct LegacyExchange { amvpt_exchange_fn fn; void *ctx; };
+int legacy_run_exchange(void *ctx, uint32_t n_runs, const uint64_t *, const uint64_t *run_count, uint64_t *run_prefix,
+                        uint64_t *total) {
+    const LegacyExchange *x = static_cast<const LegacyExchange *>(ctx);
+    if (n_runs > 1) return 1;
+    uint64_t prefix = 0;
+    const int rc = x->fn(x->ctx, n_runs ? run_count[0] : 0, &prefix, total);
+    if (n_runs) run_prefix[0] = prefix;
+    return rc;
+}
+/* amvpt_render / amvpt_render_records: contiguous lanes, whole-quilt film, process-global knobs */
+amvpt_status render_legacy(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                           uint64_t lane_begin, uint64_t lane_end, float *film, void *stream, amvpt_counters *counters,
+                           float *records, uint32_t pass) {
+    if (!params) { set_error("amvpt_render: null argument"); return AMVPT_ERR_INVALID; }
+    amvpt_lane_set lanes{};
+    lanes.lane_begin = lane_begin;
+    lanes.lane_end = lane_end;
+    amvpt_film_window w{};
+    w.film = film;
+    w.width = params->film_width;
+    w.height = params->film_height;
+    LegacyExchange lx{g_exchange, g_exchange_ctx};
+    amvpt_render_opts o{};
+    o.chunk_lanes = g_chunk_lanes;
+    o.traversal = g_traversal;
+    if (g_exchange) { o.exchange = legacy_run_exchange; o.exchange_ctx = &lx; }
+    return render_impl(scene, views, params, lanes, w, stream, o, counters, records, pass);
+}
+} // namespace
+
+extern "C" {
+
 amvpt_status amvpt_render(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
                           uint64_t lane_begin, uint64_t lane_end, float *film_device, void *stream,
                           amvpt_counters *counters) {
     if (!device_ok()) { set_error("amvpt_render: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
-    return render_impl(scene, views, params, lane_begin, lane_end, film_device, stream, counters, nullptr, 0);
+    return render_legacy(scene, views, params, lane_begin, lane_end, film_device, stream, counters, nullptr, 0);
 }
 
 amvpt_status amvpt_render_records(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
                                   uint32_t pass, uint64_t lane_begin, uint64_t lane_end, float *film_device,
                                   float *records_device, void *stream) {
     if (!device_ok()) { set_error("amvpt_render_records: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
-    return render_impl(scene, views, params, lane_begin, lane_end, film_device, stream, nullptr, records_device, pass);
+    return render_legacy(scene, views, params, lane_begin, lane_end, film_device, stream, nullptr, records_device, pass);
+}
+
+amvpt_status amvpt_render_ex(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
+                             const amvpt_lane_set *lanes, const amvpt_film_window *film, void *stream,
+                             const amvpt_render_opts *opts, amvpt_counters *counters) {
+    if (!lanes || !film) { set_error("amvpt_render_ex: null lane set or film window"); return AMVPT_ERR_INVALID; }
+    if (!device_ok()) { set_error("amvpt_render_ex: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    const amvpt_render_opts defaults{};
+    const amvpt_render_opts &o = opts ? *opts : defaults;
+    return render_impl(scene, views, params, *lanes, *film, stream, o, counters, o.records, o.record_pass);
+}
+
+amvpt_status amvpt_film_accumulate(float *quilt, uint32_t quilt_width, uint32_t quilt_height, uint32_t channels,
+                                   const float *window, uint32_t x0, uint32_t y0, uint32_t width, uint32_t height,
+                                   const uint32_t *overflow_entries, uint64_t n_entries, void *stream) {
+    if (!device_ok()) { set_error("amvpt_film_accumulate: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    return accumulate_impl(quilt, quilt_width, quilt_height, channels, window, x0, y0, width, height, overflow_entries,
+                           n_entries, stream);
 }
 
 amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t width, uint32_t height,

@@ -52,7 +52,6 @@ namespace amvpt {
  * (config M: 2^22 386, 2^23 373, 2^24 364, 2^25 363 ms per frame; r02fd) */
 uint64_t g_chunk_lanes = 0;
 uint32_t g_traversal = 0;
-bool g_diffuse_spec = true;   /* all-diffuse kernel specialisation (AMVPT_NO_DIFFUSE_SPEC=1 turns it off) */
 amvpt_exchange_fn g_exchange = nullptr;
 void *g_exchange_ctx = nullptr;
 #endif
@@ -90,8 +89,15 @@ struct KParams {
     uint32_t win_rs;        /* splat window row stride residue mod 32 (0: stride = width) */
     uint32_t adapt_seed;    /* adaptive pass: seed of the forked sampler (base_seed + wavefront) */
     uint32_t pass_seed;     /* adaptive pass: seed_value of the pass whose lanes are refilled */
-    uint32_t adapt_base;    /* adaptive pass: index of this range's first entry in the pass's wavefront */
-    uint64_t range_begin;   /* lane_begin of the render (amask is indexed from it) */
+    uint64_t range_begin;   /* contiguous lane set: its first lane (lane_of) */
+    /* lane set (amvpt_lane_set): chunk offsets are VIRTUAL indices v in [0, span) of the render's
+     * lanes; lane_of(v) maps them to global lanes (contiguous, or rect_h runs of run_len lanes) */
+    uint32_t rect, rect_x0, rect_y0, run_len;
+    /* film window (amvpt_film_window): the film holds quilt pixels [fx0, fx0 + fw) x [fy0, fy0 + fh);
+     * cells outside go to the overflow list (header u64 count, then 16-B entries, ov_cap of them) */
+    uint32_t fx0, fy0, fw, fh;
+    uint32_t *overflow;
+    uint64_t ov_cap;
     float inv_w, inv_h;
     float adapt_w;
     FilterCoeffs filt;
@@ -120,8 +126,11 @@ struct Bufs {
     float *film;
     float *records;       /* optional [n][G][8] */
     unsigned long long *stats; /* [0] vertices [1] reuse lanes [2] visibility rays [3] splats */
-    uint8_t *amask;       /* adaptive: per-lane adapt_mask of the pass (lane order), or null */
-    const uint32_t *asel; /* adaptive: compacted lanes with adapt_mask (ascending) */
+    uint8_t *amask;       /* adaptive: per-lane adapt_mask of the pass (virtual index order), or null */
+    const uint32_t *asel; /* adaptive: virtual indices of the lanes with adapt_mask (ascending) */
+    const uint32_t *run_delta; /* adaptive: per run, (flagged lanes of the pass below the run) - (this
+                                * render's flagged lanes below it): entry e of asel is entry
+                                * e + run_delta[run] of the pass's compressed array */
     float4 *hit;          /* k_extend / k_prim_hit -> shading: closest hit (t, u, v, prim) per entry */
     float4 *nee[3];       /* k_bounce -> k_shadow: deferred emitter-sample shadow rays (NEE records), */
     float *nee_cb;        /* + the contribution's blue channel as a float plane (52 B per record) */
@@ -602,54 +611,31 @@ AD f3 camera_point(const DView &v, float apx, float apy) {
 
 AD void film_add(float *p, float v) { atomicAdd(p, v); }
 
-/* ImageBlock::put (imageblock.cpp:174-559), both accumulation methods. */
-AD void film_put(const KParams &P, float *film, float px, float py, const float *vals, bool coalesce) {
-    const uint32_t W = P.W, H = P.H, C = P.C;
-    if (P.box) {
-        int ix = (int) floorf(px), iy = (int) floorf(py);
-        uint32_t ux = (uint32_t) ix, uy = (uint32_t) iy;
-        if (!(ux < W && uy < H)) return;
-        float *ptr = film + ((size_t) uy * W + ux) * C;
-        for (uint32_t k = 0; k < C; ++k) film_add(ptr + k, vals[k]);
-        return;
-    }
-    const float radius = P.filt.radius;
-    if (!coalesce) {
-        float pfx = px + (0.f - 0.5f), pfy = py + (0.f - 0.5f);
-        int p0x = max((int) ceilf(pfx - radius), 0), p0y = max((int) ceilf(pfy - radius), 0);
-        int p1x = min((int) floorf(pfx + radius), (int) W - 1), p1y = min((int) floorf(pfy + radius), (int) H - 1);
-        uint32_t u0x = (uint32_t) p0x, u0y = (uint32_t) p0y, u1x = (uint32_t) p1x, u1y = (uint32_t) p1y;
-        const uint32_t count = (uint32_t) ceilf(2.f * radius);
-        if (!(u0x <= u1x && u0y <= u1y)) return;
-        float rx = (float) u0x - pfx, ry = (float) u0y - pfy;
-        for (uint32_t ys = 0; ys < count; ++ys) {
-            float wy = gaussian_eval(P.filt, ry + (float) ys);
-            if (!(u0y + ys <= u1y)) continue;
-            for (uint32_t xs = 0; xs < count; ++xs) {
-                float wx = gaussian_eval(P.filt, rx + (float) xs);
-                float w = wx * wy;
-                if (!(u0x + xs <= u1x)) continue;
-                float *ptr = film + ((size_t) (u0y + ys) * W + (u0x + xs)) * C;
-                for (uint32_t k = 0; k < C; ++k) film_add(ptr + k, vals[k] * w);
-            }
-        }
-        return;
-    }
-    const uint32_t n = (uint32_t) ceilf(radius - .5f), count = 2 * n + 1;
-    int pix = (int) floorf(px) - (int) n, piy = (int) floorf(py) - (int) n;
-    uint32_t x = (uint32_t) pix, y = (uint32_t) piy;
-    float rx = ((float) pix + .5f) - px, ry = ((float) piy + .5f) - py;
-    for (uint32_t ys = 0; ys < count; ++ys) {
-        float wy = gaussian_eval(P.filt, ry + (float) ys);
-        if (!(y + ys < H)) continue;
-        for (uint32_t xs = 0; xs < count; ++xs) {
-            float wx = gaussian_eval(P.filt, rx + (float) xs);
-            float w = wx * wy;
-            if (!(x + xs < W)) continue;
-            float *ptr = film + ((size_t) (y + ys) * W + (x + xs)) * C;
-            for (uint32_t k = 0; k < C; ++k) film_add(ptr + k, vals[k] * w);
-        }
-    }
+/*
+ * Film window (amvpt_film_window).  The film buffer holds the quilt rectangle [fx0, fx0 + fw) x
+ * [fy0, fy0 + fh); footprints are clipped to the QUILT as ImageBlock::put clips them
+ * (imageblock.cpp:265-558), and a cell of the quilt outside the window is appended to the overflow
+ * list (a view-group rank's rare lanes whose jittered position rounds into the next tile).  With the
+ * whole-quilt window (the single-GPU frame) every cell is inside.
+ */
+AD bool in_window(const KParams &P, int x, int y) {
+    return (uint32_t) (x - (int) P.fx0) < P.fw && (uint32_t) (y - (int) P.fy0) < P.fh;
+}
+/* film float of quilt cell (x, y), channel k -- the cell must be inside the window */
+AD float *film_cell(const KParams &P, float *film, int x, int y, int k) {
+    return film + ((size_t) (uint32_t) (y - (int) P.fy0) * P.fw + (uint32_t) (x - (int) P.fx0)) * P.C + k;
+}
+/* append quilt float `idx` += v to the overflow list (one returning atomic: rare by construction) */
+AD void overflow_push(const KParams &P, uint64_t idx, float v) {
+    if (!P.overflow) return;   /* the host requires the list for any window smaller than the quilt */
+    const unsigned long long e = atomicAdd(reinterpret_cast<unsigned long long *>(P.overflow), 1ull);
+    if (e < P.ov_cap)
+        reinterpret_cast<uint4 *>(P.overflow + 4)[e] = make_uint4((uint32_t) idx, (uint32_t) (idx >> 32), __float_as_uint(v), 0u);
+}
+/* one film float of quilt cell (x, y), channel k: the window, else the overflow list */
+AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float v) {
+    if (in_window(P, x, y)) film_add(film_cell(P, film, x, y, k), v);
+    else overflow_push(P, ((uint64_t) (uint32_t) y * P.W + (uint32_t) x) * P.C + (uint32_t) k, v);
 }
 
 /* ------------------------------------------------------------------ */
@@ -903,7 +889,10 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
     const int plane = w.plane;
     const int rowlen = w.ww * C;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
-    float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
+    /* the LDS window's quilt cells inside the film window (uniform): straight film offsets */
+    const bool inside = in_window(P, w.bx0, w.by0) && in_window(P, w.bx0 + max(w.ww, 1) - 1, w.by0 + max(w.wh, 1) - 1);
+    float *film0 = inside ? film_cell(P, film, w.bx0, w.by0, 0) : film;
+    const size_t film_row = (size_t) P.fw * C;
     WinT *win = L.win;
     const int n_elems = w.ww * w.wh * C;                    /* touched film floats (rows of ww cells) */
     for (int e = threadIdx.x; e < n_elems; e += blockDim.x) {
@@ -926,7 +915,10 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
             *src = 0.0;
             const float v = (float) d;
 #endif
-            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + (size_t) cy * P.W * C + r, v);
+            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
+                if (inside) film_add(film0 + (size_t) cy * film_row + r, v);
+                else film_cell_add(P, film, w.bx0 + cx, w.by0 + cy, k, v);
+            }
         }
     }
 }
@@ -973,9 +965,8 @@ AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn
                 if (x < 0) continue;
                 const float wxv = xs < kMaxFoot ? wx[xs] : (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs));
                 const float w = wxv * wyv;
-                float *ptr = film + ((size_t) y * P.W + (size_t) x) * C;
 #pragma unroll
-                for (int k = 0; k < C; ++k) film_add(ptr + k, P.box ? vals[k] : vals[k] * w);
+                for (int k = 0; k < C; ++k) film_cell_add(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
             }
         }
     }
@@ -1122,8 +1113,10 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
     const int rowlen = w.ww * C;
     const int n_elems = rowlen * w.wh;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
-    float *film0 = film + ((size_t) w.by0 * P.W + (size_t) w.bx0) * C;
-    const uint32_t film_row = P.W * (uint32_t) C;
+    /* the wave window's quilt cells inside the film window (uniform; always for the whole quilt) */
+    const bool inside = in_window(P, w.bx0, w.by0) && in_window(P, w.bx0 + w.ww - 1, w.by0 + w.wh - 1);
+    float *film0 = inside ? film_cell(P, film, w.bx0, w.by0, 0) : film;
+    const uint32_t film_row = P.fw * (uint32_t) C;
     for (int e = (int) __lane_id(); e < n_elems; e += 64) {
         int cy = (int) ((float) e * inv_rowlen);
         cy -= (cy * rowlen > e) ? 1 : 0;
@@ -1144,7 +1137,10 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
             *src = 0.0;
             const float v = (float) d;
 #endif
-            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) film_add(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
+            if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
+                if (inside) film_add(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
+                else film_cell_add(P, film, w.bx0 + cx, w.by0 + cy, k, v);
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1281,7 +1277,7 @@ AD unsigned long long wave_sum(unsigned long long v) {
 }
 /* lane counters: stats[s * kStatShards + shard], one shard per block residue (summed on
  * the host), so the per-wave adds never pile onto one word */
-constexpr uint32_t kStatShards = 256, kStats = 8;
+constexpr uint32_t kStatShards = 256, kStats = 9;   /* [8]: paths pushed into the suffix */
 AD void stat_add(unsigned long long *stats, uint32_t which, unsigned long long v) {
     v = wave_sum(v);
     if (__lane_id() == 0 && v) atomicAdd(stats + which * kStatShards + blockIdx.x % kStatShards, v);
@@ -1375,13 +1371,29 @@ AD PathState load_state(float4 *const *q, uint32_t slot) {
 /* k_raygen_single: render_sample prologue (mvpath_single.h:50-76)     */
 /* ------------------------------------------------------------------ */
 
+/* global lane (mvpath.cpp:173-190 wavefront index) of virtual index v of the render's lane set:
+ * a contiguous range, or rect_h runs of run_len lanes (one per pixel row of the rectangle) */
+AD uint32_t lane_of(const KParams &P, uint64_t v) {
+    if (!P.rect) return (uint32_t) (P.range_begin + v);
+    const uint32_t vv = (uint32_t) v, r = vv / P.run_len, o = vv - r * P.run_len;
+    return ((P.rect_y0 + r) * P.W + P.rect_x0) * P.spp_pp + o;
+}
+/* the adaptive fill (mvpath_multi.h:79-115: dr::compress, dr::repeat): index in the PASS's
+ * repeated wavefront of entry j of this render's part -- entry e = j / n_adapt of the render's
+ * compressed list sits at e + run_delta[run of its lane] of the pass's compressed array */
+AD uint32_t adapt_index(const KParams &P, const Bufs &B, uint32_t j) {
+    const uint32_t e = j / P.n_adapt, rep = j - e * P.n_adapt;
+    const uint32_t run = P.rect ? B.asel[e] / P.run_len : 0u;
+    return (e + B.run_delta[run]) * P.n_adapt + rep;
+}
+
 /* TEA's v1 of the lane whose path sits in chunk slot `slot` (PCG increment 2 v1 + 1): the main
  * pass seeds lane chunk_begin + slot_lane(slot) with seed_value (k_raygen_single, primary_raygen),
  * the adaptive pass wavefront entry chunk_begin + slot with adapt_seed (k_raygen_adapt) */
-AD uint32_t path_seq(const KParams &P, uint32_t slot) {
+AD uint32_t path_seq(const KParams &P, const Bufs &B, uint32_t slot) {
     uint32_t v0, v1;
-    if (P.adapt_pass) tea4(P.adapt_seed, P.adapt_base + (uint32_t) (P.chunk_begin + slot), v0, v1);
-    else tea4(P.seed_value, (uint32_t) (P.chunk_begin + slot_lane(P, slot)), v0, v1);
+    if (P.adapt_pass) tea4(P.adapt_seed, adapt_index(P, B, (uint32_t) (P.chunk_begin + slot)), v0, v1);
+    else tea4(P.seed_value, lane_of(P, P.chunk_begin + slot_lane(P, slot)), v0, v1);
     return v1;
 }
 
@@ -1398,7 +1410,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
     PathState s;
     if (ok) {
         const uint32_t i = slot_lane(P, slot);
-        uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        const uint32_t lane = lane_of(P, P.chunk_begin + i);
         int px, py;
         lane_pixel(P, lane, px, py);
         uint32_t v0, v1;
@@ -1424,6 +1436,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
     }
     uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
     if (ok) store_state(B.q_out, qslot, s);
+    if (B.stats) stat_add(B.stats, 8, ok ? 1ull : 0ull);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1451,12 +1464,12 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
     bool ok = slot < P.chunk_n;
     PathState s;
     if (ok) {
-        const uint32_t j = (uint32_t) (P.chunk_begin + slot);      /* index in the adaptive wavefront */
-        const uint32_t lane = B.asel[j / P.n_adapt];
+        const uint32_t j = (uint32_t) (P.chunk_begin + slot);      /* index in this render's part of the fill */
+        const uint32_t lane = lane_of(P, B.asel[j / P.n_adapt]);
         float sx, sy, apx, apy;
         lane_sample_pos(P, lane, sx, sy, apx, apy);
         uint32_t v0, v1;
-        tea4(P.adapt_seed, P.adapt_base + j, v0, v1);
+        tea4(P.adapt_seed, adapt_index(P, B, j), v0, v1);
         Pcg rng;
         rng.seed(v0, v1);
         uint32_t index;
@@ -1474,6 +1487,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
     }
     uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
     if (ok) store_state(B.q_out, qslot, s);
+    if (B.stats) stat_add(B.stats, 8, ok ? 1ull : 0ull);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1643,7 +1657,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             s = load_state(B.q_in, i);
             Pcg rng;
             rng.state = s.rng_state;
-            rng.inc = (((uint64_t) path_seq(P, s.idx)) << 1) | 1u;
+            rng.inc = (((uint64_t) path_seq(P, B, s.idx)) << 1) | 1u;
             ++verts;
             keep = bounce_vertex<kDiff>(P, S, sc, s, rng, hit_of(B.hit[i]), nee, shr, nee_to, nee_thr, nee_c);
             s.rng_state = rng.state;
@@ -1717,7 +1731,7 @@ __global__ void __launch_bounds__(256, AMVPT_FUSED_WAVES) k_suffix_fused(KParams
             if (got) {
                 s = load_state(B.q_in, pbase + j);
                 rng.state = s.rng_state;
-                rng.inc = (((uint64_t) path_seq(P, s.idx)) << 1) | 1u;
+                rng.inc = (((uint64_t) path_seq(P, B, s.idx)) << 1) | 1u;
                 live = true;
             }
         }
@@ -1756,7 +1770,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
     float vals[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     float putx = 0.f, puty = 0.f;
     if (ok) {
-        uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        const uint32_t lane = lane_of(P, P.chunk_begin + i);
         int px, py;
         lane_pixel(P, lane, px, py);
         Pcg rng = lane_rng(P.seed_value, lane);
@@ -1791,7 +1805,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_adapt(KParams P, Bufs B) 
     if (ok) {
         const uint32_t j = (uint32_t) (P.chunk_begin + slot);
         float apx, apy;
-        lane_sample_pos(P, B.asel[j / P.n_adapt], sx, sy, apx, apy);
+        lane_sample_pos(P, lane_of(P, B.asel[j / P.n_adapt]), sx, sy, apx, apy);
         const float4 lo = B.lane_out[slot];
         const float w = P.adapt_w;
         pack_vals(P, C3{w * lo.x, w * lo.y, w * lo.z}, 1.f, w, vals);
@@ -1815,7 +1829,7 @@ struct PrimRay {
 };
 AD PrimRay primary_raygen(const KParams &P, const DView *V, uint32_t i) {
     PrimRay r;
-    const uint32_t lane = (uint32_t) (P.chunk_begin + i);
+    const uint32_t lane = lane_of(P, P.chunk_begin + i);
     int px, py;
     lane_pixel(P, lane, px, py);
     uint32_t v0;
@@ -2460,6 +2474,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
         stat_add(B.stats, 1, st_reuse);
         stat_add(B.stats, 2, st_vis);
         stat_add(B.stats, 0, (ok && P.max_depth != 0) ? 1ull : 0ull);
+        stat_add(B.stats, 8, push ? 1ull : 0ull);
     }
 }
 #undef VSF
@@ -2508,7 +2523,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     const float pdfW = l0.w;
     const C3 R0 = C3{l0.x, l0.y, l0.z}, Dp = C3{l1.x, l1.y, l1.z}, Bv = C3{l2.x, l2.y, l2.z};
     const f3 hp = mk(l3.x, l3.y, l3.z);
-    if (ok && B.amask) B.amask[P.chunk_begin - P.range_begin + i] = (lflags & LF_ADAPT) ? 1u : 0u;
+    if (ok && B.amask) B.amask[P.chunk_begin + i] = (lflags & LF_ADAPT) ? 1u : 0u;
     const bool valid_ray = (lflags & LF_VALIDRAY) || lo.w != 0.f;
     const bool mis = (lflags & LF_MIS) != 0, adapt_mask = (lflags & LF_ADAPT) != 0;
     const bool reuse = (lflags & LF_REUSE) != 0, direct = (lflags & LF_DIRECT) != 0;
@@ -2520,7 +2535,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     float sx = 0.f, sy = 0.f, apx = .5f, apy = .5f;
     uint32_t p_idx = 0;
     if (ok) {
-        const uint32_t lane = (uint32_t) (P.chunk_begin + i);
+        const uint32_t lane = lane_of(P, P.chunk_begin + i);
         int px, py;
         lane_pixel(P, lane, px, py);
         Pcg rng = lane_rng(P.seed_value, lane);
@@ -2633,6 +2648,32 @@ void launch_shadow(int walk, dim3 grid, size_t lds, hipStream_t st, const KParam
 ;
 #endif
 
+/* A/B knobs: kernel-path choices fixed in release builds.  A build with -DAMVPT_AB_KNOBS (tools/ab.sh
+ * variant libraries) reads them once from the environment; results are identical in every setting.
+ * Per-call path selection for tests goes through amvpt_render_opts.flags instead. */
+struct AbKnobs {
+    bool fuse_prim = true, row_splat = true, brute = true, fuse_nee = true, fuse_suffix = true;
+    uint32_t win_rs = AMVPT_WIN_RS, fused_blocks = AMVPT_FUSED_BLOCKS;
+};
+inline const AbKnobs &ab_knobs() {
+    static const AbKnobs k = [] {
+        AbKnobs r;
+#ifdef AMVPT_AB_KNOBS
+        auto off = [](const char *n) { const char *e = std::getenv(n); return e && e[0] == '0'; };
+        r.fuse_prim = !off("AMVPT_FUSE_PRIM");
+        r.row_splat = !off("AMVPT_ROW_SPLAT");
+        r.brute = !off("AMVPT_BRUTE");
+        r.fuse_nee = !off("AMVPT_FUSE_NEE");
+        r.fuse_suffix = !off("AMVPT_FUSE_SUFFIX");
+        if (const char *e = std::getenv("AMVPT_WIN_RS")) r.win_rs = (uint32_t) std::strtoul(e, nullptr, 0) % 32u;
+        if (const char *e = std::getenv("AMVPT_FUSED_BLOCKS"))
+            r.fused_blocks = std::max<uint32_t>(1, std::min<uint32_t>(64, (uint32_t) std::strtoul(e, nullptr, 0)));
+#endif
+        return r;
+    }();
+    return k;
+}
+
 /* Per-kernel HIP-event timing of an instrumented render (amvpt_counters given): an
  * event pair around every launch on the render stream, resolved in batches. */
 #ifndef AMVPT_FLUSH_MARKS
@@ -2716,8 +2757,7 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
     const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
     const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
-    static const bool fuse = [] { const char *e = std::getenv("AMVPT_FUSE_PRIM"); return !(e && e[0] == '0'); }();
-    if (uni && fuse) {
+    if (uni && ab_knobs().fuse_prim) {
         T.begin(AMVPT_K_PRIM_HIT, st);
         if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
@@ -2943,15 +2983,31 @@ constexpr uint32_t kMaxG = 16;
 static uint32_t dispatch_g(uint32_t G) { return G > kMaxG ? 0u : G; }
 constexpr uint64_t kSelectChunk = 1ull << 30;
 
+/* adaptive fill: flagged lanes of each run of a rectangular lane set (one block per run) */
+AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_run_counts(const uint8_t *amask, uint32_t run_len, uint32_t *counts) {
+    __shared__ unsigned long long part[4];
+    const uint8_t *m = amask + (size_t) blockIdx.x * run_len;
+    unsigned long long c = 0;
+    for (uint32_t i = threadIdx.x; i < run_len; i += blockDim.x) c += m[i];
+    c = wave_sum(c);
+    if (__lane_id() == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = (uint32_t) (part[0] + part[1] + part[2] + part[3]);
+}
+
 amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
-                         uint64_t lane_begin, uint64_t lane_end, float *film, void *stream,
-                         amvpt_counters *counters, float *records, uint32_t record_pass) {
+                         const amvpt_lane_set &lanes, const amvpt_film_window &fwin, void *stream,
+                         const amvpt_render_opts &opts, amvpt_counters *counters, float *records,
+                         uint32_t record_pass) {
+    float *const film = fwin.film;
     if (!scene || !views || !params || !film) { set_error("amvpt_render: null argument"); return AMVPT_ERR_INVALID; }
     RoctxScope range_render("amvpt_render");
     const amvpt_params &Pp = *params;
     hipStream_t st = (hipStream_t) stream;
-    bool diffuse_spec = g_diffuse_spec;
-    { const char *e = std::getenv("AMVPT_NO_DIFFUSE_SPEC"); if (e && e[0] == '1') diffuse_spec = false; }
+    const AbKnobs &K = ab_knobs();
+    const bool diffuse_spec = !(opts.flags & AMVPT_OPT_GENERIC_KERNELS);
+    const uint32_t trav = opts.traversal;
+    if (trav > 2) { set_error("amvpt_render: traversal must be 0 (auto), 1 (wave-uniform) or 2 (per-lane)"); return AMVPT_ERR_INVALID; }
     if (Pp.n_views == 0) { set_error("amvpt_render: n_views == 0"); return AMVPT_ERR_INVALID; }
     if (Pp.multisensor && !Pp.batch && Pp.n_views != Pp.grid_x * Pp.grid_y) {
         set_error("amvpt_render: a grid MultiSensor needs n_views == grid_x * grid_y");
@@ -2979,25 +3035,58 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             set_error("amvpt_render: unknown camera type");
             return AMVPT_ERR_INVALID;
         }
-    if (lane_end > L) lane_end = L;
+    /* ---- lane set: contiguous [lane_begin, lane_end), or a pixel rectangle (runs of pixel rows) ---- */
+    const uint32_t QW = Pp.film_width, QH = Pp.film_height;
+    bool rect = lanes.rect_width != 0;
+    uint64_t lane_begin = lanes.lane_begin, lane_end = lanes.lane_end;
+    uint32_t rx0 = 0, ry0 = 0, rw = 0, rh = 0;
+    if (rect) {
+        rx0 = lanes.rect_x0; ry0 = lanes.rect_y0; rw = lanes.rect_width; rh = lanes.rect_height;
+        if ((uint64_t) rx0 + rw > QW || (uint64_t) ry0 + rh > QH) {
+            set_error("amvpt_render: lane rectangle outside the quilt");
+            return AMVPT_ERR_INVALID;
+        }
+        /* whole pixel rows are one contiguous range */
+        if (rx0 == 0 && rw == QW) {
+            rect = false;
+            lane_begin = (uint64_t) ry0 * QW * spp_pp;
+            lane_end = (uint64_t) (ry0 + rh) * QW * spp_pp;
+        } else {
+            lane_begin = 0;
+            lane_end = (uint64_t) rw * rh * spp_pp;   /* virtual span */
+        }
+    }
+    if (!rect && lane_end > L) lane_end = L;
+    const uint64_t span = lane_begin < lane_end ? lane_end - lane_begin : 0;
+    const uint32_t n_runs = span == 0 ? 0u : (rect ? rh : 1u);
+    /* ---- film window ---- */
+    if ((uint64_t) fwin.x0 + fwin.width > QW || (uint64_t) fwin.y0 + fwin.height > QH) {
+        set_error("amvpt_render: film window outside the quilt");
+        return AMVPT_ERR_INVALID;
+    }
+    const bool whole_film = fwin.x0 == 0 && fwin.y0 == 0 && fwin.width == QW && fwin.height == QH;
+    if (!whole_film && !fwin.overflow) {
+        set_error("amvpt_render: a film window smaller than the quilt needs an overflow list");
+        return AMVPT_ERR_INVALID;
+    }
     /* the adaptive fill compacts the whole pass (its RNG seeds depend on the global
-     * wavefront): a lane range needs the host's count exchange (amvpt_set_adaptive_exchange) */
+     * wavefront): a partial lane set needs the host's count exchange */
     const bool do_fill = n_adapt && !Pp.debug;
-    const bool partial = lane_begin != 0 || lane_end != L;
-    const amvpt_exchange_fn exchange = g_exchange;
-    void *const exchange_ctx = g_exchange_ctx;
+    const bool partial = rect || lane_begin != 0 || lane_end != L;
+    const amvpt_run_exchange_fn exchange = opts.exchange;
+    void *const exchange_ctx = opts.exchange_ctx;
     if (do_fill && partial && !exchange) {
         set_error("amvpt_render: adaptive > 0 over a lane range needs amvpt_set_adaptive_exchange "
                   "(or the whole frame: lane_begin = 0, lane_end = all lanes)");
         return AMVPT_ERR_UNSUPPORTED;
     }
-    if (lane_begin >= lane_end) {
-        /* an empty range still takes part in every pass's count exchange (an all-gather on
+    if (span == 0) {
+        /* an empty lane set still takes part in every pass's count exchange (an all-gather on
          * the host side: the other ranks would wait for it forever) */
         if (do_fill && partial)
             for (uint32_t pass = 0; pass < n_passes; ++pass) {
-                uint64_t prefix = 0, total = 0;
-                if (exchange(exchange_ctx, 0, &prefix, &total) != 0) {
+                uint64_t total = 0;
+                if (exchange(exchange_ctx, 0, nullptr, nullptr, nullptr, &total) != 0) {
                     set_error("amvpt_render: adaptive count exchange failed");
                     return AMVPT_ERR_INVALID;
                 }
@@ -3031,21 +3120,20 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.inv_w = 1.f / (float) P.W;
     P.inv_h = 1.f / (float) P.H;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
-    P.trav_mode = g_traversal;
-    {
-        const char *e = std::getenv("AMVPT_WIN_RS");   /* A/B knob */
-        P.win_rs = e && e[0] ? (uint32_t) std::strtoul(e, nullptr, 0) % 32u : (uint32_t) AMVPT_WIN_RS;
-    }
-    P.range_begin = lane_begin;
+    P.trav_mode = trav;
+    P.win_rs = K.win_rs;
+    P.range_begin = rect ? 0 : lane_begin;
+    P.rect = rect ? 1u : 0u;
+    P.rect_x0 = rx0; P.rect_y0 = ry0;
+    P.run_len = rect ? rw * spp_pp : 0u;
+    P.fx0 = fwin.x0; P.fy0 = fwin.y0; P.fw = fwin.width; P.fh = fwin.height;
+    P.overflow = whole_film ? nullptr : fwin.overflow;
+    P.ov_cap = whole_film ? 0 : fwin.overflow_capacity;
     P.valid_ray0 = (!Pp.hide_emitters && scene->dev.environment >= 0) ? 1u : 0u;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
     /* row-reduced splat (row_put): RGBW film, Gaussian filter, >= 16 samples per pixel and pass
      * (a 16-lane row = one pixel); AMVPT_ROW_SPLAT=0 keeps the per-lane splat (A/B) */
-    {
-        const char *e = std::getenv("AMVPT_ROW_SPLAT");
-        const bool on = !(e && e[0] == '0');
-        P.row_splat = (on && P.C == 4 && !P.box && P.pow2 && spp_pp >= 16) ? 1u : 0u;
-    }
+    P.row_splat = (K.row_splat && P.C == 4 && !P.box && P.pow2 && spp_pp >= 16) ? 1u : 0u;
 
     /* views to device (tiny) */
     std::vector<DView> hv(Pp.n_views);
@@ -3067,12 +3155,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     /* lane arena: queues (2 x 5 x 16 B), lane_out + hit (32 B), NEE queue (52 B), visibility requests
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
-    const uint64_t span = lane_end - lane_begin;
     const bool wide = G > kMaxG;   /* the runtime group-size instance (64-bit view masks) */
     const bool diff_rec = scene->all_diffuse && diffuse_spec && !wide;   /* kDiff instances, compact view records */
     const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8 +
                             (wide ? 48 : 0);
-    uint64_t chunk_max = g_chunk_lanes;
+    uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
     if (chunk_max == 0) {
         chunk_max = 1ull << 25;
         while (chunk_max > (1ull << 23) && chunk_max * per_lane > (24ull << 30)) chunk_max >>= 1;
@@ -3109,22 +3196,25 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
     uint8_t *d_amask = nullptr;
-    uint32_t *d_asel = nullptr, *d_anum = nullptr;
+    uint32_t *d_asel = nullptr, *d_anum = nullptr, *d_runs = nullptr, *d_delta = nullptr;
     void *d_cub = nullptr;
     size_t cub_bytes = 0;
-    const uint64_t span_all = lane_end - lane_begin;
+    const uint64_t span_all = span;
+    const size_t runs_bytes = 4 * (((size_t) n_runs + 63) & ~(size_t) 63);
     const uint64_t sel_max = std::min<uint64_t>(span_all, kSelectChunk);
     if (do_fill) {
         HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, cub_bytes, hipcub::CountingInputIterator<uint32_t>(0),
                                              (const uint8_t *) nullptr, (uint32_t *) nullptr, (uint32_t *) nullptr,
                                              (int) sel_max, st));
         const size_t abytes = ((span_all + 255) & ~(uint64_t) 255) + 4 * ((span_all + 63) & ~(uint64_t) 63) + 256 +
-                              cub_bytes + 256;
+                              2 * runs_bytes + cub_bytes + 256;
         { const amvpt_status as_ = arena_reserve(A, A.adapt, A.abytes, abytes, "adaptive buffers"); if (as_ != AMVPT_OK) return as_; }
         char *ap = (char *) A.adapt;
         d_amask = (uint8_t *) ap; ap += (span_all + 255) & ~(uint64_t) 255;
         d_asel = (uint32_t *) ap; ap += 4 * ((span_all + 63) & ~(uint64_t) 63);
         d_anum = (uint32_t *) ap; ap += 256;
+        d_runs = (uint32_t *) ap; ap += runs_bytes;     /* flagged lanes per run (rect lane sets) */
+        d_delta = (uint32_t *) ap; ap += runs_bytes;    /* run_delta */
         d_cub = ap;
     }
 
@@ -3151,29 +3241,23 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     B.stats = dstats;
     B.amask = d_amask;
     B.asel = d_asel;
+    B.run_delta = d_delta;
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
     const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
-    const bool uni = scene_uniform(scene->dev.n_nodes, g_traversal);
-    /* suffix walk: brute force for tiny scenes in auto mode (AMVPT_BRUTE=0 turns it off, A/B) */
+    const bool uni = scene_uniform(scene->dev.n_nodes, trav);
+    /* suffix walk: brute force for tiny scenes in auto mode */
     int walk = uni ? WALK_UNI : WALK_LANE;
-    {
-        const char *e = std::getenv("AMVPT_BRUTE");
-        const bool brute_on = !(e && e[0] == '0');
-        if (uni && g_traversal == 0u && brute_on && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
-    }
+    if (uni && trav == 0u && K.brute && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
     const bool diff = diff_rec;                                                                           /* kDiff instances */
-    /* NEE traced inside k_bounce (brute-force walks; AMVPT_FUSE_NEE=0 keeps k_shadow, A/B) */
-    bool fuse_nee = walk == WALK_BRUTE || walk == WALK_BRUTE_NS;
-    { const char *e = std::getenv("AMVPT_FUSE_NEE"); if (e && e[0] == '0') fuse_nee = false; }
+    /* NEE traced inside k_bounce (brute-force walks; AMVPT_OPT_SPLIT_NEE keeps k_shadow) */
+    const bool fuse_nee = (walk == WALK_BRUTE || walk == WALK_BRUTE_NS) && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE);
     /* the whole suffix in one launch, paths in registers (brute-force walks with fused NEE;
-     * AMVPT_FUSE_SUFFIX=0 keeps the per-depth k_extend / k_bounce wavefronts, A/B) */
-    bool fuse_suffix = fuse_nee;
-    { const char *e = std::getenv("AMVPT_FUSE_SUFFIX"); if (e && e[0] == '0') fuse_suffix = false; }
-    uint32_t fused_blocks = AMVPT_FUSED_BLOCKS;
-    { const char *e = std::getenv("AMVPT_FUSED_BLOCKS"); if (e && e[0]) fused_blocks = std::max<uint32_t>(1, std::min<uint32_t>(64, (uint32_t) std::strtoul(e, nullptr, 0))); }
+     * AMVPT_OPT_WAVEFRONT_SUFFIX keeps the per-depth k_extend / k_bounce wavefronts) */
+    const bool fuse_suffix = fuse_nee && K.fuse_suffix && !(opts.flags & AMVPT_OPT_WAVEFRONT_SUFFIX);
+    const uint32_t fused_blocks = K.fused_blocks;
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
-    const size_t lds_ext = scene_lds_bytes(scene->dev, g_traversal);                                /* BVH walks */
+    const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
     if (wide && lds_prim + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 163840) {
         set_error("amvpt_render: per-view LDS state of this group size exceeds 160 KB");
@@ -3246,11 +3330,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         RoctxScope range_pass("amvpt pass");
         P.seed_value = Pp.base_seed + (is_mv ? (spp_pp * pass + Pp.seed) : Pp.seed);
         P.record = (records && pass == record_pass) ? 1u : 0u;
-        for (uint64_t c0 = lane_begin; c0 < lane_end; c0 += chunk) {
-            const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, lane_end - c0);
+        for (uint64_t c0 = 0; c0 < span; c0 += chunk) {   /* virtual indices of the lane set */
+            const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, span - c0);
             P.chunk_begin = c0;
             P.chunk_n = cn;
-            B.records = P.record ? records + (size_t) (c0 - lane_begin) * G * 8 : records;
+            B.records = P.record ? records + (size_t) c0 * G * 8 : records;
             const dim3 grid((cn + 255) / 256);
             /* counters: [0] = queue A, [1] = queue B */
             HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
@@ -3291,34 +3375,65 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         }
         if (do_fill) {
             RoctxScope range_fill("amvpt adaptive fill");
-            /* compact the pass's adapt_mask lanes in lane order, then n_adapt re-traces each */
+            /* compact the pass's adapt_mask lanes in lane order (virtual indices of the lane set,
+             * ascending = lane order), then n_adapt re-traces each */
             /* (hipcub counts in int: select in pieces of <= 2^30 lanes, appending) */
             uint64_t n_sel = 0;
             for (uint64_t s0 = 0; s0 < span_all; s0 += kSelectChunk) {
                 const uint64_t sn = std::min<uint64_t>(kSelectChunk, span_all - s0);
-                HIPCHK(hipcub::DeviceSelect::Flagged(d_cub, cub_bytes,
-                                                     hipcub::CountingInputIterator<uint32_t>((uint32_t) (lane_begin + s0)),
+                HIPCHK(hipcub::DeviceSelect::Flagged(d_cub, cub_bytes, hipcub::CountingInputIterator<uint32_t>((uint32_t) s0),
                                                      d_amask + s0, d_asel + n_sel, d_anum, (int) sn, st));
                 uint32_t got = 0;
                 HIPCHK(hipMemcpyAsync(&got, d_anum, 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
                 n_sel += got;
             }
-            /* this range's place in the pass's compressed array */
-            uint64_t prefix = 0, total = n_sel;
+            /* this render's place in the pass's compressed array: per run, the flagged lanes of the
+             * whole pass below it (one exchange per pass), as run_delta = global - local prefix */
+            uint64_t total = n_sel;
+            std::vector<uint32_t> delta(n_runs, 0u);
             if (partial) {
-                if (exchange(exchange_ctx, n_sel, &prefix, &total) != 0 || prefix + n_sel > total) {
+                std::vector<uint64_t> run_begin(n_runs), run_count(n_runs, 0), run_prefix(n_runs, 0);
+                if (rect) {
+                    hipLaunchKernelGGL(k_run_counts, dim3(n_runs), dim3(256), 0, st, (const uint8_t *) d_amask, P.run_len, d_runs);
+                    HIPCHK(hipGetLastError());
+                    std::vector<uint32_t> rc(n_runs);
+                    HIPCHK(hipMemcpyAsync(rc.data(), d_runs, 4 * (size_t) n_runs, hipMemcpyDeviceToHost, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    for (uint32_t r = 0; r < n_runs; ++r) {
+                        run_count[r] = rc[r];
+                        run_begin[r] = ((uint64_t) (ry0 + r) * QW + rx0) * spp_pp;
+                    }
+                } else {
+                    run_count[0] = n_sel;
+                    run_begin[0] = lane_begin;
+                }
+                if (exchange(exchange_ctx, n_runs, run_begin.data(), run_count.data(), run_prefix.data(), &total) != 0) {
                     set_error("amvpt_render: adaptive count exchange failed");
                     return AMVPT_ERR_INVALID;
                 }
+                uint64_t local = 0;
+                for (uint32_t r = 0; r < n_runs; ++r) {
+                    if (run_prefix[r] < local || run_prefix[r] + run_count[r] > total) {
+                        set_error("amvpt_render: adaptive count exchange returned inconsistent prefixes");
+                        return AMVPT_ERR_INVALID;
+                    }
+                    delta[r] = (uint32_t) (run_prefix[r] - local);
+                    local += run_count[r];
+                }
+                if (local != n_sel) {
+                    set_error("amvpt_render: per-run adaptive counts disagree with the compaction");
+                    return AMVPT_ERR_INVALID;
+                }
             }
+            if (total * n_adapt > 0xffffffffull) { set_error("amvpt_render: adaptive wavefront over 2^32 lanes"); return AMVPT_ERR_UNSUPPORTED; }
+            HIPCHK(hipMemcpyAsync(d_delta, delta.data(), 4 * (size_t) n_runs, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));   /* `delta` is a host temporary */
             const uint64_t wf = n_sel * n_adapt;
             adaptive_lanes += wf;
-            if (total * n_adapt > 0xffffffffull) { set_error("amvpt_render: adaptive wavefront over 2^32 lanes"); return AMVPT_ERR_UNSUPPORTED; }
             KParams Ps = P;
             P.pass_seed = P.seed_value;
             P.adapt_seed = Pp.base_seed + (uint32_t) (total * n_adapt);   /* sampler->fork(); seed(wavefront, wavefront) */
-            P.adapt_base = (uint32_t) (prefix * n_adapt);
             P.adapt_pass = 1;
             P.record = 0;
             for (uint64_t c0 = 0; c0 < wf; c0 += chunk) {
@@ -3345,6 +3460,17 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             P = Ps;
         }
     }
+    uint64_t overflow_cells = 0;
+    if (P.overflow) {
+        /* the caller sums the list; a list that ran out of room lost cells: fail loudly */
+        HIPCHK(hipMemcpyAsync(&overflow_cells, P.overflow, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (overflow_cells > P.ov_cap) {
+            set_error("amvpt_render: film overflow list full (" + std::to_string(overflow_cells) + " cells > capacity " +
+                      std::to_string(P.ov_cap) + "): widen the film window or the list");
+            return AMVPT_ERR_OOM;
+        }
+    }
     if (counters) {
         std::vector<unsigned long long> hsh((size_t) kStats * kStatShards);
         HIPCHK(hipMemcpyAsync(hsh.data(), dstats, stats_bytes, hipMemcpyDeviceToHost, st));
@@ -3366,6 +3492,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.record_bytes = G > 1 ? 64 + 16 + (diff_rec ? 4 : 32) * (uint64_t) G : 0;
         c.nonfinite_samples = hs[6];
         c.negative_samples = hs[7];
+        c.pushed_paths = hs[8];
+        c.film_overflow = overflow_cells;
         T.flush();
         HIPCHK(T.err);
         for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }
@@ -3375,6 +3503,40 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.kernel_ms_splat = T.ms[AMVPT_K_SPLAT];
         c.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    return AMVPT_OK;
+}
+
+/* amvpt_film_accumulate: window rows into the quilt (one thread per float; a window's floats are
+ * distinct quilt floats, so plain adds), then the overflow entries (float atomics: entries repeat) */
+AMVPT_TU_LOCAL __global__ void k_accumulate(float *quilt, uint32_t qw, uint32_t C, const float *win, uint32_t x0,
+                                            uint32_t y0, uint32_t w) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (i >= w * C) return;
+    quilt[((size_t) (y0 + y) * qw + x0) * C + i] += win[(size_t) y * w * C + i];
+}
+AMVPT_TU_LOCAL __global__ void k_overflow_apply(float *quilt, uint64_t n_floats, const uint4 *e, uint64_t n) {
+    const uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 v = e[i];
+    const uint64_t idx = (uint64_t) v.x | ((uint64_t) v.y << 32);
+    if (idx < n_floats) atomicAdd(quilt + idx, __uint_as_float(v.z));
+}
+amvpt_status accumulate_impl(float *quilt, uint32_t qw, uint32_t qh, uint32_t C, const float *win, uint32_t x0,
+                             uint32_t y0, uint32_t w, uint32_t h, const uint32_t *ov, uint64_t n_ov, void *stream) {
+    if (!quilt || (w && h && !win) || (n_ov && !ov) || (C != 4 && C != 5)) {
+        set_error("amvpt_film_accumulate: bad argument");
+        return AMVPT_ERR_INVALID;
+    }
+    if ((uint64_t) x0 + w > qw || (uint64_t) y0 + h > qh) {
+        set_error("amvpt_film_accumulate: window outside the quilt");
+        return AMVPT_ERR_INVALID;
+    }
+    hipStream_t st = (hipStream_t) stream;
+    if (w && h) hipLaunchKernelGGL(k_accumulate, dim3((w * C + 255) / 256, h), dim3(256), 0, st, quilt, qw, C, win, x0, y0, w);
+    if (n_ov)
+        hipLaunchKernelGGL(k_overflow_apply, dim3((uint32_t) ((n_ov + 255) / 256)), dim3(256), 0, st, quilt,
+                           (uint64_t) qw * qh * C, (const uint4 *) ov, n_ov);
+    HIPCHK(hipGetLastError());
     return AMVPT_OK;
 }
 

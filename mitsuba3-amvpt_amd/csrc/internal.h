@@ -23,12 +23,14 @@ namespace amvpt {
 void set_error(const std::string &msg);
 amvpt_status hip_fail(const char *what, int err);
 amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
-                         uint64_t lane_begin, uint64_t lane_end, float *film, void *stream,
-                         amvpt_counters *counters, float *records, uint32_t record_pass);
+                         const amvpt_lane_set &lanes, const amvpt_film_window &film, void *stream,
+                         const amvpt_render_opts &opts, amvpt_counters *counters, float *records,
+                         uint32_t record_pass);
 amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream);
+amvpt_status accumulate_impl(float *quilt, uint32_t qw, uint32_t qh, uint32_t C, const float *win, uint32_t x0,
+                             uint32_t y0, uint32_t w, uint32_t h, const uint32_t *ov, uint64_t n_ov, void *stream);
 extern uint64_t g_chunk_lanes;
 extern uint32_t g_traversal;
-extern bool g_diffuse_spec;
 extern amvpt_exchange_fn g_exchange;
 extern void *g_exchange_ctx;
 } // namespace amvpt

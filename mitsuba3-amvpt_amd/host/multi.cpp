@@ -1,25 +1,37 @@
 /*
  * multi.cpp -- Integrator::render over several GPUs of one node, without torch.
  *
- * The path shards by lanes: every pass is the lane space [0, W*H*spp_per_pass) and a lane seeds its
- * sampler from its global index (TEA(seed_value, lane), mvpath.cpp:227-235), so device r renders the
- * contiguous range amvpt_host_lane_shard(L, r, n) of every pass (a band of quilt rows) and the frame
- * is bit-for-bit the single-GPU one up to float summation order.  The only data-path collective is
- * the sum of the per-device RGBW ImageBlocks: one RCCL reduce (sum, fp32) onto devices[0] over
- * xGMI, then develop there (hdrfilm.cpp:304-418).  With adaptive > 0 the fill compacts the whole
- * pass (mvpath_multi.h:79-115), so the devices exchange their per-pass flagged-lane counts through
- * amvpt_set_adaptive_exchange: an in-process all-gather between the device threads.
+ * Every lane seeds its sampler from its global index (TEA(seed_value, lane), mvpath.cpp:227-235), so a
+ * frame shards across devices with results bit-for-bit the single-GPU ones (float summation order
+ * aside).  Two partitions, as bench.py / amvpt.dist:
+ *   view groups (C5, "4 views per GPU"): device r owns whole view groups (mvpath_multi.h:31-38), a
+ *     rectangle of quilt tiles; it renders the lanes of those pixels (amvpt_lane_set rect form) into a
+ *     film window of its tiles + a 4-px filter border, and the windows (and the few overflow cells)
+ *     are sent to devices[0] (ncclSend / ncclRecv over xGMI) and summed into the quilt there
+ *     (amvpt_film_accumulate);
+ *   lane bands (otherwise): device r renders the contiguous range amvpt_host_lane_shard(L, r, n) of
+ *     every pass into a whole-quilt ImageBlock, summed onto devices[0] with one ncclReduce.
+ * Then develop on devices[0] (hdrfilm.cpp:304-418).  With adaptive > 0 the fill compacts the whole
+ * pass (mvpath_multi.h:79-115): the device threads exchange their per-run flagged-lane counts through
+ * the per-call amvpt_render_opts.exchange (an in-process all-gather) -- no process-global state.
  *
- * One host thread per device drives its own scene copy, stream and film (8(b) "Threading").  A
- * device whose render fails still joins the reduce with its (zeroed) film, so no peer blocks in
- * the collective; the call then reports the first error.
+ * Per-frame cost: the RCCL communicators, the per-device scene copies (scene upload + BVH build),
+ * streams and film buffers are cached on the host scene, keyed by the device list, and reused by the
+ * next frame (amvpt_host_multi_stats counts scene creations and communicator initialisations).
+ *
+ * Failure handling: the device threads meet at in-process barriers after setup and after the render;
+ * the collectives run only when every device reached them healthy, so a failing device (bad id, OOM,
+ * a failed render) never leaves a peer blocked inside RCCL, and a failed render aborts the count
+ * exchange so no peer waits in it either.  The call then reports the first error.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -31,23 +43,50 @@
 
 namespace {
 
-/* per-pass all-gather of the adaptive fill's local counts between the device threads */
-struct CountExchange {
+/* in-process barrier of the device threads; each thread reports whether it is healthy and learns
+ * whether all were */
+struct Barrier {
     std::mutex mu;
     std::condition_variable cv;
-    int world = 1;
-    int arrived = 0;
-    bool aborted = false;     /* a device failed: the others' exchanges fail instead of waiting */
+    int world = 1, arrived = 0;
     uint64_t generation = 0;
-    std::vector<uint64_t> counts, published;
+    bool all_ok = true, published_ok = true;
+    bool wait(bool ok) {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = generation;
+        all_ok = all_ok && ok;
+        if (++arrived == world) {
+            published_ok = all_ok;
+            all_ok = true;
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen; });
+        }
+        return published_ok;
+    }
+};
 
-    int exchange(int rank, uint64_t local, uint64_t *prefix, uint64_t *total) {
+/* per-pass all-gather of the adaptive fill's per-run counts between the device threads
+ * (amvpt_run_exchange_fn); a failed device aborts it so no peer waits */
+struct RunExchange {
+    std::mutex mu;
+    std::condition_variable cv;
+    int world = 1, arrived = 0;
+    bool aborted = false;
+    uint64_t generation = 0;
+    std::vector<std::vector<uint64_t>> begins, counts, pub_b, pub_c;
+
+    int exchange(int rank, uint32_t n, const uint64_t *b, const uint64_t *c, uint64_t *prefix, uint64_t *total) {
         std::unique_lock<std::mutex> lk(mu);
         if (aborted) return -1;
         const uint64_t gen = generation;
-        counts[(size_t) rank] = local;
+        begins[(size_t) rank].assign(b, b + n);
+        counts[(size_t) rank].assign(c, c + n);
         if (++arrived == world) {
-            published = counts;
+            pub_b = begins;
+            pub_c = counts;
             arrived = 0;
             ++generation;
             cv.notify_all();
@@ -55,12 +94,17 @@ struct CountExchange {
             cv.wait(lk, [&] { return generation != gen || aborted; });
             if (generation == gen) return -1;
         }
-        uint64_t p = 0, t = 0;
-        for (int r = 0; r < world; ++r) {
-            if (r < rank) p += published[(size_t) r];
-            t += published[(size_t) r];
+        /* runs of different devices are disjoint: a run's prefix is every count that starts below it */
+        uint64_t t = 0;
+        for (int r = 0; r < world; ++r)
+            for (uint64_t x : pub_c[(size_t) r]) t += x;
+        for (uint32_t i = 0; i < n; ++i) {
+            uint64_t p = 0;
+            for (int r = 0; r < world; ++r)
+                for (size_t j = 0; j < pub_b[(size_t) r].size(); ++j)
+                    if (pub_b[(size_t) r][j] < b[i]) p += pub_c[(size_t) r][j];
+            prefix[i] = p;
         }
-        *prefix = p;
         *total = t;
         return 0;
     }
@@ -70,24 +114,98 @@ struct CountExchange {
         cv.notify_all();
     }
 };
-
-thread_local int t_rank = 0;
-
-int exchange_cb(void *ctx, uint64_t local, uint64_t *prefix, uint64_t *total) {
-    return static_cast<CountExchange *>(ctx)->exchange(t_rank, local, prefix, total);
+struct RankExchange { RunExchange *ex; int rank; };
+int run_exchange_cb(void *ctx, uint32_t n, const uint64_t *b, const uint64_t *c, uint64_t *prefix, uint64_t *total) {
+    const RankExchange *x = static_cast<const RankExchange *>(ctx);
+    return x->ex->exchange(x->rank, n, b, c, prefix, total);
 }
 
-struct DeviceResult {
-    std::string error;
-    amvpt_counters counters{};
+/* device buffers of one device, grown on demand and kept across frames */
+struct DevState {
+    int device = -1;
+    amvpt_scene *scene = nullptr;
+    hipStream_t st = nullptr;
+    float *film = nullptr;  size_t film_bytes = 0;       /* window (view groups) or whole quilt (lane bands) */
+    uint32_t *ovf = nullptr; size_t ovf_bytes = 0;       /* overflow list (view groups) */
+    float *quilt = nullptr; size_t quilt_bytes = 0;      /* devices[0], view groups: the assembled ImageBlock */
+    float *out = nullptr;   size_t out_bytes = 0;        /* devices[0]: developed image */
+    std::vector<float *> recv; std::vector<size_t> recv_bytes;     /* devices[0]: peers' windows */
+    std::vector<uint32_t *> recv_ov; std::vector<size_t> recv_ov_bytes;
 };
+
+bool grow(void *&p, size_t &have, size_t need) {
+    if (have >= need) return true;
+    if (p) (void) hipFree(p);
+    p = nullptr;
+    have = 0;
+    if (hipMalloc(&p, need) != hipSuccess) return false;
+    have = need;
+    return true;
+}
+template <class T> bool grow(T *&p, size_t &have, size_t need) {
+    void *v = p;
+    const bool ok = grow(v, have, need);
+    p = static_cast<T *>(v);
+    return ok;
+}
 
 }  // namespace
 
-int amvpt_host_guarded_call(int (*fn)(void *), void *ctx);   /* scene.cpp: exception -> status + last_error */
+/* the per-scene multi-GPU cache (opaque to scene.cpp) */
+struct amvpt_multi_cache {
+    std::mutex mu;   /* one render_multi at a time per scene */
+    std::vector<int> devices;
+    std::vector<ncclComm_t> comms;
+    std::vector<DevState> dev;
+    uint64_t scene_creates = 0, comm_inits = 0, renders = 0;
+    void release() {
+        int cur = -1;
+        const bool restore = hipGetDevice(&cur) == hipSuccess;
+        for (auto c : comms) if (c) (void) ncclCommDestroy(c);
+        comms.clear();
+        for (DevState &d : dev) {
+            if (d.device >= 0) (void) hipSetDevice(d.device);
+            if (d.st) (void) hipStreamSynchronize(d.st);
+            for (void *p : {(void *) d.film, (void *) d.ovf, (void *) d.quilt, (void *) d.out}) if (p) (void) hipFree(p);
+            for (float *p : d.recv) if (p) (void) hipFree(p);
+            for (uint32_t *p : d.recv_ov) if (p) (void) hipFree(p);
+            if (d.scene) amvpt_scene_destroy(d.scene);
+            if (d.st) (void) hipStreamDestroy(d.st);
+        }
+        dev.clear();
+        devices.clear();
+        if (restore) (void) hipSetDevice(cur);   /* the caller's current device stays as it was */
+    }
+    ~amvpt_multi_cache() { release(); }
+};
+
+/* scene.cpp: the host scene's cache slot and the exception guard */
+std::shared_ptr<amvpt_multi_cache> &amvpt_host_multi_slot(amvpt_host_scene *s);
+int amvpt_host_guarded_call(int (*fn)(void *), void *ctx);
 template <class F> static int amvpt_host_guarded(F &&f) {
     return amvpt_host_guarded_call([](void *c) { return (*static_cast<F *>(c))(); }, &f);
 }
+
+namespace {
+
+/* MVPathIntegrator::render's group size (mvpath.cpp:192-217) */
+uint32_t group_size(const amvpt_params &p) {
+    const bool reuse = p.integrator == AMVPT_INTEGRATOR_MVPATH && p.sa_reuse && p.n_views > 1 && p.reuse_count != 1;
+    if (!reuse) return 1;
+    const uint32_t N = p.n_views;
+    uint32_t G = std::min(p.reuse_count, N);
+    if (G == 0 || N % G) {
+        G = 0;
+        for (uint32_t q = 8; q < N; ++q) if (N % q == 0) { G = q; break; }
+        if (!G) for (uint32_t q = 8; q > 1; --q) if (N % q == 0) { G = q; break; }
+        if (!G) G = N;
+    }
+    return G;
+}
+
+constexpr uint32_t kFilterBorder = 4;   /* amvpt.dist.FILTER_BORDER */
+
+}  // namespace
 
 extern "C" {
 
@@ -96,6 +214,48 @@ void amvpt_host_lane_shard(uint64_t lanes, uint32_t rank, uint32_t world, uint64
     const uint64_t b = rank * q + std::min<uint64_t>(rank, r);
     *begin = b;
     *end = b + q + (rank < r ? 1u : 0u);
+}
+
+int amvpt_host_view_group_partition(const amvpt_params *p, uint32_t rank, uint32_t world, uint32_t *rect,
+                                    uint32_t *window) {
+    if (!p || !p->multisensor || world == 0 || rank >= world) return 0;
+    const uint32_t G = group_size(*p);
+    if (G < 1 || p->n_views % G) return 0;
+    const uint32_t n_groups = p->n_views / G;
+    if (n_groups < world || n_groups % world) return 0;
+    const uint32_t gx = std::max(1u, p->grid_x), gy = std::max(1u, p->grid_y);
+    const uint32_t sx = p->film_width / gx, sy = p->film_height / gy;
+    const uint32_t per = n_groups / world, v0 = rank * per * G, v1 = (rank + 1) * per * G;
+    /* tiles of views [v0, v1): the inverse of GridSensor::sample_ray_idx's index (grid.cpp:269-297) */
+    uint32_t tx0 = gx, ty0 = gy, tx1 = 0, ty1 = 0;
+    std::vector<uint8_t> seen((size_t) gx * gy, 0);
+    for (uint32_t v = v0; v < v1; ++v) {
+        uint32_t ix = v % gx, iy = v / gx;
+        if (p->reverse_x) ix = gx - 1 - ix;
+        if (p->reverse_y) iy = gy - 1 - iy;
+        if (iy >= gy) return 0;
+        seen[(size_t) iy * gx + ix] = 1;
+        tx0 = std::min(tx0, ix); ty0 = std::min(ty0, iy); tx1 = std::max(tx1, ix + 1); ty1 = std::max(ty1, iy + 1);
+    }
+    if ((tx1 - tx0) * (ty1 - ty0) != v1 - v0) return 0;   /* not a rectangle of tiles */
+    rect[0] = tx0 * sx; rect[1] = ty0 * sy; rect[2] = (tx1 - tx0) * sx; rect[3] = (ty1 - ty0) * sy;
+    const uint32_t wx0 = rect[0] > kFilterBorder ? rect[0] - kFilterBorder : 0;
+    const uint32_t wy0 = rect[1] > kFilterBorder ? rect[1] - kFilterBorder : 0;
+    const uint32_t wx1 = std::min(p->film_width, rect[0] + rect[2] + kFilterBorder);
+    const uint32_t wy1 = std::min(p->film_height, rect[1] + rect[3] + kFilterBorder);
+    window[0] = wx0; window[1] = wy0; window[2] = wx1 - wx0; window[3] = wy1 - wy0;
+    return 1;
+}
+
+int amvpt_host_multi_stats(amvpt_host_scene *s, uint64_t *scene_creates, uint64_t *comm_inits, uint64_t *renders) {
+    return amvpt_host_guarded([&] {
+        if (!s) throw std::runtime_error("amvpt_host_multi_stats: null scene");
+        std::shared_ptr<amvpt_multi_cache> &slot = amvpt_host_multi_slot(s);
+        if (scene_creates) *scene_creates = slot ? slot->scene_creates : 0;
+        if (comm_inits) *comm_inits = slot ? slot->comm_inits : 0;
+        if (renders) *renders = slot ? slot->renders : 0;
+        return 0;
+    });
 }
 
 int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uint32_t spp, int raw,
@@ -113,80 +273,184 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
         const uint32_t C = amvpt_film_channels(&p);
         const size_t npx = (size_t) p.film_width * p.film_height, nfloat = npx * C;
         const int n = n_devices;
+        {
+            int visible = 0;
+            if (hipGetDeviceCount(&visible) != hipSuccess) visible = 0;
+            for (int r = 0; r < n; ++r)
+                if (devices[r] < 0 || devices[r] >= visible)
+                    throw std::runtime_error("amvpt_host_render_multi: device " + std::to_string(devices[r]) +
+                                             " is not visible (" + std::to_string(visible) + " devices)");
+        }
 
-        std::vector<ncclComm_t> comms((size_t) n);
-        if (ncclCommInitAll(comms.data(), n, devices) != ncclSuccess) throw std::runtime_error("ncclCommInitAll failed");
-        struct Comms {
-            std::vector<ncclComm_t> &c;
-            ~Comms() { for (auto x : c) if (x) (void) ncclCommDestroy(x); }
-        } comms_guard{comms};
+        /* ---- the cache: communicators, per-device scenes, streams and buffers for this device list ---- */
+        std::shared_ptr<amvpt_multi_cache> &slot = amvpt_host_multi_slot(s);
+        if (!slot) slot = std::make_shared<amvpt_multi_cache>();
+        std::shared_ptr<amvpt_multi_cache> cache = slot;
+        std::lock_guard<std::mutex> cache_lock(cache->mu);
+        const std::vector<int> devs(devices, devices + n);
+        if (cache->devices != devs) {
+            cache->release();
+            cache->devices = devs;
+            cache->dev.resize((size_t) n);
+            for (int r = 0; r < n; ++r) cache->dev[(size_t) r].device = devs[(size_t) r];
+        }
+        if (cache->comms.empty() && n > 1) {
+            cache->comms.assign((size_t) n, nullptr);
+            if (ncclCommInitAll(cache->comms.data(), n, devices) != ncclSuccess) {
+                cache->comms.clear();
+                throw std::runtime_error("ncclCommInitAll failed");
+            }
+            ++cache->comm_inits;
+        }
 
-        CountExchange ex;
+        /* ---- partition: view groups when they divide among the devices, else lane bands ---- */
+        std::vector<std::array<uint32_t, 4>> rects((size_t) n), wins((size_t) n);
+        bool groups = n > 1;
+        for (int r = 0; r < n && groups; ++r)
+            groups = amvpt_host_view_group_partition(&p, (uint32_t) r, (uint32_t) n, rects[(size_t) r].data(),
+                                                     wins[(size_t) r].data()) == 1;
+        const uint64_t ov_cap = 1u << 20;
+
+        Barrier bar;
+        bar.world = n;
+        RunExchange ex;
         ex.world = n;
-        ex.counts.assign((size_t) n, 0);
-        (void) amvpt_set_adaptive_exchange(n > 1 ? exchange_cb : nullptr, n > 1 ? &ex : nullptr);
-        struct ResetExchange { ~ResetExchange() { (void) amvpt_set_adaptive_exchange(nullptr, nullptr); } } reset_ex;
-
-        std::vector<DeviceResult> res((size_t) n);
+        ex.begins.resize((size_t) n);
+        ex.counts.resize((size_t) n);
+        std::vector<RankExchange> rx((size_t) n);
+        std::vector<std::string> errors((size_t) n);
+        std::vector<amvpt_counters> cnt((size_t) n);
+        std::vector<uint64_t> ov_count((size_t) n, 0);
         std::vector<std::thread> threads;
         for (int r = 0; r < n; ++r) {
             threads.emplace_back([&, r] {
-                t_rank = r;
-                DeviceResult &R = res[(size_t) r];
-                amvpt_scene *dsc = nullptr;
-                hipStream_t st = nullptr;
-                float *film = nullptr, *dev_out = nullptr;
-                auto fail = [&](const std::string &m) { if (R.error.empty()) R.error = m; };
-                if (hipSetDevice(devices[r]) != hipSuccess) fail("hipSetDevice failed");
-                if (R.error.empty() && hipStreamCreate(&st) != hipSuccess) fail("hipStreamCreate failed");
-                if (R.error.empty() && hipMalloc(&film, nfloat * sizeof(float)) != hipSuccess) fail("hipMalloc(film) failed");
-                if (R.error.empty() && hipMemsetAsync(film, 0, nfloat * sizeof(float), st) != hipSuccess) fail("hipMemset(film) failed");
-                if (R.error.empty() && amvpt_scene_create(sd, &dsc) != AMVPT_OK) fail(amvpt_last_error());
-                uint64_t b, e;
-                amvpt_host_lane_shard(L, (uint32_t) r, (uint32_t) n, &b, &e);
-                if (R.error.empty() &&
-                    amvpt_render(dsc, views, &p, b, e, film, st, counters ? &R.counters : nullptr) != AMVPT_OK) {
+                DevState &D = cache->dev[(size_t) r];
+                std::string &err = errors[(size_t) r];
+                auto fail = [&](const std::string &m) { if (err.empty()) err = m; };
+                /* -- setup (nothing collective) -- */
+                if (hipSetDevice(D.device) != hipSuccess) fail("hipSetDevice failed");
+                if (err.empty() && !D.st && hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking) != hipSuccess) fail("hipStreamCreate failed");
+                if (err.empty() && !D.scene) {
+                    if (amvpt_scene_create(sd, &D.scene) != AMVPT_OK) fail(amvpt_last_error());
+                    else {
+                        std::lock_guard<std::mutex> lk(bar.mu);
+                        ++cache->scene_creates;
+                    }
+                }
+                const size_t wfloats = groups ? (size_t) wins[(size_t) r][2] * wins[(size_t) r][3] * C : nfloat;
+                if (err.empty() && !grow(D.film, D.film_bytes, wfloats * sizeof(float))) fail("hipMalloc(film) failed");
+                if (err.empty() && groups && !grow(D.ovf, D.ovf_bytes, 16 * (ov_cap + 1))) fail("hipMalloc(overflow) failed");
+                if (err.empty() && hipMemsetAsync(D.film, 0, wfloats * sizeof(float), D.st) != hipSuccess) fail("hipMemset(film) failed");
+                if (err.empty() && groups && hipMemsetAsync(D.ovf, 0, 16, D.st) != hipSuccess) fail("hipMemset(overflow) failed");
+                if (r == 0 && err.empty() && groups) {
+                    if (!grow(D.quilt, D.quilt_bytes, nfloat * sizeof(float))) fail("hipMalloc(quilt) failed");
+                    D.recv.resize((size_t) n, nullptr); D.recv_bytes.resize((size_t) n, 0);
+                    D.recv_ov.resize((size_t) n, nullptr); D.recv_ov_bytes.resize((size_t) n, 0);
+                    for (int q = 1; q < n && err.empty(); ++q)
+                        if (!grow(D.recv[(size_t) q], D.recv_bytes[(size_t) q], (size_t) wins[(size_t) q][2] * wins[(size_t) q][3] * C * sizeof(float)))
+                            fail("hipMalloc(window receive) failed");
+                }
+                if (!bar.wait(err.empty())) { if (err.empty()) err = "a peer device failed during setup"; return; }
+
+                /* -- render this device's share (the count exchange is the only cross-device step) -- */
+                amvpt_lane_set lanes{};
+                amvpt_film_window fw{};
+                fw.film = D.film;
+                if (groups) {
+                    lanes.rect_x0 = rects[(size_t) r][0]; lanes.rect_y0 = rects[(size_t) r][1];
+                    lanes.rect_width = rects[(size_t) r][2]; lanes.rect_height = rects[(size_t) r][3];
+                    fw.x0 = wins[(size_t) r][0]; fw.y0 = wins[(size_t) r][1];
+                    fw.width = wins[(size_t) r][2]; fw.height = wins[(size_t) r][3];
+                    fw.overflow = D.ovf;
+                    fw.overflow_capacity = ov_cap;
+                } else {
+                    amvpt_host_lane_shard(L, (uint32_t) r, (uint32_t) n, &lanes.lane_begin, &lanes.lane_end);
+                    fw.width = p.film_width; fw.height = p.film_height;
+                }
+                rx[(size_t) r] = RankExchange{&ex, r};
+                amvpt_render_opts o{};
+                if (n > 1) { o.exchange = run_exchange_cb; o.exchange_ctx = &rx[(size_t) r]; }
+                if (amvpt_render_ex(D.scene, views, &p, &lanes, &fw, D.st, &o, counters ? &cnt[(size_t) r] : nullptr) != AMVPT_OK) {
                     fail(amvpt_last_error());
                     ex.abort();
-                    (void) hipMemsetAsync(film, 0, nfloat * sizeof(float), st);
                 }
-                /* every device joins the reduce (a missing peer would block the others in it) */
-                if (film && ncclReduce(film, film, nfloat, ncclFloat, ncclSum, 0, comms[(size_t) r], st) != ncclSuccess)
-                    fail("ncclReduce failed");
-                if (st && hipStreamSynchronize(st) != hipSuccess) fail("hipStreamSynchronize failed");
-                if (r == 0 && film) {
+                if (err.empty() && groups &&
+                    (hipMemcpyAsync(&ov_count[(size_t) r], D.ovf, 8, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
+                     hipStreamSynchronize(D.st) != hipSuccess))
+                    fail("overflow count read failed");
+                if (!bar.wait(err.empty())) { if (err.empty()) err = "a peer device failed during the render"; return; }
+
+                /* -- combine on devices[0]: every device is healthy here, so every collective completes -- */
+                if (groups) {
+                    if (r == 0)
+                        for (int q = 1; q < n && err.empty(); ++q)
+                            if (!grow(D.recv_ov[(size_t) q], D.recv_ov_bytes[(size_t) q], 16 * std::max<uint64_t>(1, ov_count[(size_t) q])))
+                                fail("hipMalloc(overflow receive) failed");
+                    if (!bar.wait(err.empty())) { if (err.empty()) err = "a peer device failed before the gather"; return; }
+                    ncclComm_t comm = cache->comms[(size_t) r];
+                    bool ok = ncclGroupStart() == ncclSuccess;
+                    if (r == 0) {
+                        for (int q = 1; q < n; ++q) {
+                            const size_t wf = (size_t) wins[(size_t) q][2] * wins[(size_t) q][3] * C;
+                            ok = ok && ncclRecv(D.recv[(size_t) q], wf, ncclFloat, q, comm, D.st) == ncclSuccess;
+                            if (ov_count[(size_t) q])
+                                ok = ok && ncclRecv(D.recv_ov[(size_t) q], 4 * ov_count[(size_t) q], ncclUint32, q, comm, D.st) == ncclSuccess;
+                        }
+                    } else {
+                        ok = ok && ncclSend(D.film, wfloats, ncclFloat, 0, comm, D.st) == ncclSuccess;
+                        if (ov_count[(size_t) r])
+                            ok = ok && ncclSend(D.ovf + 4, 4 * ov_count[(size_t) r], ncclUint32, 0, comm, D.st) == ncclSuccess;
+                    }
+                    ok = (ncclGroupEnd() == ncclSuccess) && ok;
+                    if (!ok) fail("ncclSend / ncclRecv of the film windows failed");
+                    if (r == 0 && err.empty()) {
+                        if (hipMemsetAsync(D.quilt, 0, nfloat * sizeof(float), D.st) != hipSuccess) fail("hipMemset(quilt) failed");
+                        for (int q = 0; q < n && err.empty(); ++q) {
+                            const auto &w = wins[(size_t) q];
+                            const float *win = q == 0 ? D.film : D.recv[(size_t) q];
+                            const uint32_t *ov = q == 0 ? D.ovf + 4 : D.recv_ov[(size_t) q];
+                            if (amvpt_film_accumulate(D.quilt, p.film_width, p.film_height, C, win, w[0], w[1], w[2], w[3], ov,
+                                                      ov_count[(size_t) q], D.st) != AMVPT_OK)
+                                fail(amvpt_last_error());
+                        }
+                    }
+                } else if (n > 1) {
+                    if (ncclReduce(D.film, D.film, nfloat, ncclFloat, ncclSum, 0, cache->comms[(size_t) r], D.st) != ncclSuccess)
+                        fail("ncclReduce failed");
+                }
+                if (D.st && hipStreamSynchronize(D.st) != hipSuccess) fail("hipStreamSynchronize failed");
+                /* -- develop / copy out on devices[0] -- */
+                if (r == 0 && err.empty()) {
+                    const float *frame = groups ? D.quilt : D.film;
                     if (raw) {
-                        if (hipMemcpy(out, film, nfloat * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
-                            fail("hipMemcpy(film) failed");
+                        if (hipMemcpy(out, frame, nfloat * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) fail("hipMemcpy(film) failed");
                     } else {
                         const uint32_t T = p.film_alpha ? 4u : 3u;
-                        if (hipMalloc(&dev_out, npx * T * sizeof(float)) != hipSuccess) fail("hipMalloc(out) failed");
-                        else if (amvpt_develop(film, dev_out, p.film_width, p.film_height, p.film_alpha, st) != AMVPT_OK)
+                        if (!grow(D.out, D.out_bytes, npx * T * sizeof(float))) fail("hipMalloc(out) failed");
+                        else if (amvpt_develop(frame, D.out, p.film_width, p.film_height, p.film_alpha, D.st) != AMVPT_OK)
                             fail(amvpt_last_error());
-                        else if (hipStreamSynchronize(st) != hipSuccess ||
-                                 hipMemcpy(out, dev_out, npx * T * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+                        else if (hipStreamSynchronize(D.st) != hipSuccess ||
+                                 hipMemcpy(out, D.out, npx * T * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
                             fail("develop / copy-out failed");
                     }
                 }
-                if (dev_out) (void) hipFree(dev_out);
-                if (film) (void) hipFree(film);
-                if (dsc) amvpt_scene_destroy(dsc);
-                if (st) (void) hipStreamDestroy(st);
             });
         }
         for (auto &t : threads) t.join();
         for (int r = 0; r < n; ++r)
-            if (!res[(size_t) r].error.empty()) throw std::runtime_error("device " + std::to_string(devices[r]) + ": " + res[(size_t) r].error);
+            if (!errors[(size_t) r].empty()) throw std::runtime_error("device " + std::to_string(devices[r]) + ": " + errors[(size_t) r]);
+        ++cache->renders;
         if (counters) {
             /* lane statistics sum over the shards; per-kernel and wall times: the slowest device */
-            amvpt_counters c = res[0].counters;
+            amvpt_counters c = cnt[0];
             for (int r = 1; r < n; ++r) {
-                const amvpt_counters &o = res[(size_t) r].counters;
+                const amvpt_counters &o = cnt[(size_t) r];
                 c.lanes += o.lanes; c.vertices += o.vertices; c.reuse_lanes += o.reuse_lanes;
                 c.visibility_rays += o.visibility_rays; c.view_splats += o.view_splats;
                 c.splat_fallback += o.splat_fallback; c.adaptive_lanes += o.adaptive_lanes;
                 c.shadow_rays += o.shadow_rays; c.nonfinite_samples += o.nonfinite_samples;
-                c.negative_samples += o.negative_samples;
+                c.negative_samples += o.negative_samples; c.pushed_paths += o.pushed_paths;
+                c.film_overflow += o.film_overflow;
                 c.total_ms = std::max(c.total_ms, o.total_ms);
                 c.kernel_ms_primary = std::max(c.kernel_ms_primary, o.kernel_ms_primary);
                 c.kernel_ms_bounce = std::max(c.kernel_ms_bounce, o.kernel_ms_bounce);

@@ -358,6 +358,7 @@ struct MeshStore { std::vector<float> pos, nrm, uv; std::vector<uint32_t> faces;
 
 } // namespace mi
 
+struct amvpt_multi_cache;   /* multi.cpp: communicators, per-device scenes and films of render_multi */
 struct amvpt_host_scene {
     std::shared_ptr<mi::Object> root;
     mi::IntegratorInfo integrator;
@@ -371,8 +372,12 @@ struct amvpt_host_scene {
     amvpt_scene *dev = nullptr;
     int dev_id = -1;
     std::vector<amvpt_view_desc> last_views;
-    ~amvpt_host_scene() { if (dev) amvpt_scene_destroy(dev); }
+    std::shared_ptr<amvpt_multi_cache> multi;
+    ~amvpt_host_scene() { multi.reset(); if (dev) amvpt_scene_destroy(dev); }
 };
+
+/* multi.cpp's cache slot on the host scene */
+std::shared_ptr<amvpt_multi_cache> &amvpt_host_multi_slot(amvpt_host_scene *s) { return s->multi; }
 
 namespace mi {
 

@@ -1654,6 +1654,13 @@ static oracle_exchange_fn g_exchange = nullptr;
 static void *g_exchange_ctx = nullptr;
 /* adaptive fill over a lane range: per pass, (local flagged-lane count) -> (prefix, total) */
 void oracle_set_exchange(oracle_exchange_fn fn, void *ctx) { g_exchange = fn; g_exchange_ctx = ctx; }
+/* the same over the runs of a lane rectangle (amvpt_run_exchange_fn of include/amvpt.h): per pass,
+ * (run lane begins, run flagged counts) -> (flagged lanes of the pass below each run, pass total) */
+typedef int (*oracle_run_exchange_fn)(void *ctx, uint32_t n_runs, const uint64_t *run_lane_begin,
+                                      const uint64_t *run_count, uint64_t *run_prefix, uint64_t *total);
+static oracle_run_exchange_fn g_run_exchange = nullptr;
+static void *g_run_exchange_ctx = nullptr;
+void oracle_set_run_exchange(oracle_run_exchange_fn fn, void *ctx) { g_run_exchange = fn; g_run_exchange_ctx = ctx; }
 
 struct oracle_stats { uint64_t lanes, vertices, reuse_lanes, visibility_rays, adaptive_lanes; double seconds; };
 
@@ -1663,9 +1670,35 @@ struct oracle_stats { uint64_t lanes, vertices, reuse_lanes, visibility_rays, ad
  * of pass `record_pass` (8 floats: pos.x, pos.y, r, g, b, alpha, weight, valid)
  * laid out [lane - lane_begin][view slot].  Returns 0 on success.
  */
+/* the lanes of a render: contiguous [lane_begin, lane_end), or (rect) the lanes of the quilt pixels
+ * [x0, x0 + w) x [y0, y0 + h) -- virtual index v -> lane, runs of w * spp_per_pass lanes per row */
+struct LaneMap {
+    bool rect = false;
+    uint32_t x0 = 0, y0 = 0, w = 0, h = 0;
+};
+static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views, const amvpt_params *params,
+                       uint64_t lane_begin, uint64_t lane_end, const LaneMap &lm, float *film, int n_threads,
+                       float *records, uint32_t record_pass, oracle_stats *stats);
+
 int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, const amvpt_params *params,
                   uint64_t lane_begin, uint64_t lane_end, float *film, int n_threads,
                   float *records, uint32_t record_pass, oracle_stats *stats) {
+    return render_core(sd, views, params, lane_begin, lane_end, LaneMap{}, film, n_threads, records, record_pass, stats);
+}
+
+/* the lanes of a pixel rectangle of the quilt (a view-group rank's share, amvpt_lane_set rect form) */
+int oracle_render_rect(const amvpt_scene_desc *sd, const amvpt_view_desc *views, const amvpt_params *params,
+                       uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float *film, int n_threads, oracle_stats *stats) {
+    LaneMap lm;
+    lm.rect = true;
+    lm.x0 = x0; lm.y0 = y0; lm.w = w; lm.h = h;
+    if ((uint64_t) x0 + w > params->film_width || (uint64_t) y0 + h > params->film_height) return 4;
+    return render_core(sd, views, params, 0, 0, lm, film, n_threads, nullptr, 0, stats);
+}
+
+static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views, const amvpt_params *params,
+                       uint64_t lane_begin, uint64_t lane_end, const LaneMap &lm, float *film, int n_threads,
+                       float *records, uint32_t record_pass, oracle_stats *stats) {
     auto t0 = std::chrono::steady_clock::now();
     Scene sc;
     if (!build_scene(sd, sc)) return 4;
@@ -1682,8 +1715,15 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
     uint32_t G = reuse ? group_size(P, true) : 1;
     uint32_t C = P.film_alpha ? 5 : 4;
     uint32_t W = P.film_width, H = P.film_height;
-    if (lane_end > L) lane_end = L;
+    if (lm.rect) { lane_begin = 0; lane_end = (uint64_t) lm.w * lm.h * spp_pp; }   /* virtual indices */
+    else if (lane_end > L) lane_end = L;
     if (lane_begin >= lane_end) lane_begin = lane_end;
+    const uint64_t run_len = (uint64_t) lm.w * spp_pp;
+    auto lane_of = [&](uint64_t v) -> uint64_t {
+        if (!lm.rect) return v;
+        const uint64_t r = v / run_len;
+        return ((uint64_t) (lm.y0 + r) * P.film_width + lm.x0) * spp_pp + (v - r * run_len);
+    };
     uint32_t log_spp = 0;
     while ((1u << log_spp) < spp_pp) ++log_spp;
     bool pow2 = (1u << log_spp) == spp_pp;
@@ -1692,8 +1732,9 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
     uint32_t sres_x = W / gx, sres_y = H / gy;
     uint32_t n_adapt = std::min(P.adaptive, G - 1);
     if (!is_mv && n_passes > 1) return 4; /* stock path: RNG state carried across passes (unsupported) */
-    const bool partial = lane_begin != 0 || lane_end != L;
-    if (n_adapt && partial && !g_exchange) return 4; /* adaptive needs the full frame or a count exchange */
+    const bool partial = lm.rect || lane_begin != 0 || lane_end != L;
+    if (n_adapt && partial && !(lm.rect ? (bool) g_run_exchange : (bool) g_exchange))
+        return 4; /* adaptive needs the full frame or a count exchange */
     if (n_threads <= 0) n_threads = (int) std::max(1u, std::thread::hardware_concurrency());
 
     std::atomic<uint64_t> a_vert{0}, a_reuse{0}, a_vis{0}, a_adapt{0};
@@ -1714,7 +1755,8 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
             uint64_t verts = 0;
             uint64_t b0 = lane_begin + span * tid / n_threads, b1 = lane_begin + span * (tid + 1) / n_threads;
             std::vector<SampleData> S(G);
-            for (uint64_t lane = b0; lane < b1; ++lane) {
+            for (uint64_t vi = b0; vi < b1; ++vi) {
+                const uint64_t lane = lane_of(vi);
                 uint32_t idx32 = (uint32_t) lane;
                 uint32_t pix = pow2 ? (idx32 >> log_spp) : (idx32 / spp_pp);
                 int py = (int) (pix / W);
@@ -1730,7 +1772,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
                 if (R.needs_ap) { R.ap.x = rng.next_1d(); R.ap.y = rng.next_1d(); }
                 V2 adj{fmadd(sample_pos.x, 1.f / (float) W, -0.f * (1.f / (float) W)),
                        fmadd(sample_pos.y, 1.f / (float) H, -0.f * (1.f / (float) H))};
-                float *rec = (records && pass == record_pass) ? records + (lane - lane_begin) * (size_t) G * 8 : nullptr;
+                float *rec = (records && pass == record_pass) ? records + (vi - lane_begin) * (size_t) G * 8 : nullptr;
                 if (!reuse) {
                     /* render_sample (mvpath_single.h:50-80) / SamplingIntegrator::render_sample */
                     uint32_t index;
@@ -1797,17 +1839,35 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
         if (n_adapt) {
             /* adaptive fill (mvpath_multi.h:79-115): compress + repeat, new sampler seeded (W, W) */
             std::vector<uint32_t> idx;
-            for (uint64_t l = lane_begin; l < lane_end; ++l)
-                if (amask[l]) for (uint32_t r = 0; r < n_adapt; ++r) idx.push_back((uint32_t) l);
+            std::vector<uint64_t> run_count(lm.rect ? lm.h : 1, 0);
+            for (uint64_t v = lane_begin; v < lane_end; ++v) {
+                const uint64_t l = lane_of(v);
+                if (amask[l]) {
+                    for (uint32_t r = 0; r < n_adapt; ++r) idx.push_back((uint32_t) l);
+                    run_count[lm.rect ? v / run_len : 0] += 1;
+                }
+            }
             uint64_t wf = idx.size();
-            /* lane-sharded frame: the fill's index space is the whole pass's compressed
-             * array, so ask the other ranges how many flagged lanes precede this one */
-            uint64_t prefix = 0, total = wf / n_adapt;
-            if (partial && g_exchange(g_exchange_ctx, wf / n_adapt, &prefix, &total) != 0) return 5;
+            /* sharded frame: the fill's index space is the whole pass's compressed array, so ask
+             * the other ranks how many flagged lanes precede each run of this one */
+            uint64_t total = wf / n_adapt;
+            std::vector<uint64_t> run_prefix(run_count.size(), 0);
+            if (lm.rect) {
+                std::vector<uint64_t> run_begin(lm.h);
+                for (uint32_t r = 0; r < lm.h; ++r) run_begin[r] = lane_of((uint64_t) r * run_len);
+                const uint32_t n_runs = lane_end > lane_begin ? lm.h : 0u;   /* an empty set still joins */
+                if (g_run_exchange(g_run_exchange_ctx, n_runs, run_begin.data(), run_count.data(), run_prefix.data(), &total) != 0)
+                    return 5;
+            } else if (partial) {
+                if (g_exchange(g_exchange_ctx, wf / n_adapt, &run_prefix[0], &total) != 0) return 5;
+            }
+            /* entry e of the local compressed list -> its index in the pass's compressed array */
+            std::vector<uint32_t> gidx;
+            for (size_t r = 0, e = 0; r < run_count.size(); ++r)
+                for (uint64_t k = 0; k < run_count[r]; ++k, ++e) gidx.push_back((uint32_t) (run_prefix[r] + k));
             a_adapt += wf;
             if (wf > 0) {
                 uint32_t sv = P.base_seed + (uint32_t) (total * n_adapt);
-                uint32_t jbase = (uint32_t) (prefix * n_adapt);
                 float adapt_w = 1.f / (float) (n_adapt + 1);
                 auto aworker = [&](int tid) {
                     Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, films[tid].data()};
@@ -1818,7 +1878,7 @@ int oracle_render(const amvpt_scene_desc *sd, const amvpt_view_desc *views, cons
                     uint64_t b0 = wf * tid / n_threads, b1 = wf * (tid + 1) / n_threads;
                     for (uint64_t j = b0; j < b1; ++j) {
                         uint32_t v0, v1;
-                        tea(sv, jbase + (uint32_t) j, 4, v0, v1);
+                        tea(sv, gidx[j / n_adapt] * n_adapt + (uint32_t) (j % n_adapt), 4, v0, v1);
                         PCG32 rng;
                         rng.seed(v0, v1);
                         uint32_t lane = idx[j];

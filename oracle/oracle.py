@@ -41,6 +41,10 @@ def lib():
                                     ctypes.c_uint32, ctypes.POINTER(OracleStats)]
         L.oracle_plan.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
         L.oracle_set_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
+        L.oracle_set_run_exchange.argtypes = [RunExchangeFn, ctypes.c_void_p]
+        L.oracle_render_rect.restype = ctypes.c_int
+        L.oracle_render_rect.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_uint32] * 4 + [
+            ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(OracleStats)]
         L.oracle_tea_float32.restype = ctypes.c_float
         L.oracle_tea_float64.restype = ctypes.c_double
         L.oracle_gaussian_eval.restype = ctypes.c_float
@@ -105,6 +109,49 @@ def set_exchange(fn):
             return 1
     _exchange_cb = ExchangeFn(cb)
     lib().oracle_set_exchange(_exchange_cb, None)
+
+
+RunExchangeFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64))
+_run_exchange_cb = None
+
+
+def set_run_exchange(fn):
+    """Adaptive fill over a lane rectangle: `fn(run_lane_begin, run_count) -> (run_prefix, total)` once per
+    pass (the amvpt_run_exchange_fn contract of include/amvpt.h)."""
+    global _run_exchange_cb
+    if fn is None:
+        _run_exchange_cb = None
+        lib().oracle_set_run_exchange(RunExchangeFn(), None)
+        return
+
+    def cb(_ctx, n, begins, counts, prefix, total):
+        try:
+            pre, tot = fn([int(begins[i]) for i in range(n)], [int(counts[i]) for i in range(n)])
+            for i in range(n):
+                prefix[i] = int(pre[i])
+            total[0] = int(tot)
+            return 0
+        except Exception:   # noqa: BLE001
+            return 1
+    _run_exchange_cb = RunExchangeFn(cb)
+    lib().oracle_set_run_exchange(_run_exchange_cb, None)
+
+
+def render_rect(scene_desc_ptr, views_ptr, params, rect, threads=0, film=None):
+    """Render the lanes of quilt pixels rect = (x0, y0, width, height) into a whole-quilt film."""
+    L = lib()
+    C = 5 if params.film_alpha else 4
+    if film is None:
+        film = np.zeros((params.film_height, params.film_width, C), dtype=np.float32)
+    st = OracleStats()
+    rc = L.oracle_render_rect(ctypes.cast(scene_desc_ptr, ctypes.c_void_p), ctypes.cast(views_ptr, ctypes.c_void_p),
+                              ctypes.addressof(params), *[int(v) for v in rect], film.ctypes.data, threads,
+                              ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError("oracle_render_rect failed (status %d)" % rc)
+    return film, st.as_dict()
 
 
 def render(scene_desc_ptr, views_ptr, params, lane_begin=0, lane_end=2 ** 64 - 1, threads=0,

@@ -115,7 +115,77 @@ def test_c5_light_field_array_whole_and_eight_shards(gpu_ready, amvpt_mod, oracl
     assert np.abs(summed - ofilm).max() <= 1e-5 * scale
 
 
-def test_c4_veach_eight_film_tile_shards(gpu_ready, amvpt_mod, oracle):
+def _rect_lanes(p, spp_pp, rect):
+    """Global lanes of a rectangle lane set in its virtual (lane) order (amvpt_lane_set rect form)."""
+    x0, y0, w, h = rect
+    ys = np.arange(y0, y0 + h, dtype=np.int64)[:, None, None]
+    xs = np.arange(x0, x0 + w, dtype=np.int64)[None, :, None]
+    ss = np.arange(spp_pp, dtype=np.int64)[None, None, :]
+    return ((ys * p.film_width + xs) * spp_pp + ss).reshape(-1)
+
+
+def test_c5_view_group_shards(gpu_ready, amvpt_mod, oracle):
+    """C5's view-group partition ("4 views per GPU"): 8 ranks each render the lanes of their
+    group's 4 tiles (amvpt_render_ex, rectangle lane set) into a film window of those tiles + a 4-px
+    border with an overflow list, adaptive 3 with the per-row count exchange.  Every rank's records are
+    bit-identical to the oracle's records of the same lanes, and the windows + overflow cells assembled
+    into the quilt equal the oracle frame."""
+    from amvpt import dist as adist
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=32, spp=16, gx=8, gy=4, reuse=4, adaptive=3)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    assert plan["group"] == 4 and plan["passes"] == 1
+    part = adist.view_group_partition(p, 4, 8)
+    assert part is not None
+    ofilm, orec, st = oracle.render(sd, vd, p, threads=16, record_pass=0)
+    assert st["adaptive_lanes"] > 0
+    dev = amvpt_mod.DeviceScene(sd)
+    cap = 1 << 16
+    runs = {}
+
+    def counting(r):
+        def fn(begins, counts):   # phase 1: learn every rank's per-run counts
+            runs[r] = (list(begins), list(counts))
+            return adist.exclusive_prefix(begins, counts, begins)
+        return fn
+
+    def exchange(begins, counts):   # phase 2: the all-gather's result
+        allb = sum((runs[r][0] for r in range(8)), [])
+        allc = sum((runs[r][1] for r in range(8)), [])
+        return adist.exclusive_prefix(allb, allc, begins)
+
+    for phase in (1, 2):
+        quilt = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+        overflow_cells = 0
+        for r, (rect, win) in enumerate(part):
+            x0, y0, w, h = win
+            film = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            ov = torch.zeros(4 * (cap + 1), dtype=torch.int32, device="cuda")
+            n = rect[2] * rect[3] * plan["spp_per_pass"]
+            rec = torch.zeros((n, 4, 8), dtype=torch.float32, device="cuda") if phase == 2 else None
+            cnt = amvpt_mod.Counters()
+            dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt_mod.LaneSet(0, 0, *rect), window=win,
+                          overflow_ptr=ov.data_ptr(), overflow_capacity=cap, counters=cnt,
+                          exchange=counting(r) if phase == 1 else exchange,
+                          records_ptr=rec.data_ptr() if rec is not None else None)
+            torch.cuda.synchronize()
+            assert cnt.lanes == n
+            idx, val = adist.overflow_entries(ov)
+            assert cnt.film_overflow == idx.numel()
+            overflow_cells += idx.numel()
+            quilt[y0:y0 + h, x0:x0 + w] += film
+            quilt.view(-1).index_add_(0, idx, val)
+            if phase == 2:
+                lanes = _rect_lanes(p, plan["spp_per_pass"], rect)
+                assert _records_match(rec.cpu().numpy(), orec[lanes]) == 1.0, r
+        if phase == 2:
+            got = quilt.cpu().numpy()
+            assert np.abs(got - ofilm).max() <= 1e-5 * np.abs(ofilm).max()
+            print("overflow cells over 8 ranks:", overflow_cells)
+
+
+def test_c4_veach_eight_film_tile_shards(def test_c4_veach_eight_film_tile_shards(gpu_ready, amvpt_mod, oracle):
     """C4 shape: the Veach-MIS 8-view frame (GGX plates, sphere lights, G = 8, sa_mis) split into the
     8 contiguous lane ranges (= bands of quilt rows) the 8-GPU run gives its ranks; every range's
     records match the oracle's and the 8 films sum to the oracle frame (the RCCL reduce)."""

@@ -25,7 +25,8 @@ def _torch():
     return torch
 
 
-def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records=True):
+def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records=True, flags=0):
+    """One frame through amvpt_render_ex (per-call options; records of pass 0 through the opts hook)."""
     torch = _torch()
     dev = amvpt_mod.DeviceScene(sd)
     C = 5 if p.film_alpha else 4
@@ -34,9 +35,8 @@ def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records
     rec = None
     if records:
         rec = torch.zeros((lane_end - lane_begin, plan["group"], 8), dtype=torch.float32, device="cuda")
-        dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, lane_begin, lane_end)
-    else:
-        dev.render(vd, p, film.data_ptr(), lane_begin, lane_end)
+    dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt_mod.LaneSet(lane_begin, lane_end, 0, 0, 0, 0), flags=flags,
+                  records_ptr=rec.data_ptr() if rec is not None else None)
     torch.cuda.synchronize()
     return film.cpu().numpy(), (rec.cpu().numpy() if rec is not None else None)
 
@@ -45,10 +45,10 @@ def _bit_equal(a, b):
     return (a == b) | (np.isnan(a) & np.isnan(b))
 
 
-def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0):
+def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0, flags=0):
     sd, vd, p = scene.describe(0, seed, spp)
     plan = oracle.plan(p)
-    gfilm, grec = _gpu_render(amvpt_mod, sd, vd, p, plan)
+    gfilm, grec = _gpu_render(amvpt_mod, sd, vd, p, plan, flags=flags)
     ofilm, orec, _ = oracle.render(sd, vd, p, threads=16, record_pass=0)
     eq = _bit_equal(grec, orec)
     match = eq.all(axis=(1, 2)).mean()
@@ -84,12 +84,11 @@ def test_mvpath_amvpt_mis_g8_two_passes(gpu_ready, amvpt_mod, oracle):
 
 
 @pytest.mark.parametrize("res,spp,kw", [(48, 16, dict()), (24, 32, dict(gx=4, gy=2, reuse=8))])
-def test_generic_kernels_on_diffuse_scene(gpu_ready, amvpt_mod, oracle, monkeypatch, res, spp, kw):
+def test_generic_kernels_on_diffuse_scene(gpu_ready, amvpt_mod, oracle, res, spp, kw):
     """The Cornell box is all-diffuse, so it normally runs the kDiff kernel instances;
-    AMVPT_NO_DIFFUSE_SPEC=1 forces the generic ones, which must agree just as well."""
-    monkeypatch.setenv("AMVPT_NO_DIFFUSE_SPEC", "1")
+    AMVPT_OPT_GENERIC_KERNELS (a per-call option) forces the generic ones, which must agree just as well."""
     s = amvpt_mod.load_file(CBOX, res=res, spp=spp, **kw)
-    _check(amvpt_mod, oracle, s)
+    _check(amvpt_mod, oracle, s, flags=amvpt_mod.OPT_GENERIC_KERNELS)
 
 
 def test_mvpath_reuse_without_mis(gpu_ready, amvpt_mod, oracle):
@@ -378,9 +377,9 @@ def test_veach_weighted_emitter_sampling(gpu_ready, amvpt_mod, oracle):
 
 
 @pytest.mark.parametrize("adaptive", [0, 2])
-def test_fused_suffix_matches_wavefront_suffix(gpu_ready, amvpt_mod, oracle, monkeypatch, adaptive):
+def test_fused_suffix_matches_wavefront_suffix(gpu_ready, amvpt_mod, oracle, adaptive):
     """k_suffix_fused (paths in registers, brute-force scenes) vs the per-depth k_extend / k_bounce
-    wavefronts (AMVPT_FUSE_SUFFIX=0) on the same lanes: records bit-identical, the same vertex and
+    wavefronts (AMVPT_OPT_WAVEFRONT_SUFFIX) on the same lanes: records bit-identical, the same vertex and
     shadow-ray counts, and each launch path actually taken (kernel launch counters)."""
     torch = _torch()
     s = amvpt_mod.load_file(CBOX, res=32, spp=32, gx=4, gy=2, reuse=8, adaptive=adaptive)
@@ -388,14 +387,14 @@ def test_fused_suffix_matches_wavefront_suffix(gpu_ready, amvpt_mod, oracle, mon
     plan = oracle.plan(p)
     out = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("AMVPT_FUSE_SUFFIX", fused)
+        flags = 0 if fused == "1" else amvpt_mod.OPT_WAVEFRONT_SUFFIX
         dev = amvpt_mod.DeviceScene(sd)
         film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
         rec = torch.zeros((plan["lanes"], plan["group"], 8), dtype=torch.float32, device="cuda")
-        dev.render_records(vd, p, film.data_ptr(), rec.data_ptr(), 0, 0, plan["lanes"])
+        dev.render_ex(vd, p, film.data_ptr(), flags=flags, records_ptr=rec.data_ptr())
         cnt = amvpt_mod.Counters()
         film2 = torch.zeros_like(film)
-        dev.render(vd, p, film2.data_ptr(), counters=cnt)
+        dev.render_ex(vd, p, film2.data_ptr(), counters=cnt, flags=flags)
         torch.cuda.synchronize()
         out[fused] = (rec.cpu().numpy(), film2.cpu().numpy(), cnt.as_dict())
     (r1, f1, c1), (r0, f0, c0) = out["1"], out["0"]

@@ -56,6 +56,105 @@ def _worker(rank, world, port, mode, out_dir, kw=None):
         dist.destroy_process_group()
 
 
+def _group_worker(rank, world, port, out_dir, kw):
+    """One rank of the view-group partition (C5's "4 views per GPU") on the CPU oracle: render the
+    lanes of this rank's tile rectangle with the per-run count exchange, cut the film into the rank's
+    window + overflow list exactly as amvpt_render_ex hands them over, and gather on rank 0."""
+    import sys
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import amvpt
+    from amvpt import dist as adist
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = amvpt.load_file(CBOX, **kw)
+        sd, vd, p = s.describe(0, 0, 0)
+        G = O.plan(p)["group"]
+        part = adist.view_group_partition(p, G, world)
+        assert part is not None
+        rect, win = part[rank]
+        O.set_run_exchange(adist.run_exchange())
+        full, st = O.render_rect(sd, vd, p, rect, threads=2)
+        O.set_run_exchange(None)
+        x0, y0, w, h = win
+        window = torch.from_numpy(np.ascontiguousarray(full[y0:y0 + h, x0:x0 + w]))
+        outside = full.copy()
+        outside[y0:y0 + h, x0:x0 + w] = 0
+        flat = outside.reshape(-1)
+        nz = np.flatnonzero(flat)
+        ov = np.zeros(4 * (len(nz) + 1), dtype=np.int32)
+        ov[0:2] = np.array([len(nz)], dtype=np.int64).view(np.int32)
+        e = ov[4:].reshape(-1, 4)
+        e[:, 0] = (nz & 0xffffffff).astype(np.uint32).view(np.int32)
+        e[:, 1] = (nz >> 32).astype(np.int32)
+        e[:, 2] = flat[nz].view(np.int32)
+        quilt = torch.zeros(full.shape, dtype=torch.float32)
+        out = adist.gather_windows(window, win, torch.from_numpy(ov), quilt, [q[1] for q in part], dst=0)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "film.npy"), out.numpy())
+            np.save(os.path.join(out_dir, "lanes.npy"), np.array([st["lanes"], st["adaptive_lanes"]]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_groups(world, kw):
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_group_worker, args=(world, _free_port(), d, kw), nprocs=world, join=True)
+        return np.load(os.path.join(d, "film.npy"))
+
+
+C5_SMALL = dict(res=16, spp=16, gx=8, gy=4, reuse=4, adaptive=3)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_view_group_partition_equals_single_process(oracle, amvpt_mod, world):
+    """C5's view-group partition (SURVEY 8(e)): each rank renders the lanes of its groups' tiles (an
+    8 x 4 grid of 16^2 views, groups of 4, adaptive 3, per-row count exchange); the gathered windows +
+    overflow cells equal the single-process frame."""
+    got = _run_groups(world, C5_SMALL)
+    s = amvpt_mod.load_file(CBOX, **C5_SMALL)
+    sd, vd, p = s.describe(0, 0, 0)
+    ref, _, st = oracle.render(sd, vd, p, threads=4)
+    assert st["adaptive_lanes"] > 0
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_view_group_partition_geometry(amvpt_mod):
+    """Tiles of each rank's groups form rectangles that tile the quilt; M (one group of 8) has none."""
+    from amvpt import dist as adist
+    s = amvpt_mod.load_file(CBOX, **C5_SMALL)
+    _, _, p = s.describe(0, 0, 0)
+    for world in (1, 2, 4, 8):
+        part = adist.view_group_partition(p, 4, world)
+        assert part is not None and len(part) == world
+        cover = np.zeros((p.film_height, p.film_width), dtype=np.int32)
+        for (x0, y0, w, h), (wx, wy, ww, wh) in part:
+            cover[y0:y0 + h, x0:x0 + w] += 1
+            assert wx <= x0 and wy <= y0 and wx + ww >= x0 + w and wy + wh >= y0 + h
+        assert (cover == 1).all()
+    assert adist.view_group_partition(p, 4, 3) is None           # 8 groups over 3 ranks
+    m = amvpt_mod.load_file(CBOX, res=16, spp=16, gx=4, gy=2, reuse=8)
+    assert adist.view_group_partition(m.describe(0, 0, 0)[2], 8, 2) is None
+
+
+def test_run_exchange_prefixes():
+    """The per-run prefix of the adaptive count exchange: flagged lanes of every run below it."""
+    from amvpt import dist as adist
+    begins = [0, 100, 200, 300]
+    counts = [3, 5, 7, 11]
+    pre, tot = adist.exclusive_prefix([300, 0, 200, 100], [11, 3, 7, 5], [100, 300])
+    assert pre == [3, 15] and tot == 26
+    fn = adist.run_exchange()
+    assert fn(begins, counts) == ([0, 3, 8, 15], 26)
+
+
 def _run(mode, world=2, kw=None):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
@@ -144,3 +243,30 @@ def test_balanced_shards_equalise_measured_cost():
     assert adist.balanced_shards(bounds, [1.0] * 4, align=256) == bounds
     with pytest.raises(ValueError):
         adist.balanced_shards(bounds, [1.0] * 3)
+
+
+def test_host_view_group_partition_matches_dist(amvpt_mod):
+    """The C++ host's view-group partition (amvpt_host_view_group_partition, used by render_multi) equals
+    amvpt.dist.view_group_partition (the bench's), including the configurations where neither applies."""
+    from amvpt import dist as adist
+    cases = [dict(C5_SMALL), dict(res=16, spp=16, gx=4, gy=2, reuse=4), dict(res=16, spp=16, gx=4, gy=2, reuse=2),
+             dict(res=16, spp=16, gx=4, gy=2, reuse=8), dict(res=16, spp=16, gx=3, gy=2, reuse=2)]
+    for kw in cases:
+        _, _, p = amvpt_mod.load_file(CBOX, **kw).describe(0, 0, 0)
+        from oracle import oracle as O
+        G = O.plan(p)["group"]
+        for world in (1, 2, 3, 4, 8):
+            py = adist.view_group_partition(p, G, world)
+            cc = [amvpt_mod.host_view_group_partition(p, r, world) for r in range(world)]
+            if py is None:
+                assert any(c is None for c in cc), (kw, world)   # render_multi then takes lane bands
+            else:
+                assert [(tuple(a), tuple(b)) for a, b in py] == cc, (kw, world)
+
+
+def test_render_multi_fails_fast_on_a_bad_device(amvpt_mod):
+    """a device list with an invalid id is an error before any device work starts (no thread
+    waits in a collective or an exchange)."""
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16)
+    with pytest.raises(RuntimeError, match="not visible"):
+        amvpt_mod.render_multi(s, [0, 99])

@@ -16,6 +16,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_revision as revision  # noqa: E402  (the stamp bench.py checks)
+
 
 def per_kernel(d, counter):
     acc = collections.defaultdict(lambda: [0, 0.0])
@@ -31,6 +34,7 @@ def per_kernel(d, counter):
 
 def main():
     fd, wd, out = sys.argv[1:4]
+    config = sys.argv[4] if len(sys.argv) > 4 else "M"
     f = per_kernel(fd, "FETCH_SIZE")
     w = per_kernel(wd, "WRITE_SIZE")
     res = {}
@@ -43,7 +47,8 @@ def main():
         write = sw * 1024 / max(nw, 1)
         res[k] = {"launches": max(nf, nw), "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
                   "hbm_bytes_per_launch": fetch + write}
-    json.dump({"source": [fd, wd], "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 wide-read), WRITE_SIZE KiB x1024",
+    json.dump({"source": [fd, wd], "config": config, "source_revision": revision(),
+               "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 wide-read), WRITE_SIZE KiB x1024",
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in res.items():
         print("%-70s %6d launches  %.3e B/launch (fetch %.3e, write %.3e)" % (

@@ -13,9 +13,13 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_revision as revision  # noqa: E402  (the stamp bench.py checks)
+
 
 def main():
     d, out = sys.argv[1], sys.argv[2]
+    config = sys.argv[3] if len(sys.argv) > 3 else "M"
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     ids = collections.defaultdict(set)
     for r in csv.DictReader(open(os.path.join(d, "pmc_counter_collection.csv"))):
@@ -24,7 +28,7 @@ def main():
             continue
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         ids[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
-    res = {"source": d, "peak_valu_ginst_s": 1228.8, "kernels": {}}
+    res = {"source": d, "config": config, "source_revision": revision(), "peak_valu_ginst_s": 1228.8, "kernels": {}}
     for k, c in acc.items():
         n = max(1, len(ids[k]))
         res["kernels"][k] = {"launches": n, "waves_per_launch": c["SQ_WAVES"] / n,
