@@ -172,6 +172,13 @@ typedef struct amvpt_params {
     /* MultiSensor layout: 0 grid (grid.cpp:268-297), 1 batch (batch.cpp:163-181:
      * a horizontal strip, grid_y = 1, index clamped before reverse_x) */
     uint32_t batch;
+    /* ABI 8: hdrfilm crop window (hdrfilm.cpp:245-291).  film_width / film_height above are the
+     * crop size (the ImageBlock and the lane space, mvpath.cpp:28-30,173-190); crop_offset is the
+     * ImageBlock's offset in the film (sample positions are film coordinates, ImageBlock::put
+     * subtracts it, imageblock.cpp:211,266,447) and full_width / full_height the film size (the
+     * quilt tile pitch of reprojected views is film->size() / grid, mvpath_multi.h:62).  Zeros: no crop. */
+    uint32_t crop_offset_x, crop_offset_y;
+    uint32_t full_width, full_height;
 } amvpt_params;
 
 /* Per-render counters (device-side lane statistics; SURVEY 8(d) byte model). */

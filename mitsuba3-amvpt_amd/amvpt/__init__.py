@@ -66,7 +66,8 @@ class Params(ctypes.Structure):
         "integrator", "max_depth", "rr_depth", "hide_emitters", "sa_reuse", "sa_mis", "fast_mis",
         "debug", "adaptive", "spp_pass_lim", "reuse_count", "spp", "seed", "base_seed", "n_views",
         "multisensor", "grid_x", "grid_y", "reverse_x", "reverse_y", "film_width", "film_height",
-        "film_alpha", "rfilter")] + [("rfilter_stddev", f32), ("batch", u32)]
+        "film_alpha", "rfilter")] + [("rfilter_stddev", f32), ("batch", u32), ("crop_offset_x", u32),
+                                      ("crop_offset_y", u32), ("full_width", u32), ("full_height", u32)]
 
 
 class Counters(ctypes.Structure):

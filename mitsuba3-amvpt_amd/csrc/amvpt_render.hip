@@ -99,6 +99,11 @@ struct KParams {
     uint32_t *overflow;
     uint64_t ov_cap;
     float inv_w, inv_h;
+    /* hdrfilm crop window: pixel offset of the ImageBlock in the film (lane pixels and sample
+     * positions are film coordinates), the sample_ray_idx offsets -offset / crop_size
+     * (mvpath_multi.h:12-16), and ImageBlock::put's non-coalesced shift (int) -offset - .5f */
+    uint32_t off_x, off_y;
+    float adj_ox, adj_oy, nc_ox, nc_oy;
     float adapt_w;
     FilterCoeffs filt;
     uint64_t chunk_begin;
@@ -676,7 +681,7 @@ AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float 
  * (measured: splat 206 -> 187 ms at config M; rs = ww, or % 32 in {1, 8, 17, 24}: 200-207 ms).
  * The 112-cell width leaves room for the padding (5 blocks per CU either way). */
 /* measurement-only attribution builds (wrong images): 1 skips the LDS adds, 2 the flush's
- * film atomics, 4 the filter weights */
+ * film atomics, 4 the filter weights, 8 turns the LDS atomic adds into plain stores */
 #ifndef AMVPT_ATTR_SKIP
 #define AMVPT_ATTR_SKIP 0
 #endif
@@ -765,15 +770,16 @@ AD Foot footprint(const KParams &P, float px, float py, bool coalesce) {
     Foot f;
     const int W = (int) P.W, H = (int) P.H;
     if (P.box) {
-        int ix = (int) floorf(px), iy = (int) floorf(py);
+        /* imageblock.cpp:211: floor(pos) - offset */
+        int ix = (int) floorf(px) - (int) P.off_x, iy = (int) floorf(py) - (int) P.off_y;
         f.ok = (uint32_t) ix < (uint32_t) W && (uint32_t) iy < (uint32_t) H;
         f.x0 = ix; f.y0 = iy; f.nx = f.ny = 1; f.rx = f.ry = 0.f;
         return f;
     }
     const float radius = P.filt.radius;
     if (!coalesce) {
-        /* non-coalesced method (imageblock.cpp:265-427) */
-        float pfx = px + (0.f - 0.5f), pfy = py + (0.f - 0.5f);
+        /* non-coalesced method (imageblock.cpp:265-427): pos + ((int) border - offset - .5f) */
+        float pfx = px + P.nc_ox, pfy = py + P.nc_oy;
         int p0x = max((int) ceilf(pfx - radius), 0), p0y = max((int) ceilf(pfy - radius), 0);
         int p1x = min((int) floorf(pfx + radius), W - 1), p1y = min((int) floorf(pfy + radius), H - 1);
         f.ok = (uint32_t) p0x <= (uint32_t) p1x && (uint32_t) p0y <= (uint32_t) p1y;
@@ -784,13 +790,14 @@ AD Foot footprint(const KParams &P, float px, float py, bool coalesce) {
         f.ry = (float) (uint32_t) p0y - pfy;
         return f;
     }
-    /* coalesced method (imageblock.cpp:433-558): count = 2n+1 cells from floor(pos) - n */
+    /* coalesced method (imageblock.cpp:433-558): count = 2n+1 cells from floor(pos) - n, minus the
+     * block offset; weights are evaluated at ((pix + .5) - pos) + xs in film coordinates */
     const int n = (int) ceilf(radius - .5f), count = 2 * n + 1;
-    int pix = (int) floorf(px) - n, piy = (int) floorf(py) - n;
+    const int gx0 = (int) floorf(px) - n, gy0 = (int) floorf(py) - n;
+    f.rx = ((float) gx0 + .5f) - px;
+    f.ry = ((float) gy0 + .5f) - py;
+    const int pix = gx0 - (int) P.off_x, piy = gy0 - (int) P.off_y;
     int sx = max(0, -pix), sy = max(0, -piy);
-    /* weights are evaluated at ((pix + .5) - pos) + xs, xs counted from pix */
-    f.rx = ((float) pix + .5f) - px;
-    f.ry = ((float) piy + .5f) - py;
     f.x0 = pix; f.y0 = piy;
     f.nx = min(count, W - pix);
     f.ny = min(count, H - piy);
@@ -818,7 +825,10 @@ AD void lds_add64(long long *p, long long v) {
     (void) __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(p), (unsigned long long) v, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-AD void win_add(double *p, float x) { lds_add64(p, (double) x); }
+AD void win_add(double *p, float x) {
+    if (AMVPT_ATTR_SKIP & 8) *p = (double) x;   /* attribution: a plain LDS store instead of ds_add_f64 */
+    else lds_add64(p, (double) x);
+}
 AD void win_add(float *p, float x) {
     (void) __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1397,11 +1407,12 @@ AD uint32_t path_seq(const KParams &P, const Bufs &B, uint32_t slot) {
     return v1;
 }
 
+/* film pixel of a lane (mvpath.cpp:173-190: pixel of the crop + crop_offset) */
 AD void lane_pixel(const KParams &P, uint32_t lane, int &px, int &py) {
     uint32_t pix = P.pow2 ? (lane >> P.log_spp) : (lane / P.spp_pp);
     uint32_t y = pix / P.W;
-    py = (int) y;
-    px = (int) (pix - P.W * y);
+    py = (int) (y + P.off_y);
+    px = (int) (pix - P.W * y + P.off_x);
 }
 
 AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P, const DView *V, Bufs B) {
@@ -1422,7 +1433,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
         float apx = .5f, apy = .5f;
         if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
         uint32_t index;
-        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index, apx, apy);
+        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, P.adj_ox), fmadd(sy, P.inv_h, P.adj_oy), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
         s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
         s.prev_p = mk(0.f, 0.f, 0.f);
@@ -1473,7 +1484,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
         Pcg rng;
         rng.seed(v0, v1);
         uint32_t index;
-        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f), index, apx, apy);
+        s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, P.adj_ox), fmadd(sy, P.inv_h, P.adj_oy), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
         s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
         s.prev_p = mk(0.f, 0.f, 0.f);
@@ -1840,7 +1851,7 @@ AD PrimRay primary_raygen(const KParams &P, const DView *V, uint32_t i) {
     r.sy = (float) py + jy;
     r.apx = r.apy = .5f;   /* aperture sample: raygen and every view's sample_surface */
     if (P.needs_ap) { r.apx = r.rng.next_1d(); r.apy = r.rng.next_1d(); }
-    r.ray = sample_ray_idx(P, V, fmadd(r.sx, P.inv_w, -0.f), fmadd(r.sy, P.inv_h, -0.f), r.p_idx, r.apx, r.apy);
+    r.ray = sample_ray_idx(P, V, fmadd(r.sx, P.inv_w, P.adj_ox), fmadd(r.sy, P.inv_h, P.adj_oy), r.p_idx, r.apx, r.apy);
     return r;
 }
 /*
@@ -2543,7 +2554,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         sx = (float) px + jx;
         sy = (float) py + jy;
         if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
-        p_idx = sensor_index(P, fmadd(sx, P.inv_w, -0.f), fmadd(sy, P.inv_h, -0.f));
+        p_idx = sensor_index(P, fmadd(sx, P.inv_w, P.adj_ox), fmadd(sy, P.inv_h, P.adj_oy));
     }
     const float *const vw = reinterpret_cast<const float *>(B.vrec);
     const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
@@ -3112,13 +3123,20 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         P.needs_ap |= views[v].type == AMVPT_CAMERA_THINLENS ? 1u : 0u;
     P.gx = Pp.grid_x ? Pp.grid_x : 1; P.gy = Pp.grid_y ? Pp.grid_y : 1;
     P.rev_x = Pp.reverse_x; P.rev_y = Pp.reverse_y;
-    P.sres_x = P.W / P.gx; P.sres_y = P.H / P.gy;
+    /* quilt tile pitch of reprojected views: film->size() / grid (mvpath_multi.h:62), the full film */
+    const uint32_t fullW = Pp.full_width ? Pp.full_width : P.W, fullH = Pp.full_height ? Pp.full_height : P.H;
+    P.sres_x = fullW / P.gx; P.sres_y = fullH / P.gy;
     P.box = Pp.rfilter == AMVPT_RFILTER_BOX;
     P.coalesce_single = spp_pp >= 4;
     P.path_box_pos = (!is_mv && P.box) ? 1 : 0;
     P.is_mvpath = is_mv;
     P.inv_w = 1.f / (float) P.W;
     P.inv_h = 1.f / (float) P.H;
+    P.off_x = Pp.crop_offset_x; P.off_y = Pp.crop_offset_y;
+    P.adj_ox = -(float) P.off_x * P.inv_w;   /* -ScalarVector2f(crop_offset) * scale */
+    P.adj_oy = -(float) P.off_y * P.inv_h;
+    P.nc_ox = (float) (-(int) P.off_x) - .5f;
+    P.nc_oy = (float) (-(int) P.off_y) - .5f;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = trav;
     P.win_rs = K.win_rs;

@@ -220,14 +220,15 @@ template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const
                     const uint32_t pi = first + i;
                     const DPrim p = load_uniform(sc.gprims, pi);
                     float t, u, v;
-                    if (prim_hit_u(p, ufirst(p.type), ray, t, u, v)) {
-                        const uint32_t orig = ufirst(p.pad);
-                        if (t < best.t || (t == best.t && orig < best_orig)) {
-                            best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
-                            best_orig = orig;
-                            tmax_box = t;
-                        }
-                    }
+                    const bool h = prim_hit_u(p, ufirst(p.type), ray, t, u, v);
+                    const uint32_t orig = ufirst(p.pad);
+                    const bool better = h && (t < best.t || (t == best.t && orig < best_orig));
+                    best.t = better ? t : best.t;
+                    best.u = better ? u : best.u;
+                    best.v = better ? v : best.v;
+                    best.prim = better ? (int32_t) pi : best.prim;
+                    best_orig = better ? orig : best_orig;
+                    tmax_box = better ? t : tmax_box;
                 }
             }
             node = (enter && !count) ? node + 1 : skip;
@@ -419,15 +420,17 @@ template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray
 }
 
 /* closest-hit update of the brute-force walks: (t, scene-order index) as trace_closest */
+/* branch-free: the update is a select per field (no exec-mask save / restore per primitive) */
 template <bool kSph> AD void brute_test(const DPrim &p, uint32_t pi, const Ray &ray, Hit &best, uint32_t &best_orig) {
     float t, u, v;
-    if (prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v)) {
-        const uint32_t orig = ufirst(p.pad);
-        if (t < best.t || (t == best.t && orig < best_orig)) {
-            best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
-            best_orig = orig;
-        }
-    }
+    const bool h = prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v);
+    const uint32_t orig = ufirst(p.pad);
+    const bool better = h && (t < best.t || (t == best.t && orig < best_orig));
+    best.t = better ? t : best.t;
+    best.u = better ? u : best.u;
+    best.v = better ? v : best.v;
+    best.prim = better ? (int32_t) pi : best.prim;
+    best_orig = better ? orig : best_orig;
 }
 /* Two records in flight (a, b), each reloaded in place right after its own test: the next
  * record's scalar load overlaps the current test and no record is copied between registers
@@ -456,10 +459,15 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
     const uint32_t last = np - 1u;
     DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
     for (uint32_t pi = 0; pi < np; pi += 2) {
+        /* branch-free: every lane tests (the wave runs the test anyway while any lane is open) */
         float t, u, v;
-        if (!found) found = prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
+        const bool ha = prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
+        found = found || ha;
         a = load_uniform(sc.gprims, min(pi + 2u, last));
-        if (pi + 1 < np && !found) found = prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
+        if (pi + 1 < np) {
+            const bool hb = prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
+            found = found || hb;
+        }
         b = load_uniform(sc.gprims, min(pi + 3u, last));
         if (!wave_any(!found)) break;
     }

@@ -85,6 +85,8 @@ double parse_fov(const Properties &props, double aspect) {
 
 struct FilmInfo {
     uint32_t w = 768, h = 576;
+    uint32_t cw = 768, ch = 576, cx = 0, cy = 0;   /* crop window (film.cpp:16-27; Film::set_size resets it) */
+    void reset_crop() { cw = w; ch = h; cx = cy = 0; }
     bool alpha = false;
     uint32_t rfilter = AMVPT_RFILTER_GAUSSIAN;
     float stddev = 0.5f;
@@ -95,9 +97,15 @@ static FilmInfo make_film(const Properties &p) {
     FilmInfo f;
     f.w = (uint32_t) p.get_int("width", 768);
     f.h = (uint32_t) p.get_int("height", 576);
-    if ((uint32_t) p.get_int("crop_width", f.w) != f.w || (uint32_t) p.get_int("crop_height", f.h) != f.h ||
-        p.get_int("crop_offset_x", 0) != 0 || p.get_int("crop_offset_y", 0) != 0)
-        Throw("hdrfilm: crop windows are not implemented");
+    /* Film ctor (film.cpp:16-27) + set_crop_window (film.cpp:91-100) */
+    f.cw = (uint32_t) p.get_int("crop_width", f.w);
+    f.ch = (uint32_t) p.get_int("crop_height", f.h);
+    f.cx = (uint32_t) p.get_int("crop_offset_x", 0);
+    f.cy = (uint32_t) p.get_int("crop_offset_y", 0);
+    if ((uint64_t) f.cx + f.cw > f.w || (uint64_t) f.cy + f.ch > f.h)
+        Throw("Invalid crop window specification: crop_offset(" + std::to_string(f.cx) + ", " + std::to_string(f.cy) +
+              ") + crop_size(" + std::to_string(f.cw) + ", " + std::to_string(f.ch) + ") > size(" +
+              std::to_string(f.w) + ", " + std::to_string(f.h) + ")");
     if (p.get_bool("sample_border", false)) Throw("hdrfilm: sample_border is not implemented");
     std::string pf = lower(p.get_string("pixel_format", "rgb"));
     if (pf == "rgb") f.alpha = false;
@@ -158,9 +166,12 @@ static void sensor_parts(const Properties &p, FilmInfo &film, SamplerInfo &samp)
 
 static void store3x4(const Mat4 &m, float *out16) { m.store(out16); }
 
-/* PerspectiveCamera ctor + update_camera_transforms (perspective.cpp:140-203) for a film of size (w,h) */
+/* PerspectiveCamera ctor + update_camera_transforms (perspective.cpp:140-203) for a film of size (w,h)
+ * with the crop window (cw, ch) at (cx, cy) (0 / 0: the whole film) */
 static amvpt_view_desc make_perspective_view(const Properties &p, const Transform4f &to_world, uint32_t w, uint32_t h,
-                                             double fov_x_override, bool use_override, float lens_shift) {
+                                             double fov_x_override, bool use_override, float lens_shift,
+                                             uint32_t cw = 0, uint32_t ch = 0, uint32_t cx = 0, uint32_t cy = 0) {
+    if (!cw) { cw = w; ch = h; cx = cy = 0; }
     amvpt_view_desc v;
     std::memset(&v, 0, sizeof(v));
     std::string t = lower(p.plugin);
@@ -172,8 +183,8 @@ static amvpt_view_desc make_perspective_view(const Properties &p, const Transfor
     if (near_clip >= far_clip) Throw("The 'near_clip' parameter must be smaller than 'far_clip'.");
     if (to_world.has_scale()) Throw("Scale factors in the camera-to-world transformation are not allowed!");
     float x_fov = use_override ? (float) fov_x_override : (float) parse_fov(p, (double) w / (double) h);
-    int size[2] = {(int) w, (int) h}, off[2] = {0, 0};
-    Transform4f c2s = perspective_projection(size, size, off, x_fov, near_clip, far_clip);
+    int size[2] = {(int) w, (int) h}, crop[2] = {(int) cw, (int) ch}, off[2] = {(int) cx, (int) cy};
+    Transform4f c2s = perspective_projection(size, crop, off, x_fov, near_clip, far_clip);
     c2s.matrix.m[0][2] += lens_shift;
     c2s.inverse_transpose = c2s.matrix.inverse().transpose();
     Transform4f s2c = c2s.inverse();
@@ -187,11 +198,11 @@ static amvpt_view_desc make_perspective_view(const Properties &p, const Transfor
     c2s.matrix.store(v.camera_to_sample);
     v.near_clip = near_clip;
     v.far_clip = far_clip;
-    v.resolution[0] = (float) w;
-    v.resolution[1] = (float) h;
+    v.resolution[0] = (float) cw;   /* m_resolution = film->crop_size() (sensor.cpp:69) */
+    v.resolution[1] = (float) ch;
     float ppx = (float) p.get_float("principal_point_offset_x", 0.0), ppy = (float) p.get_float("principal_point_offset_y", 0.0);
-    v.pp_offset[0] = (float) w * ppx / (float) w;
-    v.pp_offset[1] = (float) h * ppy / (float) h;
+    v.pp_offset[0] = (float) w * ppx / (float) cw;   /* film.size * principal_point_offset / crop_size */
+    v.pp_offset[1] = (float) h * ppy / (float) ch;
     v.focus_distance = (float) p.get_float("focus_distance", far_clip);
     v.aperture_radius = (float) p.get_float("aperture_radius", 0.0);
     if (v.type == AMVPT_CAMERA_THINLENS) {
@@ -220,7 +231,8 @@ static SensorInfo make_sensor(const Object &o) {
     Transform4f to_world = p.get_transform("to_world");
     if (t == "perspective" || t == "thinlens") {
         s.views.push_back(make_perspective_view(p, to_world, s.film.w, s.film.h, 0.0, false,
-                                                (float) p.get_float("lens_shift", 0.0)));
+                                                (float) p.get_float("lens_shift", 0.0), s.film.cw, s.film.ch, s.film.cx,
+                                                s.film.cy));
         return s;
     }
     if (t == "batch") {
@@ -341,6 +353,7 @@ static SensorInfo make_sensor(const Object &o) {
     }
     s.film.w = res_x;
     s.film.h = res_y;
+    s.film.reset_crop();   /* m_film->set_size(m_film_res) resets the crop window (grid.cpp:230, film.cpp:102-106) */
     return s;
 }
 
@@ -674,8 +687,12 @@ static amvpt_params params_for(const amvpt_host_scene &S, const SensorInfo &sn, 
     p.reverse_x = sn.rev_x;
     p.batch = sn.batch ? 1u : 0u;
     p.reverse_y = sn.rev_y;
-    p.film_width = sn.film.w;
-    p.film_height = sn.film.h;
+    p.film_width = sn.film.cw;    /* the ImageBlock / lane space: the crop (mvpath.cpp:28) */
+    p.film_height = sn.film.ch;
+    p.crop_offset_x = sn.film.cx;
+    p.crop_offset_y = sn.film.cy;
+    p.full_width = sn.film.w;
+    p.full_height = sn.film.h;
     p.film_alpha = sn.film.alpha;
     p.rfilter = sn.film.rfilter;
     p.rfilter_stddev = sn.film.stddev;
@@ -754,8 +771,8 @@ int amvpt_host_film_info(amvpt_host_scene *s, uint32_t si, uint32_t *w, uint32_t
     return guarded([&] {
         if (!s || si >= s->sensors.size()) throw std::runtime_error("Scene::render(): sensor index out of bounds!");
         const mi::SensorInfo &sn = s->sensors[si];
-        if (w) *w = sn.film.w;
-        if (h) *h = sn.film.h;
+        if (w) *w = sn.film.cw;   /* develop() returns the crop (hdrfilm.cpp:304-418) */
+        if (h) *h = sn.film.ch;
         if (c) *c = sn.film.alpha ? 4u : 3u;
         if (spp) *spp = sn.sampler.sample_count;
         return 0;

@@ -379,7 +379,8 @@ std::shared_ptr<Object> load_scene_string(const std::string &xml, const std::map
     for (auto &c : root->children)
         if (c->tag == "default") {
             const std::string *k = c->attr("name"), *v = c->attr("value");
-            if (k && v && !L.params.count(*k)) L.params[*k] = *v;
+            /* values may use earlier parameters ($name is substituted in every attribute, xml.cpp) */
+            if (k && v && !L.params.count(*k)) L.params[*k] = L.sub(*v);
         }
     return L.object(*root);
 }

@@ -1036,10 +1036,12 @@ struct Film {
     bool box;
     Gaussian g;
     float *data;
+    int ox = 0, oy = 0;   /* ImageBlock offset (the hdrfilm crop offset, mvpath.cpp:168) */
     void put(V2 pos, const float *values, bool active, bool coalesce) const {
         if (!active) return;
         if (box) {
-            int px = (int) std::floor(pos.x), py = (int) std::floor(pos.y);
+            /* imageblock.cpp:211: floor(pos) - offset */
+            int px = (int) std::floor(pos.x) - ox, py = (int) std::floor(pos.y) - oy;
             uint32_t ux = (uint32_t) px, uy = (uint32_t) py;
             if (!(ux < W && uy < H)) return;
             float *ptr = data + ((size_t) uy * W + ux) * C;
@@ -1048,8 +1050,8 @@ struct Film {
         }
         float radius = g.radius;
         if (!coalesce) {
-            /* imageblock.cpp:265-427 (recorded-loop form 1.2) */
-            V2 pos_f{pos.x + (0.f - 0.5f), pos.y + (0.f - 0.5f)};
+            /* imageblock.cpp:265-427 (recorded-loop form 1.2): pos + ((int) border - offset - .5f) */
+            V2 pos_f{pos.x + ((float) (-ox) - 0.5f), pos.y + ((float) (-oy) - 0.5f)};
             V2 pos_0_f{pos_f.x - radius, pos_f.y - radius}, pos_1_f{pos_f.x + radius, pos_f.y + radius};
             int p0x = std::max((int) std::ceil(pos_0_f.x), 0), p0y = std::max((int) std::ceil(pos_0_f.y), 0);
             int p1x = std::min((int) std::floor(pos_1_f.x), (int) W - 1), p1y = std::min((int) std::floor(pos_1_f.y), (int) H - 1);
@@ -1074,7 +1076,7 @@ struct Film {
         /* coalesced (imageblock.cpp:433-558, recorded-loop form 2.2) */
         uint32_t n = (uint32_t) std::ceil(radius - .5f), count = 2 * n + 1;
         int pix = (int) std::floor(pos.x) - (int) n, piy = (int) std::floor(pos.y) - (int) n;
-        uint32_t x = (uint32_t) pix, y = (uint32_t) piy;
+        uint32_t x = (uint32_t) (pix - ox), y = (uint32_t) (piy - oy);   /* pos_i_local (imageblock.cpp:447) */
         V2 rel_f{((float) pix + .5f) - pos.x, ((float) piy + .5f) - pos.y};
         for (uint32_t ys = 0; ys < count; ++ys) {
             float wy = g.eval(rel_f.y + (float) ys);
@@ -1729,7 +1731,13 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
     bool pow2 = (1u << log_spp) == spp_pp;
     bool coalesce_single = spp_pp >= 4;
     uint32_t gx = P.grid_x ? P.grid_x : 1, gy = P.grid_y ? P.grid_y : 1;
-    uint32_t sres_x = W / gx, sres_y = H / gy;
+    /* tile pitch of reprojected views: film->size() / grid (mvpath_multi.h:62), the full film */
+    const uint32_t fullW = P.full_width ? P.full_width : W, fullH = P.full_height ? P.full_height : H;
+    uint32_t sres_x = fullW / gx, sres_y = fullH / gy;
+    const int ox = (int) P.crop_offset_x, oy = (int) P.crop_offset_y;
+    /* render_multisample / render_sample: scale = 1 / crop_size, offset = -crop_offset * scale */
+    const float scale_x = 1.f / (float) W, scale_y = 1.f / (float) H;
+    const float off_x = -(float) ox * scale_x, off_y = -(float) oy * scale_y;
     uint32_t n_adapt = std::min(P.adaptive, G - 1);
     if (!is_mv && n_passes > 1) return 4; /* stock path: RNG state carried across passes (unsupported) */
     const bool partial = lm.rect || lane_begin != 0 || lane_end != L;
@@ -1748,7 +1756,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
         auto worker = [&](int tid) {
             std::vector<float> &tf = films[tid];
             if (tf.empty()) tf.assign((size_t) W * H * C, 0.f);
-            Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, tf.data()};
+            Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, tf.data(), ox, oy};
             film.g.init(P.rfilter_stddev);
             Renderer R(sc, views, P);
             R.G = G;
@@ -1761,6 +1769,8 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                 uint32_t pix = pow2 ? (idx32 >> log_spp) : (idx32 / spp_pp);
                 int py = (int) (pix / W);
                 int px = (int) (pix - W * (uint32_t) py);
+                px += ox;   /* pos += film->crop_offset() (mvpath.cpp:190) */
+                py += oy;
                 uint32_t v0, v1;
                 tea(seed_value, idx32, 4, v0, v1);
                 PCG32 rng;
@@ -1770,8 +1780,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                 V2 sample_pos{(float) px + jit.x, (float) py + jit.y};
                 R.ap = V2{.5f, .5f};
                 if (R.needs_ap) { R.ap.x = rng.next_1d(); R.ap.y = rng.next_1d(); }
-                V2 adj{fmadd(sample_pos.x, 1.f / (float) W, -0.f * (1.f / (float) W)),
-                       fmadd(sample_pos.y, 1.f / (float) H, -0.f * (1.f / (float) H))};
+                V2 adj{fmadd(sample_pos.x, scale_x, off_x), fmadd(sample_pos.y, scale_y, off_y)};
                 float *rec = (records && pass == record_pass) ? records + (vi - lane_begin) * (size_t) G * 8 : nullptr;
                 if (!reuse) {
                     /* render_sample (mvpath_single.h:50-80) / SamplingIntegrator::render_sample */
@@ -1870,7 +1879,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                 uint32_t sv = P.base_seed + (uint32_t) (total * n_adapt);
                 float adapt_w = 1.f / (float) (n_adapt + 1);
                 auto aworker = [&](int tid) {
-                    Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, films[tid].data()};
+                    Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, films[tid].data(), ox, oy};
                     film.g.init(P.rfilter_stddev);
                     Renderer R(sc, views, P);
                     R.G = G;
@@ -1884,8 +1893,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                         uint32_t lane = idx[j];
                         V2 sample_pos{spos[2 * lane], spos[2 * lane + 1]};
                         R.ap = V2{sap[2 * lane], sap[2 * lane + 1]};   /* nested_gather(aperture_sample, idx) */
-                        V2 adj{fmadd(sample_pos.x, 1.f / (float) W, -0.f * (1.f / (float) W)),
-                               fmadd(sample_pos.y, 1.f / (float) H, -0.f * (1.f / (float) H))};
+                        V2 adj{fmadd(sample_pos.x, scale_x, off_x), fmadd(sample_pos.y, scale_y, off_y)};
                         uint32_t index;
                         Ray ray = R.sample_ray_idx(adj, index);
                         auto [spec, valid] = R.sample_single(rng, ray, verts);
@@ -1913,6 +1921,37 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
         stats->adaptive_lanes = a_adapt;
         stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
+    return 0;
+}
+
+/*
+ * Test hook (the unbiasedness gate's geometric edge mask): the primary hit through the centre of every
+ * quilt pixel -- sample_ray_idx at (x + .5, y + .5) / quilt size, closest hit -- as 8 floats per
+ * pixel: shape index (-1 for a miss), geometric normal, hit point, view index.  Scene geometry only;
+ * no sampling.
+ */
+int oracle_primary_hits(const amvpt_scene_desc *sd, const amvpt_view_desc *views, const amvpt_params *params,
+                        float *out) {
+    Scene sc;
+    if (!build_scene(sd, sc)) return 4;
+    const amvpt_params P = *params;
+    Renderer R(sc, views, P);
+    const uint32_t W = P.film_width, H = P.film_height;
+    const float sx = 1.f / (float) W, sy = 1.f / (float) H;
+    const float ox = -(float) P.crop_offset_x * sx, oy = -(float) P.crop_offset_y * sy;
+    for (uint32_t y = 0; y < H; ++y)
+        for (uint32_t x = 0; x < W; ++x) {
+            /* crop pixel (x, y) = film pixel + crop offset, mapped as render_sample maps it */
+            const V2 adj{fmadd((float) (x + P.crop_offset_x) + .5f, sx, ox), fmadd((float) (y + P.crop_offset_y) + .5f, sy, oy)};
+            uint32_t index = 0;
+            const Ray ray = R.sample_ray_idx(adj, index);
+            const SI si = intersect(sc, ray);
+            float *o = out + ((size_t) y * W + x) * 8;
+            o[0] = si.valid() ? (float) si.shape : -1.f;
+            o[1] = si.n.x; o[2] = si.n.y; o[3] = si.n.z;
+            o[4] = si.p.x; o[5] = si.p.y; o[6] = si.p.z;
+            o[7] = (float) index;
+        }
     return 0;
 }
 

@@ -42,6 +42,8 @@ def lib():
         L.oracle_plan.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
         L.oracle_set_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.oracle_set_run_exchange.argtypes = [RunExchangeFn, ctypes.c_void_p]
+        L.oracle_primary_hits.restype = ctypes.c_int
+        L.oracle_primary_hits.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_render_rect.restype = ctypes.c_int
         L.oracle_render_rect.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_uint32] * 4 + [
             ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(OracleStats)]
@@ -194,3 +196,14 @@ def develop(film, alpha=False):
     w = film[..., -1:]
     n = 4 if alpha else 3
     return film[..., :n] / np.where(w == 0, 1.0, w)
+
+
+def primary_hits(scene_desc_ptr, views_ptr, params):
+    """(H, W, 8) float32: primary hit through each quilt pixel centre -- shape index (-1: miss), geometric
+    normal, hit point, view index (scene geometry only; the unbiasedness gate's edge mask)."""
+    out = np.zeros((params.film_height, params.film_width, 8), dtype=np.float32)
+    rc = lib().oracle_primary_hits(ctypes.cast(scene_desc_ptr, ctypes.c_void_p), ctypes.cast(views_ptr, ctypes.c_void_p),
+                                   ctypes.addressof(params), out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("oracle_primary_hits failed (status %d)" % rc)
+    return out

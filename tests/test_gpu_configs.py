@@ -185,7 +185,7 @@ def test_c5_view_group_shards(gpu_ready, amvpt_mod, oracle):
             print("overflow cells over 8 ranks:", overflow_cells)
 
 
-def test_c4_veach_eight_film_tile_shards(def test_c4_veach_eight_film_tile_shards(gpu_ready, amvpt_mod, oracle):
+def test_c4_veach_eight_film_tile_shards(gpu_ready, amvpt_mod, oracle):
     """C4 shape: the Veach-MIS 8-view frame (GGX plates, sphere lights, G = 8, sa_mis) split into the
     8 contiguous lane ranges (= bands of quilt rows) the 8-GPU run gives its ranks; every range's
     records match the oracle's and the 8 films sum to the oracle frame (the RCCL reduce)."""

@@ -107,9 +107,28 @@ def test_mvpath_seed_and_odd_spp(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s, seed=7)
 
 
-def test_path_integrator_c1(gpu_ready, amvpt_mod, oracle):
-    """C1 plumbing: stock `path` on a single perspective camera (reduced resolution)."""
-    s = amvpt_mod.load_file(CBOX_PATH, res=64, spp=16)
+@pytest.mark.parametrize("res", [64, 256], ids=["res64", "c1_full_256"])
+def test_path_integrator_c1(gpu_ready, amvpt_mod, oracle, res):
+    """C1: stock `path` on a single perspective camera; 256^2 at 16 spp is BASELINE's config itself."""
+    s = amvpt_mod.load_file(CBOX_PATH, res=res, spp=16)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert (p.film_width, p.film_height, amvpt_mod.plan(p)[0]) == (res, res, 16)
+    _check(amvpt_mod, oracle, s)
+
+
+@pytest.mark.parametrize("scene,defines", [
+    ("cbox_path.xml", dict(res=64, spp=16, crop_w=40, crop_h=24, crop_x=10, crop_y=30)),
+    ("cbox_batch.xml", dict(res=32, width=128, spp=16, crop_w=64, crop_h=16, crop_x=32, crop_y=8)),
+], ids=["path_c1", "batch_mvpath"])
+def test_crop_window(gpu_ready, amvpt_mod, oracle, scene, defines):
+    """hdrfilm crop windows (hdrfilm.cpp:245-291; film.cpp:16-27,91-100): lanes span the crop, positions are
+    film coordinates (+ crop_offset, mvpath.cpp:173-190), sample_ray_idx sees (pos - offset) / crop_size
+    (mvpath_multi.h:12-16), ImageBlock::put subtracts the offset (imageblock.cpp:211,266,447) and a batch's
+    reprojected views keep the full film's tile pitch; the single camera's projection includes the crop."""
+    s = amvpt_mod.load_file(os.path.join(SCENES, scene), **defines)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert (p.film_width, p.film_height, p.crop_offset_x, p.crop_offset_y) == (
+        defines["crop_w"], defines["crop_h"], defines["crop_x"], defines["crop_y"])
     _check(amvpt_mod, oracle, s)
 
 

@@ -230,3 +230,28 @@ def test_ply_binary_with_recomputed_normals(amvpt_mod):
 def test_mesh_errors(amvpt_mod):
     with pytest.raises(RuntimeError, match="not found"):
         amvpt_mod.load_string(_mesh_scene('<shape type="obj"><string name="filename" value="/nope.obj"/></shape>'))
+
+
+def test_crop_window_descriptors_and_projection(amvpt_mod, oracle):
+    """hdrfilm crop windows: the ImageBlock / lane space is the crop, the film keeps its full size, an invalid
+    window is the reference's error (film.cpp:91-96), and crop pixel (x, y) sees what film pixel
+    (x + crop_x, y + crop_y) of the uncropped camera sees (perspective_projection with the crop, sensor.h:319-356)."""
+    import numpy as np
+    path = os.path.join(SCENES, "cbox_path.xml")
+    full = amvpt_mod.load_file(path, res=64)
+    crop = amvpt_mod.load_file(path, res=64, crop_w=40, crop_h=24, crop_x=10, crop_y=30)
+    assert crop.film_info()[:2] == (40, 24)
+    sf, vf, pf = full.describe()
+    sc, vc, pc = crop.describe()
+    assert (pc.film_width, pc.film_height, pc.crop_offset_x, pc.crop_offset_y, pc.full_width, pc.full_height) == (
+        40, 24, 10, 30, 64, 64)
+    hf, hc = oracle.primary_hits(sf, vf, pf), oracle.primary_hits(sc, vc, pc)
+    sub = hf[30:54, 10:50]
+    assert (sub[..., 0] == hc[..., 0]).mean() > 0.99
+    assert np.abs(sub[..., 4:7] - hc[..., 4:7])[sub[..., 0] == hc[..., 0]].max() < 1e-4
+    with pytest.raises(RuntimeError, match="Invalid crop window specification"):
+        amvpt_mod.load_file(path, res=64, crop_w=60, crop_x=10)
+    # the grid sensor resizes its film, which resets any crop window (grid.cpp:230, film.cpp:102-106)
+    g = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=16)
+    gp = g.describe()[2]
+    assert (gp.crop_offset_x, gp.full_width) == (0, gp.film_width)
