@@ -623,11 +623,15 @@ AD void film_add(float *p, float v) { atomicAdd(p, v); }
  * list (a view-group rank's rare lanes whose jittered position rounds into the next tile).  With the
  * whole-quilt window (the single-GPU frame) every cell is inside.
  */
-AD bool in_window(const KParams &P, int x, int y) {
+/* kWin = false: the whole-quilt window, known at compile time (the row-splat kernels' instance for
+ * single-GPU frames; the runtime test cost 3.5 ms of k_splat per config-M frame, A/B r03d) */
+template <bool kWin = true> AD bool in_window(const KParams &P, int x, int y) {
+    if (!kWin) return true;
     return (uint32_t) (x - (int) P.fx0) < P.fw && (uint32_t) (y - (int) P.fy0) < P.fh;
 }
 /* film float of quilt cell (x, y), channel k -- the cell must be inside the window */
-AD float *film_cell(const KParams &P, float *film, int x, int y, int k) {
+template <bool kWin = true> AD float *film_cell(const KParams &P, float *film, int x, int y, int k) {
+    if (!kWin) return film + ((size_t) (uint32_t) y * P.W + (uint32_t) x) * P.C + k;
     return film + ((size_t) (uint32_t) (y - (int) P.fy0) * P.fw + (uint32_t) (x - (int) P.fx0)) * P.C + k;
 }
 /* append quilt float `idx` += v to the overflow list (one returning atomic: rare by construction) */
@@ -638,8 +642,8 @@ AD void overflow_push(const KParams &P, uint64_t idx, float v) {
         reinterpret_cast<uint4 *>(P.overflow + 4)[e] = make_uint4((uint32_t) idx, (uint32_t) (idx >> 32), __float_as_uint(v), 0u);
 }
 /* one film float of quilt cell (x, y), channel k: the window, else the overflow list */
-AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float v) {
-    if (in_window(P, x, y)) film_add(film_cell(P, film, x, y, k), v);
+template <bool kWin = true> AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float v) {
+    if (in_window<kWin>(P, x, y)) film_add(film_cell<kWin>(P, film, x, y, k), v);
     else overflow_push(P, ((uint64_t) (uint32_t) y * P.W + (uint32_t) x) * P.C + (uint32_t) k, v);
 }
 
@@ -936,7 +940,7 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
 /* one footprint's cells straight into the window (or the film when it does not fit) */
 /* kRolled: the window loop is not unrolled (row_put's rare per-lane path: an unrolled 5 x 5 x C
  * body would set the register allocation of the whole splat kernel) */
-template <int C, bool kRolled = false>
+template <int C, bool kRolled = false, bool kWin = true>
 AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, const float *wx,
                  const float *wy, const float *vals, bool coalesce, uint32_t *fallback) {
     const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
@@ -976,7 +980,7 @@ AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn
                 const float wxv = xs < kMaxFoot ? wx[xs] : (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs));
                 const float w = wxv * wyv;
 #pragma unroll
-                for (int k = 0; k < C; ++k) film_cell_add(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
+                for (int k = 0; k < C; ++k) film_cell_add<kWin>(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
             }
         }
     }
@@ -1029,7 +1033,7 @@ AD float union_weight(const KParams &P, float r, int x0, int cell, int lo, int h
     return (cell >= lo && cell < hi) ? w : 0.f;
 }
 
-template <int C>
+template <int C, bool kWin = true>
 AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, bool act,
                     const float *vals, bool coalesce, uint32_t *fallback) {
     const int x0c = max(f.x0, 0), y0c = max(f.y0, 0), x1 = f.x0 + f.nx, y1 = f.y0 + f.ny;
@@ -1096,7 +1100,7 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
     } else if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
-        foot_add<C, true>(P, film, wbase, wn, f, wx, wy, vals, coalesce, fallback);
+        foot_add<C, true, kWin>(P, film, wbase, wn, f, wx, wy, vals, coalesce, fallback);
     }
 }
 
@@ -1117,16 +1121,16 @@ AD int wave_max_dpp(int v) {
  * reciprocal with a one-step correction (e < 2^24), not an integer division.  (Batching four
  * cells per lane -- four LDS reads, one wait -- measured no faster and its live pointers pushed
  * the 5-wave register budget into scratch.) */
-template <int C>
+template <int C, bool kWin = true>
 AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int rowlen = w.ww * C;
     const int n_elems = rowlen * w.wh;
     const float inv_rowlen = 1.f / (float) max(rowlen, 1);
     /* the wave window's quilt cells inside the film window (uniform; always for the whole quilt) */
-    const bool inside = in_window(P, w.bx0, w.by0) && in_window(P, w.bx0 + w.ww - 1, w.by0 + w.wh - 1);
-    float *film0 = inside ? film_cell(P, film, w.bx0, w.by0, 0) : film;
-    const uint32_t film_row = P.fw * (uint32_t) C;
+    const bool inside = in_window<kWin>(P, w.bx0, w.by0) && in_window<kWin>(P, w.bx0 + w.ww - 1, w.by0 + w.wh - 1);
+    float *film0 = inside ? film_cell<kWin>(P, film, w.bx0, w.by0, 0) : film;
+    const uint32_t film_row = (kWin ? P.fw : P.W) * (uint32_t) C;
     for (int e = (int) __lane_id(); e < n_elems; e += 64) {
         int cy = (int) ((float) e * inv_rowlen);
         cy -= (cy * rowlen > e) ? 1 : 0;
@@ -1149,7 +1153,7 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
 #endif
             if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
                 if (inside) film_add(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
-                else film_cell_add(P, film, w.bx0 + cx, w.by0 + cy, k, v);
+                else film_cell_add<kWin>(P, film, w.bx0 + cx, w.by0 + cy, k, v);
             }
         }
     }
@@ -1157,7 +1161,7 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
 }
 
 /* ImageBlock::put of a wave's samples through its own window (AMVPT_WAVE_WIN, row_splat) */
-template <int C>
+template <int C, bool kWin = true>
 AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float py, const float *vals, bool valid,
                  bool coalesce, uint32_t *fallback) {
     Foot f;
@@ -1185,8 +1189,8 @@ AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float p
     }
     WinT *const win = L.win + (threadIdx.x >> 6) * (kWavePlane * C);
     /* row_put reads the window through L.win: hand it this wave's window */
-    row_put_win<C>(P, film, win, wn, f, act, vals, coalesce, fallback);
-    wave_flush<C>(P, film, win, wn);
+    row_put_win<C, kWin>(P, film, win, wn, f, act, vals, coalesce, fallback);
+    wave_flush<C, kWin>(P, film, win, wn);
 }
 
 /*
@@ -2083,6 +2087,18 @@ AD float tv_pdf(const DBsdf *T, f3 wo_l, f3 wi_k, float p_k, const BD &bd, bool 
     p = lerp_(p, q, bd.alpha);
     return active ? p : 0.f;
 }
+/* tv_pdf with wi_k's pdf row hoisted out of a loop over wo_l (same value bit for bit) */
+AD float tv_pdf_row(const PdfRow &R, f3 wo_l, float p_k, const BD &bd, bool active) {
+    active = active && p_k > 0.f;
+    float p_l = row_pdf(R, wo_l, active);
+    active = active && p_l > 0.f;
+    float p_max = vmax(p_l, p_k), p_min = vmin(p_l, p_k);
+    float q = p_min * rcp(p_max);
+    float p = fmadd(q - 1.f, bd.rsqrt_a, 1.f);
+    p = sqr(vmax(p, 0.f));
+    p = lerp_(p, q, bd.alpha);
+    return active ? p : 0.f;
+}
 AD float tv_pdf_fast(f3 wo_l, f3 wi_k, float p_k, const BD &bd, bool active) {
     float p_l = sqr(normalize(wi_k + wo_l).z);
     float N = fmadd(bd.sqr_a, vmax(p_k, p_l), 1.f), D = fmadd(bd.sqr_a, vmin(p_k, p_l), 1.f);
@@ -2110,6 +2126,14 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #endif
 #ifndef AMVPT_PRIM_SLOT_ORDER
 #define AMVPT_PRIM_SLOT_ORDER 1
+#endif
+#ifndef AMVPT_DEFER_SAMPLE
+/* camera_selection's per-view BSDF samples: the loop takes each view's sample type (no sampling)
+ * and one bsdf_sample runs for the last replacing view (0: a sample per view, A/B) */
+#define AMVPT_DEFER_SAMPLE 1
+#endif
+#ifndef AMVPT_PDF_ROW
+#define AMVPT_PDF_ROW 1   /* the pairwise MIS sum hoists wi_k's pdf row (0: per-pair bsdf_pdf, A/B) */
 #endif
 #ifndef AMVPT_PRIM_WAVES
 #define AMVPT_PRIM_WAVES 1
@@ -2259,6 +2283,8 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                                       : tv_pdf(S.bsdfs, wo_r0, wik, pdfM, bd, active);
                 };
                 float n_direct = 1.f, n_indir = 2.f;
+                int rep_k = 0;   /* AMVPT_DEFER_SAMPLE: the view whose BSDF sample replaces the primary's */
+                (void) rep_k;
 #pragma unroll 1
                 for (int k = 1; k < Gn; ++k) {
                     Surf r = camera_sample_surface(V[view_of(k)], si, bd.reuse, apx, apy);
@@ -2296,9 +2322,16 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     direct_pdf += direct ? bpk : 0.f;
                     n_direct += (float) direct;
                     if (!kDiff) {
+#if AMVPT_DEFER_SAMPLE
+                        /* only the last replacing view's sampled direction survives the loop: its type
+                         * decides here, the one bsdf_sample runs after the loop */
+                        indirect = indirect && bsdf_sample_type(S.bsdfs, b, CTX_ALL, wik, valid) == bsmp.type;
+                        if (indirect && replace) rep_k = k;
+#else
                         bsdf_sample(S.bsdfs, b, CTX_ALL, wik, r2a, r2b, valid, bsk, bwk);
                         indirect = indirect && bsk.type == bsmp.type;
                         if (indirect && replace) bsmp.wo = bsk.wo;
+#endif
                     }
                     /* kDiff: a valid view's sample is the primary's (same type, same wo) */
                     (void) replace;
@@ -2306,6 +2339,14 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     vmask |= valid ? vbit<G>(k) : 0u;
                     imask |= indirect ? vbit<G>(k) : 0u;
                 }
+#if AMVPT_DEFER_SAMPLE
+                if (!kDiff && rep_k > 0) {
+                    BSample bsk;
+                    C3 bwk;
+                    bsdf_sample(S.bsdfs, b, CTX_ALL, wi_of(rep_k), r2a, r2b, true, bsk, bwk);
+                    bsmp.wo = bsk.wo;
+                }
+#endif
                 direct_pdf /= n_direct;
                 const float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
                 const C3 emis_mis = em_w * mis_em;
@@ -2350,14 +2391,22 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     bool cond = k > 0 ? vk : bd.reuse;
                     float acc = 0.f;
                     if (!kDiff && cond && !bd.diffuse) {
+#if AMVPT_PDF_ROW
+                        const PdfRow row = pdf_row(S.bsdfs, b, CTX_GLOSSY, wik);
+#endif
 #pragma unroll 1
                         for (int j = 1; j < Gn; ++j) {
                             if (j == k) continue;
                             float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
                             f3 worj = reflect_l(mk(VSF(F_WX, j), VSF(F_WY, j), VSF(F_WZ, j)));
                             const bool vj = (vmask >> j) & 1u;
+#if AMVPT_PDF_ROW
+                            float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
+                                                       : tv_pdf_row(row, worj, pdfMk, bd, vj);
+#else
                             float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
                                                        : tv_pdf(S.bsdfs, worj, wik, pdfMk, bd, vj);
+#endif
                             acc = fmadd(VSF(F_PDF, j), pdf_J * pdf_Mat, acc);
                         }
                     } else {
@@ -2502,15 +2551,16 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
 #ifndef AMVPT_SPLAT_WAVES
 #define AMVPT_SPLAT_WAVES 5
 #endif
-/* kRow: the row-reduced splat with wave windows (P.row_splat, RGBW), else the block window */
-template <int G, int C, bool kDiff, bool kRow>
+/* kRow: the row-reduced splat with wave windows (P.row_splat, RGBW), else the block window;
+ * kWin = false (kRow only): the film is the whole quilt */
+template <int G, int C, bool kDiff, bool kRow, bool kWin = true>
 __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(KParams P, const DView *V, Bufs B) {
     __shared__ typename std::conditional<kRow, WaveLds<C>, SplatLds<C>>::type L;
     if (kRow) wave_lds_init(reinterpret_cast<WaveLds<C> &>(L));
     else splat_lds_init(reinterpret_cast<SplatLds<C> &>(L));
     /* one put of this kernel's kind */
     auto put = [&](float x, float y, const float *vals, bool valid, bool coalesce, int buf, uint32_t *fb) {
-        if constexpr (kRow) wave_put<C>(P, B.film, L, x, y, vals, valid, coalesce, fb);
+        if constexpr (kRow) wave_put<C, kWin>(P, B.film, L, x, y, vals, valid, coalesce, fb);
         else block_put<C>(P, B.film, L, buf, x, y, vals, valid, coalesce, fb);
     };
     const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
@@ -2802,8 +2852,11 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
 template <int G>
 void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff) {
     const bool row = AMVPT_WAVE_WIN && P.row_splat && P.C == 4;
+    const bool whole = P.fx0 == 0u && P.fy0 == 0u && P.fw == P.W && P.fh == P.H;
     if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
     else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (diff && row && whole) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
+    else if (row && whole) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
     else if (diff && row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
     else if (row) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, false, true>), grid, dim3(kSplatBlock), 0, st, P, V, B);
     else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 4, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);

@@ -49,6 +49,7 @@ constexpr float kInvSqrtPi = 0.56418958354775628695f;
 struct Mf {
     float au, av;
     bool visible, beckmann;
+    AD Mf() : au(1.f), av(1.f), visible(false), beckmann(false) {}
     AD Mf(const DBsdf &b)
         : au(vmax(b.alpha_u, 1e-4f)), av(vmax(b.alpha_v, 1e-4f)), visible(b.sample_visible != 0),
           beckmann(b.distribution == AMVPT_MICROFACET_BECKMANN) {}
@@ -290,6 +291,50 @@ AD float bsdf_pdf(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, f3 wo, bool ac
     return leaf_pdf(T[r.leaf], ctx, ts_wi(r, wi), ts_wo(r, wi, wo));
 }
 
+/*
+ * bsdf_pdf with wi fixed, for loops over many wo (the pairwise MIS sums): the twosided
+ * resolve, the leaf's microfacet parameters, smith_g1(wi) and 4 wi.z are taken once.
+ * smith_g1(wi, m) is G1(wi) unless dot(wi, m) wi.z <= 0, which leaf_pdf's own validity
+ * test already zeroes, so row_pdf returns leaf_pdf's value bit for bit (same operations
+ * in the same order).
+ */
+struct PdfRow {
+    int32_t leaf;     /* < 0: every pdf is zero */
+    uint32_t flip;
+    f3 wi, twi;       /* wi and its twosided-resolved form */
+    Mf mf;
+    float g1, den;    /* smith_g1(twi, .) before its orientation test; 4 twi.z */
+    bool diffuse, on; /* leaf type; ctx enables the leaf's lobe */
+};
+AD PdfRow pdf_row(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi) {
+    PdfRow R{-1, 0u, wi, wi, Mf(), 0.f, 1.f, false, false};
+    if (b < 0) return R;
+    const TwoSided r = resolve_twosided(T, b, wi);
+    R.leaf = r.leaf;
+    if (r.leaf < 0) return R;
+    R.flip = r.flip;
+    R.twi = ts_wi(r, wi);
+    const DBsdf &d = T[r.leaf];
+    R.diffuse = d.type == BSDF_DIFFUSE;
+    R.on = ctx_on(ctx, R.diffuse ? BF_DiffuseReflection : BF_GlossyReflection);
+    R.mf = Mf(d);
+    R.g1 = R.mf.smith_g1(R.twi, R.twi);   /* m = wi passes the orientation test when wi.z != 0 */
+    R.den = 4.f * R.twi.z;
+    return R;
+}
+AD float row_pdf(const PdfRow &R, f3 wo, bool active) {
+    if (R.leaf < 0 || !active || !R.on) return 0.f;
+    const f3 two = ts_wo(TwoSided{R.leaf, R.flip}, R.wi, wo);
+    if (R.diffuse) {
+        float p = kInvPi * two.z;
+        return (R.twi.z > 0.f && two.z > 0.f) ? p : 0.f;
+    }
+    f3 m = normalize(two + R.twi);
+    bool a = R.twi.z > 0.f && two.z > 0.f && dot(R.twi, m) > 0.f && dot(two, m) > 0.f;
+    float r = R.mf.visible ? R.mf.eval(m) * R.g1 / R.den : R.mf.eval(m) * m.z / (4.f * dot(two, m));
+    return a ? r : 0.f;
+}
+
 template <bool kDiff = false>
 AD void bsdf_sample(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, float u1, float u2, bool active, BSample &bs,
                     C3 &w) {
@@ -301,6 +346,22 @@ AD void bsdf_sample(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, float u1, fl
     leaf_sample(T[r.leaf], ctx, ts_wi(r, wi), u1, u2, bs, w);
     if (r.flip == 1u) bs.wo.z *= -1.f;
     if (r.flip == 2u) bs.wo.z = mulsign(bs.wo.z, wi.z);
+}
+
+/* bsdf_sample(...).type without the sample: leaf_sample sets the lobe's type whether or not the
+ * sample is valid, and zero when the BSDF is null, the lane masked, the lobe off in ctx or the
+ * twosided resolve finds no side */
+template <bool kDiff = false>
+AD uint32_t bsdf_sample_type(const DBsdf *T, int32_t b, uint32_t ctx, f3 wi, bool active) {
+    if (b < 0 || !active) return 0u;
+    int32_t leaf = b;
+    if (!kDiff) {
+        const TwoSided r = resolve_twosided(T, b, wi);
+        if (r.leaf < 0) return 0u;
+        leaf = r.leaf;
+    }
+    const uint32_t lobe = (kDiff || T[leaf].type == BSDF_DIFFUSE) ? BF_DiffuseReflection : BF_GlossyReflection;
+    return ctx_on(ctx, lobe) ? lobe : 0u;
 }
 
 AD float leaf_roughness(const DBsdf &d) {

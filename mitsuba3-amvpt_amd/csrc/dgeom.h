@@ -419,18 +419,18 @@ template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray
     return sphere_hit(p, r, t);
 }
 
-/* closest-hit update of the brute-force walks: (t, scene-order index) as trace_closest */
-/* branch-free: the update is a select per field (no exec-mask save / restore per primitive) */
+/* closest-hit update of the brute-force walks: (t, scene-order index) as trace_closest.  Branchy:
+ * a select per field instead measured 1-2 ms slower per config-M frame (k_suffix 133.3 vs
+ * 133.7..135.2 ms, A/B r03d) */
 template <bool kSph> AD void brute_test(const DPrim &p, uint32_t pi, const Ray &ray, Hit &best, uint32_t &best_orig) {
     float t, u, v;
-    const bool h = prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v);
-    const uint32_t orig = ufirst(p.pad);
-    const bool better = h && (t < best.t || (t == best.t && orig < best_orig));
-    best.t = better ? t : best.t;
-    best.u = better ? u : best.u;
-    best.v = better ? v : best.v;
-    best.prim = better ? (int32_t) pi : best.prim;
-    best_orig = better ? orig : best_orig;
+    if (prim_hit_b<kSph>(p, ufirst(p.type), ray, t, u, v)) {
+        const uint32_t orig = ufirst(p.pad);
+        if (t < best.t || (t == best.t && orig < best_orig)) {
+            best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+            best_orig = orig;
+        }
+    }
 }
 /* Two records in flight (a, b), each reloaded in place right after its own test: the next
  * record's scalar load overlaps the current test and no record is copied between registers

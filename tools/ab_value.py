@@ -1,4 +1,4 @@
-"""Timed Msamples/s of config M for each variant: a library dir or an environment setting.
+"""Timed Msamples/s of config M (or $AB_CONFIG) for each variant: a library dir or an environment setting.
 
     python tools/ab_value.py <libdir> [<libdir> ...]    (dirs relative to mitsuba3-amvpt_amd/)
     python tools/ab_value.py --env AMVPT_BRUTE=0 --env AMVPT_BRUTE=1 ...   (current lib/)
@@ -12,6 +12,12 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# bench.py's workloads (AB_CONFIG selects one; default M)
+CONFIGS = {
+    "M": dict(scene="cbox_grid.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),
+    "C3": dict(scene="veach_grid.xml", res=1024, spp=256, gx=4, gy=2, reuse=8),
+    "mesh": dict(scene="cbox_mesh.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),
+}
 
 
 def child(steps=3, kernels=False):
@@ -22,11 +28,14 @@ def child(steps=3, kernels=False):
         amvpt.set_chunk_lanes(int(os.environ["AB_CHUNK"]))
     if os.environ.get("AB_TRAV"):
         amvpt.set_traversal(int(os.environ["AB_TRAV"]))
-    s = amvpt.load_file(os.path.join(REPO, "scenes", "cbox_grid.xml"), res=1024, spp=64, gx=4, gy=2, reuse=8)
+    cfg = dict(CONFIGS[os.environ.get("AB_CONFIG", "M")])
+    scene = cfg.pop("scene")
+    s = amvpt.load_file(os.path.join(REPO, "scenes", scene), **cfg)
     sd, vd, p = s.describe(0, 0, 0)
+    spp = cfg["spp"]
     dev = amvpt.DeviceScene(sd)
     film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
-    lanes = p.film_width * p.film_height * 64
+    lanes = p.film_width * p.film_height * spp
     dev.render(vd, p, film.data_ptr())
     torch.cuda.synchronize()
     t0 = time.perf_counter()
