@@ -2132,6 +2132,12 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * and one bsdf_sample runs for the last replacing view (0: a sample per view, A/B) */
 #define AMVPT_DEFER_SAMPLE 1
 #endif
+#ifndef AMVPT_PAIR_REGS
+/* pair-sum operands of views j >= 1 in registers for G <= 8: k_mv_primary 459 -> 427 ms per C3 frame
+ * (0: read from LDS per pair, A/B r03g); reading view k's own fields from the register copies too
+ * (uniform dynamic index) measured slower, 444 ms (r03h) */
+#define AMVPT_PAIR_REGS 1
+#endif
 #ifndef AMVPT_PDF_ROW
 #define AMVPT_PDF_ROW 1   /* the pairwise MIS sum hoists wi_k's pdf row (0: per-pair bsdf_pdf, A/B) */
 #endif
@@ -2373,6 +2379,17 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                 /* ---- per view: mis_weights (mvpath_multi.h:466-523), direct light and
                  *      the multi-view mixture pdf (mvpath_multi.h:245-317) ---- */
                 float n_ind = 0.f, pdf = 0.f;
+                /* the pair sums' operands of views j >= 1 (same for every k): registers for the
+                 * compile-time groups up to 8 views, LDS otherwise */
+                constexpr int kPR = (AMVPT_PAIR_REGS && !kDiff && G >= 2 && G <= 8) ? G : 1;
+                float pJp[kPR], pPdf[kPR], pWx[kPR], pWy[kPR], pWz[kPR];
+                if constexpr (kPR > 1) {
+#pragma unroll
+                    for (int j = 1; j < kPR; ++j) {
+                        pJp[j] = VSF(F_JP, j); pPdf[j] = VSF(F_PDF, j);
+                        pWx[j] = VSF(F_WX, j); pWy[j] = VSF(F_WY, j); pWz[j] = VSF(F_WZ, j);
+                    }
+                }
 #pragma unroll 1
                 for (int k = 0; k < Gn; ++k) {
                     const bool vk = (vmask >> k) & 1u;
@@ -2394,6 +2411,23 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
 #if AMVPT_PDF_ROW
                         const PdfRow row = pdf_row(S.bsdfs, b, CTX_GLOSSY, wik);
 #endif
+                        if constexpr (kPR > 1) {
+#pragma unroll
+                            for (int j = 1; j < kPR; ++j) {
+                                if (j == k) continue;
+                                const float pdf_J = vmin(sqr(pJp[j] * iJpk), 1.f);
+                                const f3 worj = reflect_l(mk(pWx[j], pWy[j], pWz[j]));
+                                const bool vj = (vmask >> j) & 1u;
+#if AMVPT_PDF_ROW
+                                const float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
+                                                                 : tv_pdf_row(row, worj, pdfMk, bd, vj);
+#else
+                                const float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
+                                                                 : tv_pdf(S.bsdfs, worj, wik, pdfMk, bd, vj);
+#endif
+                                acc = fmadd(pPdf[j], pdf_J * pdf_Mat, acc);
+                            }
+                        } else
 #pragma unroll 1
                         for (int j = 1; j < Gn; ++j) {
                             if (j == k) continue;
@@ -2409,6 +2443,14 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
 #endif
                             acc = fmadd(VSF(F_PDF, j), pdf_J * pdf_Mat, acc);
                         }
+                    } else if constexpr (kPR > 1) {
+#pragma unroll
+                        for (int j = 1; j < kPR; ++j) {
+                            if (j == k) continue;
+                            const float pdf_J = vmin(sqr(pJp[j] * iJpk), 1.f);
+                            acc = fmadd(pPdf[j], pdf_J, acc);
+                        }
+                        acc = cond ? acc : 0.f;
                     } else {
 #pragma unroll 1
                         for (int j = 1; j < Gn; ++j) {

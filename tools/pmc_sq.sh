@@ -10,6 +10,6 @@ B="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 C="SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64"
 for P in A B C; do
   eval CS=\$$P
-  timeout -s KILL 120 rocprofv3 --pmc $CS --output-format csv -d gpurun_out/${TAG}_sq$P -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 "$@" > gpurun_out/${TAG}_sq$P.log 2>&1 || { echo "pass $P failed"; tail -5 gpurun_out/${TAG}_sq$P.log; }
+  timeout -s KILL 120 rocprofv3 --pmc $CS --output-format csv -d gpurun_out/${TAG}_sq$P -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 "$@" > gpurun_out/${TAG}_sq$P.log 2>&1 || { echo "pass $P failed"; tail -5 gpurun_out/${TAG}_sq$P.log; exit 1; }
 done
 echo done
