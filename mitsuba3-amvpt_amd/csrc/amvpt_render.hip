@@ -2138,6 +2138,9 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * (uniform dynamic index) measured slower, 444 ms (r03h) */
 #define AMVPT_PAIR_REGS 1
 #endif
+#ifndef AMVPT_CHUNK_STREAMS
+#define AMVPT_CHUNK_STREAMS 2   /* chunk streams of a render (1: every chunk on the render stream, A/B) */
+#endif
 #ifndef AMVPT_PDF_ROW
 #define AMVPT_PDF_ROW 1   /* the pairwise MIS sum hoists wi_k's pdf row (0: per-pair bsdf_pdf, A/B) */
 #endif
@@ -2799,8 +2802,9 @@ struct KTimer {
     }
     void flush() {
         if (!on || n == 0 || err != hipSuccess) return;
-        err = hipEventSynchronize(ev[2 * n - 1]);
         for (size_t i = 0; i < n && err == hipSuccess; ++i) {
+            err = hipEventSynchronize(ev[2 * i + 1]);   /* pairs may sit on either chunk stream */
+            if (err != hipSuccess) break;
             float t = 0.f;
             err = hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
             ms[kid[i]] += t;
@@ -3011,6 +3015,10 @@ struct DevArena {
     hipEvent_t done = nullptr;
     hipStream_t last = nullptr;
     bool pending = false;
+    /* the second chunk stream (AMVPT_CHUNK_STREAMS = 2): created once per device; fork / join
+     * order it after / before the render stream */
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 static std::mutex g_arenas_mu;
 static std::map<int, std::unique_ptr<DevArena>> g_arenas;
@@ -3283,7 +3291,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
     const uint64_t qlen = (uint64_t) qcap * kQParts;
     const size_t stats_bytes = (size_t) kStats * kStatShards * 8, cnt_bytes = (size_t) 3 * kQParts * kCntStride * 4;
-    const size_t need = views_bytes + stats_bytes + cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
+    /* chunks alternate between two buffer sets on two streams (the render stream and the arena's side
+     * stream): one chunk's kernels fill the CUs the other's leave idle (low-occupancy primary
+     * shading, launch tails) */
+    const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk) ? 2 : 1;
+    const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
+    const size_t need = views_bytes + stats_bytes + set_bytes * n_sets;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     DevArena &A = dev_arena(dev);
@@ -3292,17 +3305,37 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* the previous render's buffers may still be in flight on another stream */
     if (A.pending && A.last != st) HIPCHK(hipStreamWaitEvent(st, A.done, 0));
     /* every return below records `done` on this stream (also the error paths) */
+    if (n_sets > 1 && !A.side) {
+        HIPCHK(hipStreamCreateWithFlags(&A.side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&A.fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&A.join, hipEventDisableTiming));
+    }
+    /* every return below joins the side stream into this one and records `done` (also the error paths) */
     struct ArenaRelease {
-        DevArena &A; hipStream_t st;
-        ~ArenaRelease() { if (hipEventRecord(A.done, st) == hipSuccess) { A.pending = true; A.last = st; } }
+        DevArena &A; hipStream_t st; bool side = false;
+        void join() {
+            if (!side) return;
+            side = false;
+            if (hipEventRecord(A.join, A.side) == hipSuccess) (void) hipStreamWaitEvent(st, A.join, 0);
+        }
+        ~ArenaRelease() {
+            join();
+            if (hipEventRecord(A.done, st) == hipSuccess) { A.pending = true; A.last = st; }
+        }
     } arena_release{A, st};
+    /* the side stream starts after `st`'s work so far (views upload, counters) */
+    auto fork_side = [&]() -> amvpt_status {
+        if (n_sets < 2 || arena_release.side) return AMVPT_OK;
+        HIPCHK(hipEventRecord(A.fork, st));
+        HIPCHK(hipStreamWaitEvent(A.side, A.fork, 0));
+        arena_release.side = true;
+        return AMVPT_OK;
+    };
     { const amvpt_status as_ = arena_reserve(A, A.base, A.bytes, need, "lane arena"); if (as_ != AMVPT_OK) return as_; }
     char *base = (char *) A.base;
     DView *dviews = (DView *) base;
     unsigned long long *dstats = (unsigned long long *) (base + views_bytes);
-    uint32_t *dcnt = (uint32_t *) (base + views_bytes + stats_bytes);   /* [3][kQParts * kCntStride] */
-    uint32_t *const cntA = dcnt, *const cntB = dcnt + kQParts * kCntStride, *const cntN = dcnt + 2 * kQParts * kCntStride;
-    char *p = base + views_bytes + stats_bytes + cnt_bytes;
+    char *p = base + views_bytes + stats_bytes;
     auto carve = [&](size_t bytes) { char *r = p; p += (bytes + 255) & ~(size_t) 255; return r; };
     HIPCHK(hipMemcpyAsync(dviews, hv.data(), hv.size() * sizeof(DView), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(dstats, 0, stats_bytes, st));
@@ -3331,30 +3364,42 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         d_cub = ap;
     }
 
-    Bufs B{};
-    float4 *qa[kQPlanes], *qb[kQPlanes];
-    for (int k = 0; k < kQPlanes; ++k) qa[k] = (float4 *) carve(16 * qlen);
-    for (int k = 0; k < kQPlanes; ++k) qb[k] = (float4 *) carve(16 * qlen);
-    B.lane_out = (float4 *) carve(16 * chunk);
-    for (int k = 0; k < 4; ++k) B.lrec[k] = (float4 *) carve(16 * chunk);
-    B.hit = (float4 *) carve(16 * std::max<uint64_t>(chunk, qlen));
-    for (int k = 0; k < 3; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
-    B.nee_cb = (float *) carve(4 * qlen);
-    for (int k = 0; k < 3; ++k) B.vreq[k] = (float4 *) carve(16 * chunk);
-    B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
-    B.cnt_nee = cntN;
-    B.qcap = qcap;
-    B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : 32) * G * chunk);
-    if (wide) {
-        B.vreq_w = (uint4 *) carve(16 * chunk);
-        for (int k = 0; k < 2; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
+    /* one buffer set per chunk stream: queues A / B and their counters, the chunk's lane arena */
+    struct ChunkSet {
+        Bufs B{};
+        float4 *qa[kQPlanes], *qb[kQPlanes];
+        uint32_t *cntA, *cntB, *cntN;   /* [kQParts * kCntStride] each */
+        hipStream_t st;
+    } sets[2];
+    for (int si = 0; si < n_sets; ++si) {
+        ChunkSet &cs = sets[si];
+        Bufs &B = cs.B;
+        cs.st = si == 0 ? st : A.side;
+        uint32_t *dcnt = (uint32_t *) carve(cnt_bytes);
+        cs.cntA = dcnt; cs.cntB = dcnt + kQParts * kCntStride; cs.cntN = dcnt + 2 * kQParts * kCntStride;
+        for (int k = 0; k < kQPlanes; ++k) cs.qa[k] = (float4 *) carve(16 * qlen);
+        for (int k = 0; k < kQPlanes; ++k) cs.qb[k] = (float4 *) carve(16 * qlen);
+        B.lane_out = (float4 *) carve(16 * chunk);
+        for (int k = 0; k < 4; ++k) B.lrec[k] = (float4 *) carve(16 * chunk);
+        B.hit = (float4 *) carve(16 * std::max<uint64_t>(chunk, qlen));
+        for (int k = 0; k < 3; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
+        B.nee_cb = (float *) carve(4 * qlen);
+        for (int k = 0; k < 3; ++k) B.vreq[k] = (float4 *) carve(16 * chunk);
+        B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
+        B.cnt_nee = cs.cntN;
+        B.qcap = qcap;
+        B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : 32) * G * chunk);
+        if (wide) {
+            B.vreq_w = (uint4 *) carve(16 * chunk);
+            for (int k = 0; k < 2; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
+        }
+        B.film = film;
+        B.records = records;
+        B.stats = dstats;
+        B.amask = d_amask;
+        B.asel = d_asel;
+        B.run_delta = d_delta;
     }
-    B.film = film;
-    B.records = records;
-    B.stats = dstats;
-    B.amask = d_amask;
-    B.asel = d_asel;
-    B.run_delta = d_delta;
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
     const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
@@ -3384,7 +3429,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     /* the shared suffix (sample_suffix / sample_single loop) over the queue the raygen
      * or primary kernel filled: one k_bounce launch per depth, ping-pong A <-> B */
-    auto run_suffix = [&](uint32_t cn) -> amvpt_status {
+    auto run_suffix = [&](ChunkSet &cs, uint32_t cn) -> amvpt_status {
+        Bufs &B = cs.B;
+        hipStream_t st = cs.st;
+        float4 *const *qa = cs.qa, *const *qb = cs.qb;
+        uint32_t *const cntA = cs.cntA, *const cntB = cs.cntB;
         if (fuse_suffix) {
             /* one k_suffix_fused launch over the primary queue (A); B's counters are its work counters */
             for (int k = 0; k < kQPlanes; ++k) { B.q_in[k] = qa[k]; B.q_out[k] = qb[k]; }
@@ -3439,12 +3488,24 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     };
     uint64_t adaptive_lanes = 0;
 
+    uint64_t chunk_index = 0;
     for (uint32_t pass = 0; pass < n_passes; ++pass) {
         RoctxScope range_pass("amvpt pass");
         P.seed_value = Pp.base_seed + (is_mv ? (spp_pp * pass + Pp.seed) : Pp.seed);
         P.record = (records && pass == record_pass) ? 1u : 0u;
-        for (uint64_t c0 = 0; c0 < span; c0 += chunk) {   /* virtual indices of the lane set */
+        for (uint64_t c0 = 0; c0 < span; c0 += chunk, ++chunk_index) {   /* virtual indices of the lane set */
             const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, span - c0);
+            /* odd chunks on the side stream, which starts once the first chunk's primary stage is queued
+             * (the two streams then run offset by about half a chunk) */
+            ChunkSet &cs = sets[chunk_index & (uint64_t) (n_sets - 1)];
+            Bufs &B = cs.B;
+            hipStream_t st = cs.st;
+            uint32_t *const cntA = cs.cntA, *const cntB = cs.cntB;
+            float4 *const *qa = cs.qa, *const *qb = cs.qb;
+            if (&cs != &sets[0]) {   /* a side chunk never runs before the fork (e.g. after a pass's join) */
+                const amvpt_status fs_ = fork_side();
+                if (fs_ != AMVPT_OK) return fs_;
+            }
             P.chunk_begin = c0;
             P.chunk_n = cn;
             B.records = P.record ? records + (size_t) c0 * G * 8 : records;
@@ -3467,10 +3528,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);
             T.mark(st);
+            if (n_sets > 1 && (chunk_index & 1) == 0) {   /* the side stream's start: after this primary stage */
+                const amvpt_status fs_ = fork_side();
+                if (fs_ != AMVPT_OK) return fs_;
+            }
             /* suffix bounces: ping-pong A <-> B */
             {
                 RoctxScope range_suffix("amvpt shared suffix (extend, bounce, NEE)");
-                const amvpt_status rs_ = run_suffix(cn);
+                const amvpt_status rs_ = run_suffix(cs, cn);
                 if (rs_ != AMVPT_OK) return rs_;
             }
             T.mark(st);
@@ -3483,10 +3548,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             T.end(st);
             T.mark(st);
             HIPCHK(hipGetLastError());
-            T.flush();
+            if (n_sets < 2) T.flush();
             HIPCHK(T.err);
         }
         if (do_fill) {
+            /* the fill reads the whole pass's adapt_mask: both chunk streams first */
+            arena_release.join();
             RoctxScope range_fill("amvpt adaptive fill");
             /* compact the pass's adapt_mask lanes in lane order (virtual indices of the lane set,
              * ascending = lane order), then n_adapt re-traces each */
@@ -3549,6 +3616,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             P.adapt_seed = Pp.base_seed + (uint32_t) (total * n_adapt);   /* sampler->fork(); seed(wavefront, wavefront) */
             P.adapt_pass = 1;
             P.record = 0;
+            ChunkSet &cs = sets[0];
+            Bufs &B = cs.B;
+            uint32_t *const cntA = cs.cntA, *const cntB = cs.cntB;
+            float4 *const *qa = cs.qa, *const *qb = cs.qb;
             for (uint64_t c0 = 0; c0 < wf; c0 += chunk) {
                 const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, wf - c0);
                 P.chunk_begin = c0;
@@ -3560,7 +3631,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 hipLaunchKernelGGL(k_raygen_adapt, dim3((cn + 255) / 256), dim3(256), 0, st, P, dviews, B);
                 T.end(st);
                 HIPCHK(hipGetLastError());
-                { const amvpt_status rs_ = run_suffix(cn); if (rs_ != AMVPT_OK) return rs_; }
+                { const amvpt_status rs_ = run_suffix(cs, cn); if (rs_ != AMVPT_OK) return rs_; }
                 const dim3 sgrid((cn + kSplatBlock - 1) / kSplatBlock);
                 T.begin(AMVPT_K_SPLAT, st);
                 if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_adapt<5>), sgrid, dim3(kSplatBlock), 0, st, P, B);
@@ -3573,6 +3644,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             P = Ps;
         }
     }
+    arena_release.join();
     uint64_t overflow_cells = 0;
     if (P.overflow) {
         /* the caller sums the list; a list that ran out of room lost cells: fail loudly */
