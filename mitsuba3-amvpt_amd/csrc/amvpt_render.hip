@@ -1523,8 +1523,17 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
  * The accumulation order of a lane's result is the reference's: emitter hit of
  * vertex d, then NEE of vertex d, then vertex d + 1.
  */
+/* waves per SIMD the suffix walks' register allocation must allow (latency-bound dependent node loads):
+ * k_extend at 6 (80 VGPRs) took the mesh frame 599 -> 609 Msamples/s; 8 (64 VGPRs, 48 B of spills)
+ * 606; k_shadow keeps its own allocation (r03k) */
+#ifndef AMVPT_EXTEND_WAVES
+#define AMVPT_EXTEND_WAVES 6
+#endif
+#ifndef AMVPT_SHADOW_WAVES
+#define AMVPT_SHADOW_WAVES 1
+#endif
 template <int kWalk>
-__global__ void __launch_bounds__(256) k_extend(KParams P, const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(256, AMVPT_EXTEND_WAVES) k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
@@ -1545,7 +1554,7 @@ __global__ void __launch_bounds__(256) k_extend(KParams P, const DScene *Sp, Buf
 }
 
 template <int kWalk>
-__global__ void __launch_bounds__(256) k_shadow(KParams P, const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
