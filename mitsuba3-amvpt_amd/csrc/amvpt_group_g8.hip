@@ -1,7 +1,7 @@
 /*
  * amvpt_group_g8.hip -- explicit instances of the group-size launchers (launch_primary<G>,
  * launch_splat<G> and their kernels) for G in { 8 }
- * (G = 0: the runtime instance for 17..64 views).  Split from amvpt_render.hip so the
+ * (G = 0: the runtime instance for 17..256 views).  Split from amvpt_render.hip so the
  * instances compile in parallel; see "Group-size instances" there.
  */
 #define AMVPT_GROUP_TU 1

@@ -113,6 +113,7 @@ struct KParams {
     uint32_t adapt_pass;  /* the suffix runs paths of the adaptive wavefront (path_seq) */
     uint32_t valid_ray0;  /* !hide_emitters && environment: escaped camera rays count as valid
                            * (mvpath_multi.h:140, mvpath_single.h:98, path.cpp:114) */
+    uint32_t vs_stride;   /* Bufs::vstate: floats between a field's consecutive view slots (the chunk) */
 };
 
 /* SoA streams of one chunk */
@@ -142,8 +143,9 @@ struct Bufs {
     uint32_t *cnt_nee;
     float4 *vreq[3];      /* k_prim_req -> k_vis: (p, bits), (n, ap.x), (emitter point, ap.y) per lane */
     unsigned long long *occ; /* k_vis -> k_mv_primary: occlusion ballots, word (i >> 6) * G + slot */
-    uint4 *vreq_w;        /* groups > 16 views (G = 0 instances): request bits lo / hi, primary view per lane */
-    uint4 *lmask_w[2];    /* groups > 16 views: (valid lo, hi, indirect lo, hi), (wi.z > 0 lo, hi) per slot */
+    uint4 *vreq_w[2];     /* groups > 16 views (G = 0 instances): the lane's visibility-request mask (mstore) */
+    uint4 *lmask_w[6];    /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (two planes each) */
+    float *vstate;        /* runtime groups whose per-view state exceeds LDS: VS_FIELDS x G x vs_stride floats */
 };
 
 /* ------------------------------------------------------------------ */
@@ -1869,14 +1871,49 @@ AD PrimRay primary_raygen(const KParams &P, const DView *V, uint32_t i) {
 }
 /*
  * Group sizes.  G = 2..16 are compile-time instances; G = 0 is the runtime instance for groups
- * of 17..64 views (KParams::G): 64-bit per-view masks kept in their own planes (vreq_w,
- * lmask_w), 64-thread primary blocks (the per-view LDS state grows with G), k_vis waves that
- * walk several slots.
+ * of 17..256 views (KParams::G): 256-bit per-view masks (WMask) kept in their own planes (vreq_w,
+ * lmask_w), 64-thread primary blocks with the per-view state in LDS while it fits in 64 KB and in
+ * a global plane per chunk beyond (Bufs::vstate), k_vis waves that walk several slots.
  */
-constexpr uint32_t kMaxGWide = 64;
+constexpr uint32_t kMaxGWide = 256;
 template <int G> AD int group_size(const KParams &P) { return G ? G : (int) P.G; }
-template <int G> using VMask = typename std::conditional<G == 0, unsigned long long, uint32_t>::type;
-template <int G> AD VMask<G> vbit(int k) { return (VMask<G>) 1 << k; }
+/* per-view bit masks: 32 bits for G <= 16 (bits 16+ carry other fields), four 64-bit words for the
+ * runtime instance (17..256 views), indexed with a wave-uniform view slot k */
+struct WMask {
+    unsigned long long w[4];
+    AD WMask(uint32_t v = 0u) : w{v, 0ull, 0ull, 0ull} {}
+};
+template <int G> using VMask = typename std::conditional<G == 0, WMask, uint32_t>::type;
+AD bool mget(uint32_t m, int k) { return (m >> k) & 1u; }
+AD bool mget(const WMask &m, int k) {
+    const unsigned long long x = k < 128 ? (k < 64 ? m.w[0] : m.w[1]) : (k < 192 ? m.w[2] : m.w[3]);
+    return (x >> (k & 63)) & 1ull;
+}
+AD void mset(uint32_t &m, int k, bool b) { m |= b ? 1u << k : 0u; }
+AD void mset(WMask &m, int k, bool b) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m.w[q] |= (b && (k >> 6) == q) ? 1ull << (k & 63) : 0ull;
+}
+AD void mclr(uint32_t &m, int k) { m &= ~(1u << k); }
+/* a compile-time group's mask in bits 16..31 of a record word (0 for the runtime instance) */
+AD uint32_t mlow16(uint32_t m) { return m << 16; }
+AD uint32_t mlow16(const WMask &) { return 0u; }
+AD void mclr(WMask &m, int k) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m.w[q] &= (k >> 6) == q ? ~(1ull << (k & 63)) : ~0ull;
+}
+/* a runtime-instance mask through two uint4 planes (words 0-1, 2-3) */
+AD void mstore(uint4 *const *pl, uint32_t slot, const WMask &m) {
+    pl[0][slot] = make_uint4((uint32_t) m.w[0], (uint32_t) (m.w[0] >> 32), (uint32_t) m.w[1], (uint32_t) (m.w[1] >> 32));
+    pl[1][slot] = make_uint4((uint32_t) m.w[2], (uint32_t) (m.w[2] >> 32), (uint32_t) m.w[3], (uint32_t) (m.w[3] >> 32));
+}
+AD WMask mload(const uint4 *const *pl, uint32_t slot) {
+    const uint4 a = pl[0][slot], b = pl[1][slot];
+    WMask m;
+    m.w[0] = ((unsigned long long) a.y << 32) | a.x; m.w[1] = ((unsigned long long) a.w << 32) | a.z;
+    m.w[2] = ((unsigned long long) b.y << 32) | b.x; m.w[3] = ((unsigned long long) b.w << 32) | b.z;
+    return m;
+}
 /* view index of group slot k of a lane whose primary view is p_idx (mvpath_multi.h:31-38) */
 AD uint32_t group_view_n(uint32_t Gn, uint32_t p_idx, int k) {
     const uint32_t max_idx = Gn * (p_idx / Gn + 1u), id = p_idx + (uint32_t) k;
@@ -1928,7 +1965,7 @@ AD void prim_requests(const KParams &P, const SceneRef &sc, const DScene &S, con
         const float e1 = pr.rng.next_1d(), e2 = pr.rng.next_1d();
         DSamp ds;
         C3 em_w;
-        if (sample_emitter_direction(sc, si, e1, e2, p_hit && bsdf_smooth, ds, em_w)) bits |= 1u;
+        if (sample_emitter_direction(sc, si, e1, e2, p_hit && bsdf_smooth, ds, em_w)) mset(bits, 0, true);
         (void) pr.rng.next_1d();   /* rand_1 */
         const float r2a = pr.rng.next_1d(), r2b = pr.rng.next_1d();
         BSample bsmp;
@@ -1940,17 +1977,18 @@ AD void prim_requests(const KParams &P, const SceneRef &sc, const DScene &S, con
 #pragma unroll 1
         for (int k = 1; k < Gn; ++k) {
             const Surf r = camera_sample_surface(V[group_view_n((uint32_t) Gn, pr.p_idx, k)], si, reuse, pr.apx, pr.apy);
-            if (r.valid && (r.face == p_face) && r.Jp > 0.f) bits |= vbit<G>(k);
+            mset(bits, k, r.valid && (r.face == p_face) && r.Jp > 0.f);
         }
         p = si.p; n = si.n; dsp = ds.p;
     }
-    if (G == 0) {
-        B.vreq_w[i] = make_uint4((uint32_t) bits, (uint32_t) ((unsigned long long) bits >> 32), pr.p_idx, 0u);
-        bits = 0;
+    uint32_t w0 = 0;
+    if constexpr (G == 0) {
+        mstore(B.vreq_w, i, bits);
+        w0 = pr.p_idx;   /* the runtime instance keeps the primary view in the first plane */
     } else {
-        bits |= (VMask<G>) pr.p_idx << 16;
+        w0 = bits | (pr.p_idx << 16);
     }
-    B.vreq[0][i] = make_float4(p.x, p.y, p.z, bitsf((uint32_t) bits));
+    B.vreq[0][i] = make_float4(p.x, p.y, p.z, bitsf(w0));
     B.vreq[1][i] = make_float4(n.x, n.y, n.z, pr.apx);
     B.vreq[2][i] = make_float4(dsp.x, dsp.y, dsp.z, pr.apy);
 }
@@ -2044,10 +2082,9 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
     uint32_t p_idx = 0;
     if (i < P.chunk_n) {
         a = B.vreq[0][i];
-        if (G == 0) {
-            const uint4 w = B.vreq_w[i];
-            bits = (VMask<G>) (((unsigned long long) w.y << 32) | w.x);
-            p_idx = w.z;
+        if constexpr (G == 0) {
+            bits = mload(B.vreq_w, i);
+            p_idx = fbits(a.w);
         } else {
             bits = fbits(a.w);
             p_idx = (uint32_t) bits >> 16;
@@ -2057,7 +2094,7 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
 #pragma unroll 1
     for (int k = (int) (threadIdx.x >> 6); G ? true : k < Gn; k += vis_waves<G>()) {
         bool occ = false;
-        if (i < P.chunk_n && ((bits >> k) & 1u)) {
+        if (i < P.chunk_n && mget(bits, k)) {
             nn = B.vreq[1][i]; d = B.vreq[2][i];
             const f3 target = k == 0 ? mk(d.x, d.y, d.z) : camera_point(V[group_view_n((uint32_t) Gn, p_idx, k)], nn.w, d.w);
             occ = trace_any<kUni>(sc, spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target));
@@ -2172,8 +2209,12 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
     const uint32_t vs_off = kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u;
     SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPB] */
-    float *const vs = reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
-#define VSF(f, k) vs[((f) * Gn + (k)) * kPB]
+    /* (runtime groups too large for LDS: the chunk's global per-view state, field-major, slot-minor) */
+    const bool vs_glob = G == 0 && B.vstate != nullptr;
+    const uint32_t vs_stride = vs_glob ? P.vs_stride : (uint32_t) kPB;
+    float *const vs = vs_glob ? B.vstate + (blockIdx.x * blockDim.x + threadIdx.x)
+                              : reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
+#define VSF(f, k) vs[((f) * Gn + (k)) * vs_stride]
 #if AMVPT_PRIM_SLOT_ORDER
     /* threads run in slot order (a wave = 64 pixels of one sample, see slot_lane), so every
      * record store of a wave is 64 contiguous slots; the hit and the ballots are read at the
@@ -2197,7 +2238,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
         const float4 hitv = B.hit[i];
         VMask<G> occm = 0;   /* bit k: k_vis found slot k occluded */
 #pragma unroll
-        for (int k = 0; k < Gn; ++k) occm |= occluded_n(B, (uint32_t) Gn, i, k) ? vbit<G>(k) : 0u;
+        for (int k = 0; k < Gn; ++k) mset(occm, k, occluded_n(B, (uint32_t) Gn, i, k));
         const uint32_t n = P.chunk_n;
         const PrimRay pr = primary_raygen(P, V, i);
         Pcg rng = pr.rng;
@@ -2247,7 +2288,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
             float e1 = rng.next_1d(), e2 = rng.next_1d();
             DSamp ds;
             C3 em_w;
-            if (sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w) && (occm & 1u))
+            if (sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w) && mget(occm, 0))
                 occlude_emitter_sample(ds, em_w);
             active_em = active_em && ds.pdf != 0.f;
             direct_l = active_em;
@@ -2280,8 +2321,8 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                 Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
                 VSF(F_PDF, 0) = pdf0; VSF(F_JP, 0) = Jp0;
-                vmask |= p_hit ? 1u : 0u;
-                imask |= p_hit ? 1u : 0u;
+                mset(vmask, 0, p_hit);
+                mset(imask, 0, p_hit);
                 const f3 wo_r0 = reflect_l(si.wi);
                 VMask<G> wpos = p_face ? 1u : 0u;   /* kDiff: bit k = (wi_k.z > 0) */
                 if (!kDiff) {
@@ -2291,7 +2332,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                 }
                 /* view k's wi (kDiff: diffuse eval / pdf read wi only through the sign of its z) */
                 auto wi_of = [&](int k) -> f3 {
-                    if (kDiff) return k == 0 ? si.wi : mk(0.f, 0.f, ((wpos >> k) & 1u) ? 1.f : -1.f);
+                    if (kDiff) return k == 0 ? si.wi : mk(0.f, 0.f, mget(wpos, k) ? 1.f : -1.f);
                     return mk(VSF(F_WX, k), VSF(F_WY, k), VSF(F_WZ, k));
                 };
                 /* pdf_Mat of view k toward view 0 (tv_pdf, camera_selection) */
@@ -2309,7 +2350,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
-                        valid = !((occm >> k) & 1u);
+                        valid = !mget(occm, k);
                     }
                     f3 wik = si.sh.to_local(r.d);
                     float pdf_Mat = 1.f;   /* kDiff: valid implies a diffuse hit (mat_pdf = 1) */
@@ -2321,7 +2362,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                         VSF(F_PDFM, k) = pdfM;
                         pdf_Mat = mat_pdf(wik, pdfM, valid);
                     } else {
-                        wpos |= wik.z > 0.f ? vbit<G>(k) : 0u;
+                        mset(wpos, k, wik.z > 0.f);
                     }
                     float J = r.Jp * iJp0;
                     float pdf_J = J > 1.f ? rcp(J) : J;
@@ -2354,8 +2395,8 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     /* kDiff: a valid view's sample is the primary's (same type, same wo) */
                     (void) replace;
                     n_indir += (float) indirect;
-                    vmask |= valid ? vbit<G>(k) : 0u;
-                    imask |= indirect ? vbit<G>(k) : 0u;
+                    mset(vmask, k, valid);
+                    mset(imask, k, indirect);
                 }
 #if AMVPT_DEFER_SAMPLE
                 if (!kDiff && rep_k > 0) {
@@ -2376,7 +2417,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                 float bp_d = 0.f;
                 if (kDiff) {
                     R0 = emitted;
-                    if (active_em && (vmask & 1u)) R0 = cfma(bsdf_val, emis_mis, emitted);
+                    if (active_em && mget(vmask, 0)) R0 = cfma(bsdf_val, emis_mis, emitted);
                     if (active_em) {
                         C3 ep;
                         float epd;
@@ -2404,7 +2445,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                 }
 #pragma unroll 1
                 for (int k = 0; k < Gn; ++k) {
-                    const bool vk = (vmask >> k) & 1u;
+                    const bool vk = mget(vmask, k);
                     const float Jpk = VSF(F_JP, k);
                     const float iJpk = k == 0 ? iJp0 : (vk ? rcp(Jpk) : 0.f);
                     const f3 wik = wi_of(k);
@@ -2429,7 +2470,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                                 if (j == k) continue;
                                 const float pdf_J = vmin(sqr(pJp[j] * iJpk), 1.f);
                                 const f3 worj = reflect_l(mk(pWx[j], pWy[j], pWz[j]));
-                                const bool vj = (vmask >> j) & 1u;
+                                const bool vj = mget(vmask, j);
 #if AMVPT_PDF_ROW
                                 const float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
                                                                  : tv_pdf_row(row, worj, pdfMk, bd, vj);
@@ -2445,7 +2486,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                             if (j == k) continue;
                             float pdf_J = vmin(sqr(VSF(F_JP, j) * iJpk), 1.f);
                             f3 worj = reflect_l(mk(VSF(F_WX, j), VSF(F_WY, j), VSF(F_WZ, j)));
-                            const bool vj = (vmask >> j) & 1u;
+                            const bool vj = mget(vmask, j);
 #if AMVPT_PDF_ROW
                             float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
                                                        : tv_pdf_row(row, worj, pdfMk, bd, vj);
@@ -2474,11 +2515,11 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     }
                     pdfSum += acc;
                     const float wk = pdf_lk / pdfSum;
-                    bool valid = (imask >> k) & 1u;
+                    bool valid = mget(imask, k);
                     C3 res = c3(0.f), bv = c3(0.f);
                     float bp;
                     if (kDiff) {
-                        bp = (valid && ((wpos >> k) & 1u)) ? bp_d : 0.f;
+                        bp = (valid && mget(wpos, k)) ? bp_d : 0.f;
                     } else {
                         /* result: emission (slot 0) + direct light through this view's BSDF value */
                         res = csel(k == 0, emitted, c3(0.f));
@@ -2504,7 +2545,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     bv = csel(valid, bv, c3(0.f));
                     pdf += bp;
                     n_ind += (float) valid;
-                    if (!valid) imask &= ~vbit<G>(k);
+                    if (!valid) mclr(imask, k);
                     if (k == 0) w0 = wk;
                     else put_view(k, wk, res, bv, (vk ? VF_VALID : 0u) | (valid ? VF_INDIRECT : 0u));
                     if (k == 0 && !kDiff) Bv = bv;   /* slot 0's (bsdf value), stored with slot 0 below */
@@ -2513,16 +2554,16 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                 adapt_mask = p_hit && !flag_null && (n_ind <= 1.f);
                 records_done = true;
             } else {
-                vmask |= p_hit ? 1u : 0u;
+                mset(vmask, 0, p_hit);
 #pragma unroll 1
                 for (int k = 1; k < Gn; ++k) {
                     Surf r = camera_sample_surface(V[view_of(k)], si, reuse, apx, apy);
                     bool valid = r.valid && (r.face == p_face) && r.Jp > 0.f;
                     if (valid) {
                         ++st_vis;
-                        valid = !((occm >> k) & 1u);
+                        valid = !mget(occm, k);
                     }
-                    vmask |= valid ? vbit<G>(k) : 0u;
+                    mset(vmask, k, valid);
                 }
                 float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, direct_pdf);
                 R0 = emitted;
@@ -2553,33 +2594,33 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
             }
             /* p_sample.weight/valid finalisation happens after the suffix */
             if (!p_hit) w0 = 1.f;
-            vmask |= 1u;
+            mset(vmask, 0, true);
         }
         if (!push) B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (P.max_depth == 0) {
             /* no intersection at all: every slot keeps weight 0 and is invalid */
-            vmask = 0;
-            imask = 0;
+            vmask = 0u;
+            imask = 0u;
             w0 = 0.f;
         }
         const uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) |
                                 (should_mis ? LF_MIS : 0u) | (reuse_l ? LF_REUSE : 0u) | (direct_l ? LF_DIRECT : 0u) |
-                                (nf_bits << 8) | (G ? (uint32_t) smask << 16 : 0u);
+                                (nf_bits << 8) | mlow16(smask);
         B.lrec[0][slot] = make_float4(R0.r, R0.g, R0.b, pdfW);
         B.lrec[1][slot] = make_float4(Dp.r, Dp.g, Dp.b, bitsf(lflags));
-        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(G ? (uint32_t) (vmask | (imask << 16)) : 0u));
-        if (G == 0) {
-            const unsigned long long vm = vmask, im = imask, sm = smask;
-            B.lmask_w[0][slot] = make_uint4((uint32_t) vm, (uint32_t) (vm >> 32), (uint32_t) im, (uint32_t) (im >> 32));
-            B.lmask_w[1][slot] = make_uint4((uint32_t) sm, (uint32_t) (sm >> 32), 0u, 0u);
+        B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(mlow16(vmask) >> 16 | mlow16(imask)));
+        if constexpr (G == 0) {   /* planes: valid (0-1), indirect (2-3), wi.z > 0 (4-5) */
+            mstore(B.lmask_w, slot, vmask);
+            mstore(B.lmask_w + 2, slot, imask);
+            mstore(B.lmask_w + 4, slot, smask);
         }
         B.lrec[3][slot] = make_float4(hp.x, hp.y, hp.z, 0.f);
         /* slot 0 (generic: its bsdf value rides in L2), and the views the MIS loop did not write */
-        put_view(0, w0, R0, Bv, (vmask & 1u ? VF_VALID : 0u) | (imask & 1u ? VF_INDIRECT : 0u));
+        put_view(0, w0, R0, Bv, (mget(vmask, 0) ? VF_VALID : 0u) | (mget(imask, 0) ? VF_INDIRECT : 0u));
         if (!records_done) {
 #pragma unroll 1
             for (int k = 1; k < Gn; ++k)
-                put_view(k, P.max_depth != 0 ? 1.f : 0.f, c3(0.f), c3(0.f), ((vmask >> k) & 1u) ? VF_VALID : 0u);
+                put_view(k, P.max_depth != 0 ? 1.f : 0.f, c3(0.f), c3(0.f), (mget(vmask, k)) ? VF_VALID : 0u);
         }
     }
     const uint32_t qslot = push_slot(push, B.cnt_out, B.qcap);
@@ -2625,12 +2666,11 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     if (ok) { l0 = B.lrec[0][slot]; l1 = B.lrec[1][slot]; l2 = B.lrec[2][slot]; l3 = B.lrec[3][slot]; lo = B.lane_out[slot]; }
     const int Gn = group_size<G>(P);
     const uint32_t lflags = fbits(l1.w);
-    VMask<G> vmask = fbits(l2.w) & 0xffffu, imask = fbits(l2.w) >> 16, smask = lflags >> 16;
-    if (G == 0 && ok) {
-        const uint4 m0 = B.lmask_w[0][slot], m1 = B.lmask_w[1][slot];
-        vmask = (VMask<G>) (((unsigned long long) m0.y << 32) | m0.x);
-        imask = (VMask<G>) (((unsigned long long) m0.w << 32) | m0.z);
-        smask = (VMask<G>) (((unsigned long long) m1.y << 32) | m1.x);
+    VMask<G> vmask = 0u, imask = 0u, smask = 0u;
+    if constexpr (G == 0) {
+        if (ok) { vmask = mload(B.lmask_w, slot); imask = mload(B.lmask_w + 2, slot); smask = mload(B.lmask_w + 4, slot); }
+    } else {
+        vmask = fbits(l2.w) & 0xffffu; imask = fbits(l2.w) >> 16; smask = lflags >> 16;
     }
     const float qnan = __builtin_nanf("");
     /* cfma(0, emis_mis, 0) of a valid view whose wi.z <= 0 (kDiff, see k_mv_primary) */
@@ -2667,7 +2707,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     for (int k = 0; k < Gn; ++k) {
         /* a view no lane of the wave splats into: no reprojection, no put (all-diffuse records carry
          * the valid bits in the lane record; records / debug mode write every view's entry) */
-        if (AMVPT_SPLAT_SKIP && kDiff && k > 0 && !P.record && !P.debug && !wave_any(ok && ((vmask >> k) & 1u))) continue;
+        if (AMVPT_SPLAT_SKIP && kDiff && k > 0 && !P.record && !P.debug && !wave_any(ok && (mget(vmask, k)))) continue;
         const size_t o = (size_t) k * n + slot;
         float weight = 0.f;
         bool valid = false;
@@ -2689,10 +2729,10 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         if (ok) {
             if (kDiff) {
                 weight = vw[o];
-                valid = (vmask >> k) & 1u;
+                valid = mget(vmask, k);
                 if (mis) {
-                    result = k == 0 ? R0 : csel(direct && valid, csel((smask >> k) & 1u, Dp, Dn), c3(0.f));
-                    if ((imask >> k) & 1u) result = cfma(Bv * pdfW, indirect, result);
+                    result = k == 0 ? R0 : csel(direct && valid, csel(mget(smask, k), Dp, Dn), c3(0.f));
+                    if (mget(imask, k)) result = cfma(Bv * pdfW, indirect, result);
                 } else {
                     result = res0;
                 }
@@ -2872,7 +2912,7 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
                            const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T) {
     constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
     const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
-    const size_t lds_view = (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
+    const size_t lds_view = B.vstate ? 0u : (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
     if (uni && ab_knobs().fuse_prim) {
         T.begin(AMVPT_K_PRIM_HIT, st);
         if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
@@ -3093,7 +3133,7 @@ typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams 
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const DView *, const Bufs &, bool);
 /* group sizes 2..16: the per-view bit masks (k_prim_req's request bits below the view index at
  * bit 16, k_mv_primary's valid / indirect flags at bits k and 16 + k) hold 16 views; entry 0 is
- * the runtime instance for 17..64 views (64-bit masks in vreq_w / lmask_w) */
+ * the runtime instance for 17..256 views (256-bit masks in vreq_w / lmask_w) */
 static const primary_fn kPrimary[] = {launch_primary<0>, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>,
                                       launch_primary<9>, launch_primary<10>, launch_primary<11>, launch_primary<12>,
@@ -3146,7 +3186,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool is_mv = Pp.integrator == AMVPT_INTEGRATOR_MVPATH;
     const bool reuse = is_mv && Pp.sa_reuse && Pp.n_views > 1 && Pp.reuse_count != 1;
     const uint32_t G = reuse ? group_size(Pp) : 1;
-    if (G > kMaxGWide) { set_error("amvpt_render: group size > 64 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+    if (G > kMaxGWide) { set_error("amvpt_render: group size > 256 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
     if (!is_mv && n_passes > 1) { set_error("path: more than 2^32 lanes per frame"); return AMVPT_ERR_UNSUPPORTED; }
     if (Pp.multisensor && (Pp.grid_x == 0 || Pp.grid_y == 0 || Pp.film_width % Pp.grid_x || Pp.film_height % Pp.grid_y)) {
@@ -3285,16 +3325,22 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     /* lane arena: queues (2 x 5 x 16 B), lane_out + hit (32 B), NEE queue (52 B), visibility requests
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
-    const bool wide = G > kMaxG;   /* the runtime group-size instance (64-bit view masks) */
+    const bool wide = G > kMaxG;   /* the runtime group-size instance (256-bit view masks) */
     const bool diff_rec = scene->all_diffuse && diffuse_spec && !wide;   /* kDiff instances, compact view records */
+    /* the runtime instance's per-view state: LDS (64-thread blocks) while it fits, else a global
+     * VS_FIELDS x G float plane per lane */
+    const size_t lds_tab_views = (AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views))
+                                     ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;
+    const bool vs_global = wide && lds_tab_views + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 65536;
     const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8 +
-                            (wide ? 48 : 0);
+                            (wide ? 128 : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
     if (chunk_max == 0) {
         chunk_max = 1ull << 25;
-        while (chunk_max > (1ull << 23) && chunk_max * per_lane > (24ull << 30)) chunk_max >>= 1;
+        while (chunk_max > (1ull << 16) && chunk_max * per_lane > (24ull << 30)) chunk_max >>= 1;
     }
     const uint64_t chunk = std::min<uint64_t>(chunk_max, span);
+    P.vs_stride = (uint32_t) chunk;
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
@@ -3399,8 +3445,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.qcap = qcap;
         B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : 32) * G * chunk);
         if (wide) {
-            B.vreq_w = (uint4 *) carve(16 * chunk);
-            for (int k = 0; k < 2; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
+            for (int k = 0; k < 2; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
+            for (int k = 0; k < 6; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
+            if (vs_global) B.vstate = (float *) carve((size_t) VS_FIELDS * 4 * G * chunk);
         }
         B.film = film;
         B.records = records;
@@ -3426,10 +3473,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
-    if (wide && lds_prim + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 163840) {
-        set_error("amvpt_render: per-view LDS state of this group size exceeds 160 KB");
-        return AMVPT_ERR_UNSUPPORTED;
-    }
     KTimer T;
     T.init(counters != nullptr);
     HIPCHK(T.err);

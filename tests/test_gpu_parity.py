@@ -345,17 +345,32 @@ def test_large_view_groups(gpu_ready, amvpt_mod, oracle, gx, gy, reuse):
 
 @pytest.mark.parametrize("scene,gx,gy,reuse,res", [
     ("cbox_grid.xml", 8, 4, 32, 12),    # the C5 light-field array as ONE group of 32 views
-    ("cbox_grid.xml", 8, 8, 64, 8),     # the largest group (64-bit view masks)
+    ("cbox_grid.xml", 8, 8, 64, 8),     # 64 views: per-view state past 64 KB of LDS -> global plane
     ("veach_grid.xml", 5, 4, 20, 12),   # glossy: per-view BSDF sampling + G x (G-1) BSDF pdfs
-], ids=["cbox_g32", "cbox_g64", "veach_g20"])
+    ("cbox_grid.xml", 16, 8, 128, 6),   # 128 views: masks beyond one 64-bit word
+    ("cbox_grid.xml", 16, 16, 256, 4),  # 256 views: the largest group (four mask words)
+    ("veach_grid.xml", 10, 8, 80, 6),   # glossy, 80 views, global per-view state
+], ids=["cbox_g32", "cbox_g64", "veach_g20", "cbox_g128", "cbox_g256", "veach_g80"])
 def test_groups_above_16_views(gpu_ready, amvpt_mod, oracle, scene, gx, gy, reuse, res):
-    """Groups of 17..64 views (the reference has no cap, mvpath.cpp:192-217):
-    the runtime group-size instance with 64-bit view masks (vreq_w / lmask_w planes), 16-wave
-    k_vis blocks walking several slots each, 64-thread k_mv_primary blocks."""
+    """Groups of 17..256 views (the reference has no cap,
+    mvpath.cpp:192-217): the runtime group-size instance with 256-bit view masks (WMask in the
+    vreq_w / lmask_w planes), 16-wave k_vis blocks walking several slots each, 64-thread
+    k_mv_primary blocks whose per-view state leaves LDS for a global plane past 64 KB."""
     s = amvpt_mod.load_file(os.path.join(SCENES, scene), res=res, spp=16, gx=gx, gy=gy, reuse=reuse)
     sd, vd, p = s.describe(0, 0, 0)
     assert oracle.plan(p)["group"] == reuse
     _check(amvpt_mod, oracle, s)
+
+
+def test_group_above_256_views_refused(gpu_ready, amvpt_mod):
+    """Groups past 256 views (four mask words) fail loudly instead of rendering wrong."""
+    torch = _torch()
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=2, spp=16, gx=20, gy=16, reuse=320)
+    sd, vd, p = s.describe(0, 0, 0)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    with pytest.raises(Exception, match="256"):
+        dev.render(vd, p, film.data_ptr())
 
 
 CBOX_ENV = os.path.join(SCENES, "cbox_env.xml")
@@ -395,13 +410,21 @@ def test_veach_weighted_emitter_sampling(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
-@pytest.mark.parametrize("adaptive", [0, 2])
-def test_fused_suffix_matches_wavefront_suffix(gpu_ready, amvpt_mod, oracle, adaptive):
+SMALL_MESHLIGHT = dict(ball_file="meshes/quad_fan.obj", ring_type="obj", ring_file="meshes/quad_fan.obj")
+
+
+@pytest.mark.parametrize("scene,adaptive", [("cbox", 0), ("cbox", 2), ("meshlight", 0)])
+def test_fused_suffix_matches_wavefront_suffix(gpu_ready, amvpt_mod, oracle, scene, adaptive):
     """k_suffix_fused (paths in registers, brute-force scenes) vs the per-depth k_extend / k_bounce
     wavefronts (AMVPT_OPT_WAVEFRONT_SUFFIX) on the same lanes: records bit-identical, the same vertex and
-    shadow-ray counts, and each launch path actually taken (kernel launch counters)."""
+    shadow-ray counts, and each launch path actually taken (kernel launch counters).  `meshlight`: the
+    27-primitive mesh-light box (a 12-triangle cube light and a 5-triangle polygon mesh light), so the
+    fused suffix samples and prices mesh emitters (Mesh::sample_position, mesh.cpp:765-816)."""
     torch = _torch()
-    s = amvpt_mod.load_file(CBOX, res=32, spp=32, gx=4, gy=2, reuse=8, adaptive=adaptive)
+    if scene == "meshlight":
+        s = amvpt_mod.load_file(MESHLIGHT, res=32, spp=32, gx=4, gy=2, reuse=8, **SMALL_MESHLIGHT)
+    else:
+        s = amvpt_mod.load_file(CBOX, res=32, spp=32, gx=4, gy=2, reuse=8, adaptive=adaptive)
     sd, vd, p = s.describe(0, 0, 0)
     plan = oracle.plan(p)
     out = {}
@@ -452,4 +475,20 @@ def test_mesh_area_emitters(gpu_ready, amvpt_mod, oracle, defines):
     (interpolated vertex normal on the icosphere, face normal on the flat cube);
     Shape::pdf_direction (shape.cpp:379-390) prices emitter hits by 1 / surface area."""
     s = amvpt_mod.load_file(MESHLIGHT, **defines)
+    _check(amvpt_mod, oracle, s)
+
+
+def test_small_mesh_light_scene_takes_fused_suffix(gpu_ready, amvpt_mod, oracle):
+    """The 27-primitive mesh-light box runs the brute-force walks and k_suffix_fused (launch counters)
+    and its lane records are bit-identical to the oracle's."""
+    torch = _torch()
+    s = amvpt_mod.load_file(MESHLIGHT, res=24, spp=16, gx=4, gy=2, reuse=8, **SMALL_MESHLIGHT)
+    sd, vd, p = s.describe(0, 0, 0)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    cnt = amvpt_mod.Counters()
+    dev.render_ex(vd, p, film.data_ptr(), counters=cnt)
+    torch.cuda.synchronize()
+    c = cnt.as_dict()
+    assert c["kernel_launches"]["k_suffix"] > 0 and c["kernel_launches"]["k_extend"] == 0
     _check(amvpt_mod, oracle, s)
