@@ -1725,6 +1725,13 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
  * are the same operations in the same order as the k_extend / k_bounce wavefronts.
  * The work counters (cnt_out of the queue pair) are zeroed by the host before the launch.
  */
+#ifndef AMVPT_FUSE_BVH
+/* 1: BVH scenes run k_suffix_fused too (per-lane / wave-uniform walks inside the fused loop).  Off:
+ * on the 3.6 k-triangle mesh it measured 519 vs 608 Msamples/s for the wavefront suffix (r03m) --
+ * the walks, latency-bound on dependent node loads, lose more at the fused kernel's register budget
+ * (80 VGPRs + 144 B of spills) than the fused loop saves in state traffic and launches */
+#define AMVPT_FUSE_BVH 0
+#endif
 #ifndef AMVPT_FUSED_BLOCKS
 /* blocks per queue partition (x kQParts blocks of 256 threads), more than are resident at once:
  * blocks that start late find their partition partly drained, which evens out the tail
@@ -1733,7 +1740,8 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
 #define AMVPT_FUSED_BLOCKS 24
 #endif
 #ifndef AMVPT_FUSED_WAVES
-/* 6 waves/SIMD (80 VGPRs, 24 B of spills): suffix 146.4 -> 143.2 ms per config-M frame; 4 waves 157.8 (r02fc) */
+/* 6 waves/SIMD (80 VGPRs, 68 B of spills): suffix 146.4 -> 143.2 ms per config-M frame; 4 waves 157.8 (r02fc);
+ * 5 waves (no spills) 1480 vs 1510 Msamples/s at 6 (r03m) */
 #define AMVPT_FUSED_WAVES 6
 #endif
 template <bool kTab, bool kDiff, int kW>
@@ -1762,7 +1770,9 @@ __global__ void __launch_bounds__(256, AMVPT_FUSED_WAVES) k_suffix_fused(KParams
             }
         }
         if (!wave_any(live)) break;
-        const Hit h = walk_closest<kW>(sc, s.ray);
+        constexpr bool kBruteW = kW == WALK_BRUTE || kW == WALK_BRUTE_NS;
+        Hit h{kInf, 0.f, 0.f, -1};
+        if (kBruteW || live) h = walk_closest<kW>(sc, s.ray);   /* brute force: every lane of the wave walks */
         bool keep = false, nee = false;
         Ray shr;
         f3 nee_to;
@@ -1772,7 +1782,9 @@ __global__ void __launch_bounds__(256, AMVPT_FUSED_WAVES) k_suffix_fused(KParams
             keep = bounce_vertex<kDiff>(P, S, sc, s, rng, h, nee, shr, nee_to, nee_thr, nee_c);
         }
         shadows += nee ? 1 : 0;
-        const bool occluded = brute_any<kW == WALK_BRUTE>(sc, shr, !nee);
+        bool occluded = true;
+        if constexpr (kBruteW) occluded = brute_any<kW == WALK_BRUTE>(sc, shr, !nee);
+        else if (nee) occluded = walk_any<kW>(sc, shr);
         if (nee && !occluded) s.res = cfma(nee_thr, nee_c, s.res);
         if (live && !keep) {
             B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
@@ -3101,7 +3113,12 @@ static void launch_suffix_fused(bool tab, bool diff, int walk, dim3 grid, size_t
     do {                                                                                                              \
         if (walk == WALK_BRUTE_NS)                                                                                    \
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, S, B); \
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_BRUTE>), grid, dim3(256), lds, st, P, S, B); \
+        else if (walk == WALK_BRUTE)                                                                                  \
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_BRUTE>), grid, dim3(256), lds, st, P, S, B); \
+        else if (AMVPT_FUSE_BVH && walk == WALK_UNI)                                                                  \
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_UNI>), grid, dim3(256), lds, st, P, S, B); \
+        else if (AMVPT_FUSE_BVH)                                                                                      \
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_suffix_fused<T_, D_, WALK_LANE>), grid, dim3(256), lds, st, P, S, B); \
     } while (0)
     if (tab && diff) AMVPT_FUSED(true, true);
     else if (tab) AMVPT_FUSED(true, false);
@@ -3468,7 +3485,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool fuse_nee = (walk == WALK_BRUTE || walk == WALK_BRUTE_NS) && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE);
     /* the whole suffix in one launch, paths in registers (brute-force walks with fused NEE;
      * AMVPT_OPT_WAVEFRONT_SUFFIX keeps the per-depth k_extend / k_bounce wavefronts) */
-    const bool fuse_suffix = fuse_nee && K.fuse_suffix && !(opts.flags & AMVPT_OPT_WAVEFRONT_SUFFIX);
+    const bool fuse_suffix = (fuse_nee || (AMVPT_FUSE_BVH && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE))) &&
+                             K.fuse_suffix && !(opts.flags & AMVPT_OPT_WAVEFRONT_SUFFIX);
     const uint32_t fused_blocks = K.fused_blocks;
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
