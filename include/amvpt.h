@@ -359,7 +359,8 @@ enum {
     /* amvpt_render_opts.flags: kernel-path selection for tests and A/B runs (results are identical) */
     AMVPT_OPT_GENERIC_KERNELS = 1u,   /* no all-diffuse kernel instances (kDiff) */
     AMVPT_OPT_WAVEFRONT_SUFFIX = 2u,  /* per-depth k_extend / k_bounce instead of k_suffix_fused */
-    AMVPT_OPT_SPLIT_NEE = 4u          /* suffix NEE rays in k_shadow instead of inside k_bounce */
+    AMVPT_OPT_SPLIT_NEE = 4u,         /* suffix NEE rays in k_shadow instead of inside k_bounce */
+    AMVPT_OPT_ONE_STREAM = 8u         /* every chunk on the render stream (no second chunk stream) */
 };
 typedef struct amvpt_render_opts {
     uint64_t chunk_lanes;             /* 0: automatic (see amvpt_set_chunk_lanes) */

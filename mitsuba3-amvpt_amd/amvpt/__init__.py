@@ -113,7 +113,7 @@ class RenderOpts(ctypes.Structure):
 
 
 # amvpt_render_opts.flags (results are identical; kernel-path selection for tests / A/B)
-OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE = 1, 2, 4
+OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE, OPT_ONE_STREAM = 1, 2, 4, 8
 
 
 def wrap_run_exchange(fn):
@@ -342,10 +342,15 @@ def plan(params):
     return spp.value, spl.value, npass.value, lanes.value
 
 
+# process-wide defaults of the legacy setters, also the defaults of render_ex's per-call options
+_DEFAULTS = {"chunk_lanes": 0, "traversal": 0}
+
+
 def set_traversal(mode):
     """BVH walk: 0 auto (brute force for tiny scenes), 1 wave-uniform, 2 per-lane (amvpt_set_traversal)."""
     L = hip_lib()
     _check(L.amvpt_set_traversal(u32(mode)), L)
+    _DEFAULTS["traversal"] = int(mode)
 
 
 def set_bvh_build(max_leaf_prims=4, traversal_cost=0.0):
@@ -357,6 +362,7 @@ def set_bvh_build(max_leaf_prims=4, traversal_cost=0.0):
 def set_chunk_lanes(n):
     L = hip_lib()
     _check(L.amvpt_set_chunk_lanes(u64(n)), L)
+    _DEFAULTS["chunk_lanes"] = int(n)
 
 
 # amvpt_exchange_fn: (ctx, local_count, *prefix, *total) -> 0 on success
@@ -451,13 +457,15 @@ class DeviceScene:
         return counters
 
     def render_ex(self, views_ptr, params, film_ptr, lanes=None, window=None, overflow_ptr=None,
-                  overflow_capacity=0, stream=None, counters=None, chunk_lanes=0, traversal=0, flags=0,
+                  overflow_capacity=0, stream=None, counters=None, chunk_lanes=None, traversal=None, flags=0,
                   exchange=None, records_ptr=None, record_pass=0):
         """amvpt_render_ex: `lanes` a LaneSet (None: the whole pass), `window` (x0, y0, width, height)
         of the quilt the film holds (None: the whole quilt), per-call options; `exchange` is
         `fn(run_lane_begin, run_count) -> (run_prefix, total)` (see amvpt.dist.run_exchange)."""
         if lanes is None:
             lanes = LaneSet(0, 2 ** 64 - 1, 0, 0, 0, 0)
+        chunk_lanes = _DEFAULTS["chunk_lanes"] if chunk_lanes is None else chunk_lanes
+        traversal = _DEFAULTS["traversal"] if traversal is None else traversal
         x0, y0, w, h = window if window is not None else (0, 0, params.film_width, params.film_height)
         fw = FilmWindow(ctypes.c_void_p(film_ptr), x0, y0, w, h, ctypes.c_void_p(overflow_ptr or 0),
                         overflow_capacity)

@@ -3363,10 +3363,24 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
     const uint64_t qlen = (uint64_t) qcap * kQParts;
     const size_t stats_bytes = (size_t) kStats * kStatShards * 8, cnt_bytes = (size_t) 3 * kQParts * kCntStride * 4;
-    /* chunks alternate between two buffer sets on two streams (the render stream and the arena's side
-     * stream): one chunk's kernels fill the CUs the other's leave idle (low-occupancy primary
-     * shading, launch tails) */
-    const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk) ? 2 : 1;
+    const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
+    const bool uni = scene_uniform(scene->dev.n_nodes, trav);
+    /* suffix walk: brute force for tiny scenes in auto mode */
+    int walk = uni ? WALK_UNI : WALK_LANE;
+    if (uni && trav == 0u && K.brute && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
+    const bool diff = diff_rec;                                                                           /* kDiff instances */
+    /* NEE traced inside k_bounce (brute-force walks; AMVPT_OPT_SPLIT_NEE keeps k_shadow) */
+    const bool fuse_nee = (walk == WALK_BRUTE || walk == WALK_BRUTE_NS) && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE);
+    /* the whole suffix in one launch, paths in registers (brute-force walks with fused NEE;
+     * AMVPT_OPT_WAVEFRONT_SUFFIX keeps the per-depth k_extend / k_bounce wavefronts) */
+    const bool fuse_suffix = (fuse_nee || (AMVPT_FUSE_BVH && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE))) &&
+                             K.fuse_suffix && !(opts.flags & AMVPT_OPT_WAVEFRONT_SUFFIX);
+    /* chunks of the per-depth wavefront suffix (BVH scenes) alternate between two buffer sets on two
+     * streams (the render stream and the arena's side stream): one chunk's short deep-bounce launches
+     * and tails leave CUs idle that the other chunk's kernels fill (mesh 550 -> 599 Msamples/s).  The
+     * fused-suffix scenes gain 0.0-0.5 % (r03i) and keep one stream, so their per-kernel HIP-event
+     * times are not overlapped (AMVPT_OPT_ONE_STREAM forces one stream everywhere) */
+    const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && !fuse_suffix && !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? 2 : 1;
     const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
     const size_t need = views_bytes + stats_bytes + set_bytes * n_sets;
     int dev = 0;
@@ -3475,18 +3489,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     }
 
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
-    const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
-    const bool uni = scene_uniform(scene->dev.n_nodes, trav);
-    /* suffix walk: brute force for tiny scenes in auto mode */
-    int walk = uni ? WALK_UNI : WALK_LANE;
-    if (uni && trav == 0u && K.brute && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
-    const bool diff = diff_rec;                                                                           /* kDiff instances */
-    /* NEE traced inside k_bounce (brute-force walks; AMVPT_OPT_SPLIT_NEE keeps k_shadow) */
-    const bool fuse_nee = (walk == WALK_BRUTE || walk == WALK_BRUTE_NS) && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE);
-    /* the whole suffix in one launch, paths in registers (brute-force walks with fused NEE;
-     * AMVPT_OPT_WAVEFRONT_SUFFIX keeps the per-depth k_extend / k_bounce wavefronts) */
-    const bool fuse_suffix = (fuse_nee || (AMVPT_FUSE_BVH && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE))) &&
-                             K.fuse_suffix && !(opts.flags & AMVPT_OPT_WAVEFRONT_SUFFIX);
     const uint32_t fused_blocks = K.fused_blocks;
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */

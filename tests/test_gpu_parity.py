@@ -333,6 +333,21 @@ def test_many_chunks_per_pass(gpu_ready, amvpt_mod, oracle, chunk):
         amvpt_mod.set_chunk_lanes(0)   # back to the automatic chunk
 
 
+def test_two_chunk_streams(gpu_ready, amvpt_mod, oracle):
+    """BVH scenes (per-depth wavefront suffix) alternate chunks between two buffer sets on two streams:
+    with many small chunks on both streams the records stay bit-identical to the oracle, as they are
+    with every chunk on the render stream (AMVPT_OPT_ONE_STREAM)."""
+    amvpt_mod.set_chunk_lanes(2048)
+    try:
+        s = amvpt_mod.load_file(MESH, res=16, spp=16, gx=4, gy=2, reuse=8)
+        sd, vd, p = s.describe(0, 0, 0)
+        assert oracle.plan(p)["lanes"] > 8 * 2048
+        _check(amvpt_mod, oracle, s)
+        _check(amvpt_mod, oracle, s, flags=amvpt_mod.OPT_ONE_STREAM)
+    finally:
+        amvpt_mod.set_chunk_lanes(0)
+
+
 @pytest.mark.parametrize("gx,gy,reuse", [(4, 4, 16), (4, 3, 12)], ids=["g16", "g12"])
 def test_large_view_groups(gpu_ready, amvpt_mod, oracle, gx, gy, reuse):
     """Group sizes above 8 (reuse_count = n_views = 12 or 16): camera selection over up to 15
