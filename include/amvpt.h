@@ -360,7 +360,11 @@ enum {
     AMVPT_OPT_GENERIC_KERNELS = 1u,   /* no all-diffuse kernel instances (kDiff) */
     AMVPT_OPT_WAVEFRONT_SUFFIX = 2u,  /* per-depth k_extend / k_bounce instead of k_suffix_fused */
     AMVPT_OPT_SPLIT_NEE = 4u,         /* suffix NEE rays in k_shadow instead of inside k_bounce */
-    AMVPT_OPT_ONE_STREAM = 8u         /* every chunk on the render stream (no second chunk stream) */
+    AMVPT_OPT_ONE_STREAM = 8u,        /* every chunk on the render stream (no second chunk stream) */
+    AMVPT_OPT_DETERMINISTIC = 16u     /* bitwise-reproducible film: splats summed as 32.32 fixed point with
+                                       * integer atomics (order-independent), added to the film once at the
+                                       * end; non-finite splat values are dropped (nonfinite_samples counts
+                                       * them); needs a whole-quilt film window */
 };
 typedef struct amvpt_render_opts {
     uint64_t chunk_lanes;             /* 0: automatic (see amvpt_set_chunk_lanes) */

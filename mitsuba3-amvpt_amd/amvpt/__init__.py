@@ -113,7 +113,7 @@ class RenderOpts(ctypes.Structure):
 
 
 # amvpt_render_opts.flags (results are identical; kernel-path selection for tests / A/B)
-OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE, OPT_ONE_STREAM = 1, 2, 4, 8
+OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE, OPT_ONE_STREAM, OPT_DETERMINISTIC = 1, 2, 4, 8, 16
 
 
 def wrap_run_exchange(fn):

@@ -110,10 +110,13 @@ struct KParams {
     uint32_t chunk_n;
     uint32_t record;      /* write per-lane splat records */
     uint32_t row_splat;   /* row-reduced splat (row_put): lanes in pixel-major order, see slot_lane */
+    uint32_t tile_w;      /* != 0: row-splat slots run over 4 x 4 pixel tiles of a tile_w-pixel-wide quilt */
     uint32_t adapt_pass;  /* the suffix runs paths of the adaptive wavefront (path_seq) */
     uint32_t valid_ray0;  /* !hide_emitters && environment: escaped camera rays count as valid
                            * (mvpath_multi.h:140, mvpath_single.h:98, path.cpp:114) */
     uint32_t vs_stride;   /* Bufs::vstate: floats between a field's consecutive view slots (the chunk) */
+    unsigned long long *film_fx;   /* deterministic mode: 32.32 fixed-point shadow of the film (else null) */
+    float *film_base;              /* the film the shadow mirrors (film_fx index = film float index) */
 };
 
 /* SoA streams of one chunk */
@@ -616,7 +619,22 @@ AD f3 camera_point(const DView &v, float apx, float apy) {
 /* Film                                                               */
 /* ------------------------------------------------------------------ */
 
-AD void film_add(float *p, float v) { atomicAdd(p, v); }
+/*
+ * One film float += v.  Deterministic mode (AMVPT_OPT_DETERMINISTIC, KParams::film_fx): the value goes to
+ * the same cell of a 32.32 fixed-point shadow film with an integer atomic -- integer sums do not depend
+ * on the order the waves arrive in, so the film is bitwise reproducible (imageblock.cpp:119-133's
+ * accumulation, resolved once per render by k_fixed_resolve).  Non-finite values are dropped there.
+ */
+constexpr double kFixScale = 4294967296.0, kFixLimit = 2147483647.0;
+AD void film_add(const KParams &P, float *p, float v) {
+    if (P.film_fx) {
+        const double d = (double) v * kFixScale;
+        if (!(fabs(d) < kFixLimit * kFixScale)) return;   /* NaN / Inf / out of range */
+        atomicAdd(P.film_fx + (p - P.film_base), (unsigned long long) (long long) __builtin_rint(d));
+        return;
+    }
+    atomicAdd(p, v);
+}
 
 /*
  * Film window (amvpt_film_window).  The film buffer holds the quilt rectangle [fx0, fx0 + fw) x
@@ -645,7 +663,7 @@ AD void overflow_push(const KParams &P, uint64_t idx, float v) {
 }
 /* one film float of quilt cell (x, y), channel k: the window, else the overflow list */
 template <bool kWin = true> AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float v) {
-    if (in_window<kWin>(P, x, y)) film_add(film_cell<kWin>(P, film, x, y, k), v);
+    if (in_window<kWin>(P, x, y)) film_add(P, film_cell<kWin>(P, film, x, y, k), v);
     else overflow_push(P, ((uint64_t) (uint32_t) y * P.W + (uint32_t) x) * P.C + (uint32_t) k, v);
 }
 
@@ -932,7 +950,7 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
             const float v = (float) d;
 #endif
             if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
-                if (inside) film_add(film0 + (size_t) cy * film_row + r, v);
+                if (inside) film_add(P, film0 + (size_t) cy * film_row + r, v);
                 else film_cell_add(P, film, w.bx0 + cx, w.by0 + cy, k, v);
             }
         }
@@ -984,6 +1002,30 @@ AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn
 #pragma unroll
                 for (int k = 0; k < C; ++k) film_cell_add<kWin>(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
             }
+        }
+    }
+}
+
+/*
+ * Deterministic mode's put: every cell of the sample's footprint straight into the fixed-point film,
+ * value * (wx * wy) per cell as ImageBlock::put forms it (imageblock.cpp:265-558) -- no LDS window and
+ * no row reduction, so no float sum depends on which lanes share a wave, a chunk or a stream.
+ */
+template <int C, bool kWin = true>
+AD void direct_put(const KParams &P, float *film, float px, float py, const float *vals, bool valid, bool coalesce) {
+    if (!valid) return;
+    const Foot f = footprint(P, px, py, coalesce);
+    if (!f.ok) return;
+    for (int ys = 0; ys < f.ny; ++ys) {
+        const int y = f.y0 + ys;
+        if (y < 0) continue;
+        const float wyv = P.box ? 1.f : gaussian_eval(P.filt, f.ry + (float) ys);
+        for (int xs = 0; xs < f.nx; ++xs) {
+            const int x = f.x0 + xs;
+            if (x < 0) continue;
+            const float w = (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs)) * wyv;
+#pragma unroll
+            for (int k = 0; k < C; ++k) film_cell_add<kWin>(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
         }
     }
 }
@@ -1154,7 +1196,7 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
             const float v = (float) d;
 #endif
             if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
-                if (inside) film_add(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
+                if (inside) film_add(P, film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
                 else film_cell_add<kWin>(P, film, w.bx0 + cx, w.by0 + cy, k, v);
             }
         }
@@ -1234,7 +1276,23 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
  * use the identity map.  The map is a bijection on [0, chunk_n).
  */
 constexpr int kSplatSplit = kSplatSuper / kSplatBlock;
+/*
+ * Tiled slot order (KParams::tile_w, 16 samples per pixel and pass): slot block b of 256 = the 4 x 4
+ * pixel tile b of the chunk's rows (tile rows of tile_w / 4 tiles), a wave = one pixel row of the
+ * tile (64 consecutive lanes), a DPP row = one pixel.  A splat block's footprints then cover ~8 x 8
+ * cells instead of 20 x 5, so a block-wide window flushes fewer film cells per sample.
+ */
+AD uint32_t tile_slot_lane(const KParams &P, uint32_t slot) {
+    const uint32_t b = slot >> 8, t = slot & 255u, tpr = P.tile_w >> 2;
+    const uint32_t trow = b / tpr, tcol = b - trow * tpr, pt = t >> 4;
+    return ((trow * 4u + (pt >> 2)) * P.tile_w + tcol * 4u + (pt & 3u)) * 16u + (t & 15u);
+}
+AD uint32_t tile_lane_slot(const KParams &P, uint32_t lane) {
+    const uint32_t pix = lane >> 4, y = pix / P.tile_w, x = pix - y * P.tile_w, tpr = P.tile_w >> 2;
+    return (((y >> 2) * tpr + (x >> 2)) << 8) | ((((y & 3u) << 2) | (x & 3u)) << 4) | (lane & 15u);
+}
 AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
+    if (P.tile_w) return tile_slot_lane(P, slot);
     if (P.row_splat) return slot;   /* pixel-major: a 16-lane row = 16 samples of one pixel (row_put) */
     const uint32_t super = slot / (uint32_t) kSplatSuper, within = slot % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
@@ -1249,6 +1307,7 @@ AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
 }
 /* inverse of slot_lane */
 AD uint32_t lane_slot(const KParams &P, uint32_t lane) {
+    if (P.tile_w) return tile_lane_slot(P, lane);
     if (P.row_splat) return lane;
     const uint32_t super = lane / (uint32_t) kSplatSuper, off = lane % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
@@ -1828,7 +1887,8 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
     }
     unsigned long long nonfinite = 0, negative = 0;
     check_sample(P, vals, ok, nonfinite, negative);
-    block_put<C>(P, B.film, L, 0, putx, puty, vals, ok, P.coalesce_single != 0);
+    if (P.film_fx) direct_put<C>(P, B.film, putx, puty, vals, ok, P.coalesce_single != 0);
+    else block_put<C>(P, B.film, L, 0, putx, puty, vals, ok, P.coalesce_single != 0);
     if (B.stats) { stat_add(B.stats, 6, nonfinite); stat_add(B.stats, 7, negative); }
 }
 
@@ -1850,7 +1910,8 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_adapt(KParams P, Bufs B) 
     }
     unsigned long long nonfinite = 0, negative = 0;
     check_sample(P, vals, ok, nonfinite, negative);
-    block_put<C>(P, B.film, L, 0, sx, sy, vals, ok, false);
+    if (P.film_fx) direct_put<C>(P, B.film, sx, sy, vals, ok, false);
+    else block_put<C>(P, B.film, L, 0, sx, sy, vals, ok, false);
     if (B.stats) { stat_add(B.stats, 6, nonfinite); stat_add(B.stats, 7, negative); }
 }
 
@@ -2198,6 +2259,9 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #endif
 #ifndef AMVPT_CHUNK_STREAMS
 #define AMVPT_CHUNK_STREAMS 2   /* chunk streams of a render (1: every chunk on the render stream, A/B) */
+#endif
+#ifndef AMVPT_TILE_SLOTS
+#define AMVPT_TILE_SLOTS 0   /* 4 x 4 pixel tiles per row-splat block (see tile_slot_lane) */
 #endif
 #ifndef AMVPT_PDF_ROW
 #define AMVPT_PDF_ROW 1   /* the pairwise MIS sum hoists wi_k's pdf row (0: per-pair bsdf_pdf, A/B) */
@@ -2667,7 +2731,8 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     else splat_lds_init(reinterpret_cast<SplatLds<C> &>(L));
     /* one put of this kernel's kind */
     auto put = [&](float x, float y, const float *vals, bool valid, bool coalesce, int buf, uint32_t *fb) {
-        if constexpr (kRow) wave_put<C, kWin>(P, B.film, L, x, y, vals, valid, coalesce, fb);
+        if (P.film_fx) direct_put<C, kWin>(P, B.film, x, y, vals, valid, coalesce);   /* deterministic mode */
+        else if constexpr (kRow) wave_put<C, kWin>(P, B.film, L, x, y, vals, valid, coalesce, fb);
         else block_put<C>(P, B.film, L, buf, x, y, vals, valid, coalesce, fb);
     };
     const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
@@ -3080,6 +3145,8 @@ struct DevArena {
      * order it after / before the render stream */
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    void *fx = nullptr;   /* deterministic mode's fixed-point film */
+    size_t fxbytes = 0;
 };
 static std::mutex g_arenas_mu;
 static std::map<int, std::unique_ptr<DevArena>> g_arenas;
@@ -3175,6 +3242,13 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_run_counts(const uint8_t
     if (threadIdx.x == 0) counts[blockIdx.x] = (uint32_t) (part[0] + part[1] + part[2] + part[3]);
 }
 
+/* deterministic mode: film += fixed-point sums (one thread per float, a fixed conversion per cell) */
+AMVPT_TU_LOCAL __global__ void k_fixed_resolve(float *film, const unsigned long long *fx, uint64_t n) {
+    const uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    film[i] += (float) ((double) (long long) fx[i] * (1.0 / kFixScale));
+}
+
 amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const amvpt_params *params,
                          const amvpt_lane_set &lanes, const amvpt_film_window &fwin, void *stream,
                          const amvpt_render_opts &opts, amvpt_counters *counters, float *records,
@@ -3245,6 +3319,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         return AMVPT_ERR_INVALID;
     }
     const bool whole_film = fwin.x0 == 0 && fwin.y0 == 0 && fwin.width == QW && fwin.height == QH;
+    const bool deterministic = (opts.flags & AMVPT_OPT_DETERMINISTIC) != 0;
+    if (deterministic && !whole_film) {
+        set_error("amvpt_render: AMVPT_OPT_DETERMINISTIC needs a whole-quilt film window");
+        return AMVPT_ERR_UNSUPPORTED;
+    }
     if (!whole_film && !fwin.overflow) {
         set_error("amvpt_render: a film window smaller than the quilt needs an overflow list");
         return AMVPT_ERR_INVALID;
@@ -3321,6 +3400,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* row-reduced splat (row_put): RGBW film, Gaussian filter, >= 16 samples per pixel and pass
      * (a 16-lane row = one pixel); AMVPT_ROW_SPLAT=0 keeps the per-lane splat (A/B) */
     P.row_splat = (K.row_splat && P.C == 4 && !P.box && P.pow2 && spp_pp >= 16) ? 1u : 0u;
+    /* tiled slots: whole 4-row bands of a quilt row width divisible by 4, 16 samples per pixel and pass,
+     * contiguous lane sets whose chunks start and end on band boundaries */
+    {
+        const uint64_t band = 4ull * QW * 16ull;
+        P.tile_w = (AMVPT_TILE_SLOTS && P.row_splat && spp_pp == 16 && QW % 4 == 0 && !rect && lane_begin % band == 0 &&
+                    span % band == 0 && span <= 0xffffffffull) ? QW : 0u;
+    }
 
     /* views to device (tiny) */
     std::vector<DView> hv(Pp.n_views);
@@ -3357,6 +3443,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         while (chunk_max > (1ull << 16) && chunk_max * per_lane > (24ull << 30)) chunk_max >>= 1;
     }
     const uint64_t chunk = std::min<uint64_t>(chunk_max, span);
+    if (P.tile_w && chunk % (4ull * QW * 16ull) != 0) P.tile_w = 0;   /* chunks must hold whole tile bands */
     P.vs_stride = (uint32_t) chunk;
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
@@ -3425,6 +3512,15 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     auto carve = [&](size_t bytes) { char *r = p; p += (bytes + 255) & ~(size_t) 255; return r; };
     HIPCHK(hipMemcpyAsync(dviews, hv.data(), hv.size() * sizeof(DView), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(dstats, 0, stats_bytes, st));
+
+    /* deterministic mode: the zeroed 32.32 fixed-point film the splats add into (k_fixed_resolve at the end) */
+    const size_t film_floats = (size_t) QW * QH * (Pp.film_alpha ? 5 : 4);
+    if (deterministic) {
+        { const amvpt_status as_ = arena_reserve(A, A.fx, A.fxbytes, film_floats * 8, "deterministic film"); if (as_ != AMVPT_OK) return as_; }
+        HIPCHK(hipMemsetAsync(A.fx, 0, film_floats * 8, st));
+        P.film_fx = (unsigned long long *) A.fx;
+        P.film_base = film;
+    }
 
     /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
     uint8_t *d_amask = nullptr;
@@ -3717,6 +3813,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         }
     }
     arena_release.join();
+    if (deterministic) {
+        hipLaunchKernelGGL(k_fixed_resolve, dim3((uint32_t) ((film_floats + 255) / 256)), dim3(256), 0, st, film,
+                           (const unsigned long long *) A.fx, (uint64_t) film_floats);
+        HIPCHK(hipGetLastError());
+    }
     uint64_t overflow_cells = 0;
     if (P.overflow) {
         /* the caller sums the list; a list that ran out of room lost cells: fail loudly */

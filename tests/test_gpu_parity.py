@@ -348,6 +348,44 @@ def test_two_chunk_streams(gpu_ready, amvpt_mod, oracle):
         amvpt_mod.set_chunk_lanes(0)
 
 
+@pytest.mark.parametrize("scene", ["cbox", "mesh"])
+def test_deterministic_film(gpu_ready, amvpt_mod, oracle, scene):
+    """AMVPT_OPT_DETERMINISTIC: the splats are summed as 32.32 fixed point with integer atomics, so the
+    film is bitwise identical across runs, chunk sizes and (mesh: two chunk streams) stream interleavings,
+    and agrees with the float-atomic film and the oracle's film to float summation order."""
+    torch = _torch()
+    path = CBOX if scene == "cbox" else MESH
+    s = amvpt_mod.load_file(path, res=16, spp=32, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    plan = oracle.plan(p)
+    dev = amvpt_mod.DeviceScene(sd)
+    films = []
+    for chunk, flags in [(0, amvpt_mod.OPT_DETERMINISTIC), (3000, amvpt_mod.OPT_DETERMINISTIC),
+                         (0, amvpt_mod.OPT_DETERMINISTIC), (0, 0)]:
+        film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+        dev.render_ex(vd, p, film.data_ptr(), chunk_lanes=chunk, flags=flags)
+        torch.cuda.synchronize()
+        films.append(film.cpu().numpy())
+    assert _bit_equal(films[0], films[1]).all() and _bit_equal(films[0], films[2]).all()
+    ofilm, _, _ = oracle.render(sd, vd, p, threads=16, record_pass=0)
+    scale = np.abs(ofilm).max()
+    assert np.abs(films[0] - films[3]).max() <= 1e-5 * scale
+    assert np.abs(films[0] - ofilm).max() <= 1e-5 * scale
+    assert plan["lanes"] > 3000 * 4
+
+
+def test_deterministic_film_needs_whole_window(gpu_ready, amvpt_mod):
+    torch = _torch()
+    s = amvpt_mod.load_file(CBOX, res=16, spp=16, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width // 2, 4), dtype=torch.float32, device="cuda")
+    ov = torch.zeros(1 << 16, dtype=torch.int64, device="cuda")
+    with pytest.raises(Exception, match="DETERMINISTIC"):
+        dev.render_ex(vd, p, film.data_ptr(), window=(0, 0, p.film_width // 2, p.film_height),
+                      overflow_ptr=ov.data_ptr(), overflow_capacity=1000, flags=amvpt_mod.OPT_DETERMINISTIC)
+
+
 @pytest.mark.parametrize("gx,gy,reuse", [(4, 4, 16), (4, 3, 12)], ids=["g16", "g12"])
 def test_large_view_groups(gpu_ready, amvpt_mod, oracle, gx, gy, reuse):
     """Group sizes above 8 (reuse_count = n_views = 12 or 16): camera selection over up to 15
