@@ -1196,7 +1196,7 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
             const float v = (float) d;
 #endif
             if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
-                if (inside) film_add(P, film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);
+                if (inside) atomicAdd(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);   /* never deterministic */
                 else film_cell_add<kWin>(P, film, w.bx0 + cx, w.by0 + cy, k, v);
             }
         }
@@ -2261,7 +2261,10 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #define AMVPT_CHUNK_STREAMS 2   /* chunk streams of a render (1: every chunk on the render stream, A/B) */
 #endif
 #ifndef AMVPT_TILE_SLOTS
-#define AMVPT_TILE_SLOTS 0   /* 4 x 4 pixel tiles per row-splat block (see tile_slot_lane) */
+/* 4 x 4 pixel tiles per row-splat block (see tile_slot_lane): config M 1472 -> 1521 Msamples/s (splat
+ * 106.3 -> 100.7 ms, and the fused suffix 134 -> 129.6 ms: its queue drains spatially coherent paths);
+ * with block-wide windows instead of wave windows it lost (splat 122 ms, r03s) */
+#define AMVPT_TILE_SLOTS 1
 #endif
 #ifndef AMVPT_PDF_ROW
 #define AMVPT_PDF_ROW 1   /* the pairwise MIS sum hoists wi_k's pdf row (0: per-pair bsdf_pdf, A/B) */
@@ -2731,9 +2734,13 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     else splat_lds_init(reinterpret_cast<SplatLds<C> &>(L));
     /* one put of this kernel's kind */
     auto put = [&](float x, float y, const float *vals, bool valid, bool coalesce, int buf, uint32_t *fb) {
-        if (P.film_fx) direct_put<C, kWin>(P, B.film, x, y, vals, valid, coalesce);   /* deterministic mode */
-        else if constexpr (kRow) wave_put<C, kWin>(P, B.film, L, x, y, vals, valid, coalesce, fb);
-        else block_put<C>(P, B.film, L, buf, x, y, vals, valid, coalesce, fb);
+        if constexpr (kRow) {
+            wave_put<C, kWin>(P, B.film, L, x, y, vals, valid, coalesce, fb);
+        } else {
+            /* deterministic mode runs these instances only (launch_splat) */
+            if (P.film_fx) direct_put<C, kWin>(P, B.film, x, y, vals, valid, coalesce);
+            else block_put<C>(P, B.film, L, buf, x, y, vals, valid, coalesce, fb);
+        }
     };
     const uint32_t slot = blockIdx.x * kSplatBlock + threadIdx.x;
     const bool ok = slot < P.chunk_n;
@@ -2784,7 +2791,12 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     for (int k = 0; k < Gn; ++k) {
         /* a view no lane of the wave splats into: no reprojection, no put (all-diffuse records carry
          * the valid bits in the lane record; records / debug mode write every view's entry) */
-        if (AMVPT_SPLAT_SKIP && kDiff && k > 0 && !P.record && !P.debug && !wave_any(ok && (mget(vmask, k)))) continue;
+        if (AMVPT_SPLAT_SKIP && kDiff && k > 0 && !P.record && !P.debug) {
+            /* wave windows skip per wave; the block window's put has block barriers, so its skip must be
+             * block-uniform (a wave skipping alone would pair its next barriers with the wrong view's) */
+            const bool any = kRow ? wave_any(ok && mget(vmask, k)) : __syncthreads_or(ok && mget(vmask, k));
+            if (!any) continue;
+        }
         const size_t o = (size_t) k * n + slot;
         float weight = 0.f;
         bool valid = false;
@@ -3023,7 +3035,7 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
 }
 template <int G>
 void launch_splat(dim3 grid, hipStream_t st, const KParams &P, const DView *V, const Bufs &B, bool diff) {
-    const bool row = AMVPT_WAVE_WIN && P.row_splat && P.C == 4;
+    const bool row = AMVPT_WAVE_WIN && P.row_splat && P.C == 4 && !P.film_fx;   /* deterministic: direct puts */
     const bool whole = P.fx0 == 0u && P.fy0 == 0u && P.fw == P.W && P.fh == P.H;
     if (P.C == 5 && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, true, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);
     else if (P.C == 5) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_splat_multi<G, 5, false, false>), grid, dim3(kSplatBlock), 0, st, P, V, B);

@@ -91,6 +91,15 @@ def test_generic_kernels_on_diffuse_scene(gpu_ready, amvpt_mod, oracle, res, spp
     _check(amvpt_mod, oracle, s, flags=amvpt_mod.OPT_GENERIC_KERNELS)
 
 
+@pytest.mark.parametrize("defines", [dict(rfilter="box"), dict(spp=24)], ids=["box_filter", "spp24"])
+def test_block_window_splat(gpu_ready, amvpt_mod, oracle, defines):
+    """The block-window splat (box filter, or spp per pass not a power of two): its put has block
+    barriers, so the all-diffuse kernels skip a view only when no lane of the whole block splats it."""
+    kw = dict(res=24, spp=32, gx=4, gy=2, reuse=8)
+    kw.update(defines)
+    _check(amvpt_mod, oracle, amvpt_mod.load_file(CBOX, **kw))
+
+
 def test_mvpath_reuse_without_mis(gpu_ready, amvpt_mod, oracle):
     s = amvpt_mod.load_file(CBOX, res=48, spp=16, sa_mis="false")
     _check(amvpt_mod, oracle, s)
