@@ -2269,6 +2269,14 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #ifndef AMVPT_PDF_ROW
 #define AMVPT_PDF_ROW 1   /* the pairwise MIS sum hoists wi_k's pdf row (0: per-pair bsdf_pdf, A/B) */
 #endif
+#ifndef AMVPT_COH_UNI
+/* 1: k_prim_hit(_req) and k_vis walk wave-uniformly (scalar node loads, the wave enters a node when
+ * any lane's ray hits its box) on BVHs of any size -- a wave's camera / visibility rays are nearly
+ * identical (4 pixels x 16 samples, one target view per wave), and the primary walk fuses with the
+ * request code (k_prim_hit_req).  3.6 k-triangle mesh: 629.9 -> 663.8 Msamples/s (r03v); 0: per-lane
+ * walks above kUniformNodeLimit nodes (A/B) */
+#define AMVPT_COH_UNI 1
+#endif
 #ifndef AMVPT_PRIM_WAVES
 #define AMVPT_PRIM_WAVES 1
 #endif
@@ -3464,6 +3472,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t stats_bytes = (size_t) kStats * kStatShards * 8, cnt_bytes = (size_t) 3 * kQParts * kCntStride * 4;
     const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
     const bool uni = scene_uniform(scene->dev.n_nodes, trav);
+    /* the coherent primary and visibility rays walk wave-uniformly on every BVH in automatic mode
+     * (AMVPT_COH_UNI, see launch_primary); the incoherent suffix rays keep the per-lane walk */
+    const bool uni_coh = uni || (AMVPT_COH_UNI && trav == 0u);
     /* suffix walk: brute force for tiny scenes in auto mode */
     int walk = uni ? WALK_UNI : WALK_LANE;
     if (uni && trav == 0u && K.brute && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
@@ -3702,7 +3713,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                     hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
                     T.end(st);
                 } else {
-                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni, diff, T);
+                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni_coh, diff, T);
                 }
             }
             HIPCHK(hipGetLastError());

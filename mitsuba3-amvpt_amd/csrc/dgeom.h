@@ -208,9 +208,14 @@ template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const
     float tmax_box = ray.maxt;
     if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
+        /* BVHs with direction-octant copies (large ones, walked uniformly by the coherent primary
+         * rays): the copy of the first lane's octant (any copy gives the same hit) */
+        const DNode *const gn = sc.oct_stride ? sc.gnodes + (size_t) ufirst(
+                                    (fbits(ray.d.x) >> 31) | ((fbits(ray.d.y) >> 31) << 1) | ((fbits(ray.d.z) >> 31) << 2)) * sc.oct_stride
+                                              : sc.gnodes;
         uint32_t node = 0;
         while (node < nn) {
-            const DNode n = load_uniform(sc.gnodes, node);
+            const DNode n = load_uniform(gn, node);
             const bool enter = wave_any(box_hit(n, br, tmax_box));
             const uint32_t skc = ufirst(n.skip_count);
             const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
