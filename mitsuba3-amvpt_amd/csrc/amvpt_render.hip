@@ -626,8 +626,9 @@ AD f3 camera_point(const DView &v, float apx, float apy) {
  * accumulation, resolved once per render by k_fixed_resolve).  Non-finite values are dropped there.
  */
 constexpr double kFixScale = 4294967296.0, kFixLimit = 2147483647.0;
-AD void film_add(const KParams &P, float *p, float v) {
-    if (P.film_fx) {
+/* kDet = false: a kernel instance that never runs in deterministic mode (the row splat) */
+template <bool kDet = true> AD void film_add(const KParams &P, float *p, float v) {
+    if (kDet && P.film_fx) {
         const double d = (double) v * kFixScale;
         if (!(fabs(d) < kFixLimit * kFixScale)) return;   /* NaN / Inf / out of range */
         atomicAdd(P.film_fx + (p - P.film_base), (unsigned long long) (long long) __builtin_rint(d));
@@ -662,8 +663,8 @@ AD void overflow_push(const KParams &P, uint64_t idx, float v) {
         reinterpret_cast<uint4 *>(P.overflow + 4)[e] = make_uint4((uint32_t) idx, (uint32_t) (idx >> 32), __float_as_uint(v), 0u);
 }
 /* one film float of quilt cell (x, y), channel k: the window, else the overflow list */
-template <bool kWin = true> AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float v) {
-    if (in_window<kWin>(P, x, y)) film_add(P, film_cell<kWin>(P, film, x, y, k), v);
+template <bool kWin = true, bool kDet = true> AD void film_cell_add(const KParams &P, float *film, int x, int y, int k, float v) {
+    if (in_window<kWin>(P, x, y)) film_add<kDet>(P, film_cell<kWin>(P, film, x, y, k), v);
     else overflow_push(P, ((uint64_t) (uint32_t) y * P.W + (uint32_t) x) * P.C + (uint32_t) k, v);
 }
 
@@ -705,7 +706,8 @@ template <bool kWin = true> AD void film_cell_add(const KParams &P, float *film,
  * (measured: splat 206 -> 187 ms at config M; rs = ww, or % 32 in {1, 8, 17, 24}: 200-207 ms).
  * The 112-cell width leaves room for the padding (5 blocks per CU either way). */
 /* measurement-only attribution builds (wrong images): 1 skips the LDS adds, 2 the flush's
- * film atomics, 4 the filter weights, 8 turns the LDS atomic adds into plain stores */
+ * film atomics, 4 the filter weights, 8 turns the LDS atomic adds into plain stores, 16 (with 32:
+ * the row-half products too) drops the row splat's cross-lane reduce steps */
 #ifndef AMVPT_ATTR_SKIP
 #define AMVPT_ATTR_SKIP 0
 #endif
@@ -960,7 +962,7 @@ AD void window_flush(const KParams &P, float *film, SplatLds<C> &L, const Win &w
 /* one footprint's cells straight into the window (or the film when it does not fit) */
 /* kRolled: the window loop is not unrolled (row_put's rare per-lane path: an unrolled 5 x 5 x C
  * body would set the register allocation of the whole splat kernel) */
-template <int C, bool kRolled = false, bool kWin = true>
+template <int C, bool kRolled = false, bool kWin = true, bool kDet = true>
 AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, const float *wx,
                  const float *wy, const float *vals, bool coalesce, uint32_t *fallback) {
     const int cx0 = max(f.x0, 0), cy0 = max(f.y0, 0);
@@ -1000,7 +1002,7 @@ AD void foot_add(const KParams &P, float *film, WinT *const wbase, const Win &wn
                 const float wxv = xs < kMaxFoot ? wx[xs] : (P.box ? 1.f : gaussian_eval(P.filt, f.rx + (float) xs));
                 const float w = wxv * wyv;
 #pragma unroll
-                for (int k = 0; k < C; ++k) film_cell_add<kWin>(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
+                for (int k = 0; k < C; ++k) film_cell_add<kWin, kDet>(P, film, x, y, k, P.box ? vals[k] : vals[k] * w);
             }
         }
     }
@@ -1072,11 +1074,24 @@ AD int row_max(int v) {
 }
 /* filter weight of film cell `cell` for a footprint starting at x0 with argument r, zero outside
  * the footprint's cells [lo, hi) -- inside it eval(r + (cell - x0)), the reference's argument */
-AD float union_weight(const KParams &P, float r, int x0, int cell, int lo, int hi) {
-    const float w = gaussian_eval(P.filt, r + (float) (cell - x0));
+AD float union_weight(const FilterCoeffs &F, float r, int x0, int cell, int lo, int hi) {
+    const float w = gaussian_eval(F, r + (float) (cell - x0));
     return (cell >= lo && cell < hi) ? w : 0.f;
 }
+/* The row splat runs for the default Gaussian only (rfilter stddev 0.5, the reference's default,
+ * gaussian.cpp): its coefficients -- exactly what gaussian_coeffs(0.5) computes on the host, checked
+ * there bit for bit before the row splat is chosen -- are compile-time literals, so every Estrin step is
+ * one v_fmaak/v_fma with a literal instead of two SGPR operands copied through VGPRs (gfx9 VOP3 reads one
+ * SGPR per instruction), and the kernel keeps 11 fewer SGPRs live */
+AD FilterCoeffs default_filter() {
+    return FilterCoeffs{{0x1.ff9d52p-1f, -0x1.fda5bcp+0f, 0x1.f4a20cp+0f, -0x1.3c9afep+0f, 0x1.181032p-1f, -0x1.604b8ap-3f,
+                         0x1.34c5d4p-5f, -0x1.657e54p-8f, 0x1.e9dbd6p-12f, -0x1.2bffdp-16f},
+                        0x1p+1f};
+}
 
+#ifndef AMVPT_SPLAT_PK
+#define AMVPT_SPLAT_PK 1   /* row splat: packed-f32 products of the two row halves: config-M splat 101.8 -> 97.7 ms (r03y; 0: A/B) */
+#endif
 template <int C, bool kWin = true>
 AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, bool act,
                     const float *vals, bool coalesce, uint32_t *fallback) {
@@ -1100,9 +1115,12 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
         const float K = pick(ch);
         const float B1 = dpp_f<DPP_XOR1>(pick(ch ^ 1)), B2 = dpp_f<DPP_XOR2>(pick(ch ^ 2)),
                     B3 = dpp_f<DPP_XOR3>(pick(ch ^ 3));
+        /* inactive lanes hand over v = 0, so their (finite) weights need no masking: the weights are
+         * straight-line code, not a branch per evaluation */
+        const FilterCoeffs F = default_filter();
         float wx[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) wx[c] = act ? union_weight(P, f.rx, f.x0, ux0 + c, x0c, x1) : 0.f;
+        for (int c = 0; c < 6; ++c) wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
         WinT *const wch = wbase + ch * wn.plane;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -1110,7 +1128,7 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
             float Ky[2], B1y[2], B2y[2], B3y[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const float wy = act ? union_weight(P, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1) : 0.f;
+                const float wy = union_weight(F, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1);
                 Ky[h] = K * wy;
                 B1y[h] = B1 * dpp_f<DPP_XOR1>(wy);
                 B2y[h] = B2 * dpp_f<DPP_XOR2>(wy);
@@ -1119,6 +1137,20 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
             /* steps 1-2: the quad's sum of this lane's channel, sum_j v_j[ch] wy_j wx_j; step 3: plus
              * the rotate-4 partner's quad sum of the other row half */
             float z[6];
+#if AMVPT_SPLAT_PK
+            /* the two row halves as one packed pair (v_pk_mul_f32 / v_pk_fma_f32: per-element IEEE, the
+             * same products and sums bit for bit) */
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            const f2v Ky2 = {Ky[0], Ky[1]}, B1y2 = {B1y[0], B1y[1]}, B2y2 = {B2y[0], B2y[1]}, B3y2 = {B3y[0], B3y[1]};
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                f2v a = Ky2 * (f2v) wx[c];
+                a = __builtin_elementwise_fma((f2v) dpp_f<DPP_XOR1>(wx[c]), B1y2, a);
+                a = __builtin_elementwise_fma((f2v) dpp_f<DPP_XOR2>(wx[c]), B2y2, a);
+                a = __builtin_elementwise_fma((f2v) dpp_f<DPP_XOR3>(wx[c]), B3y2, a);
+                z[c] = a.x + dpp_f<DPP_ROR4>(a.y);
+            }
+#else
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
                 float y[2];
@@ -1131,11 +1163,12 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
                 }
                 z[c] = y[0] + dpp_f<DPP_ROR4>(y[1]);
             }
+#endif
             const int row = r + 3 * b2;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float keep = b3 ? z[c + 3] : z[c], send = b3 ? z[c] : z[c + 3];
-                const float u = keep + dpp_f<DPP_ROR8>(send);
+                const float u = (AMVPT_ATTR_SKIP & 16) ? z[c] : keep + dpp_f<DPP_ROR8>(send);
                 const int col = c + 3 * b3;
                 if (ux0 + col < ux1 && uy0 + row < uy1 && !(AMVPT_ATTR_SKIP & 1))
                     win_add(wch + (uy0 + row - wn.by0) * wn.rs + (ux0 + col - wn.bx0), u);
@@ -1144,7 +1177,7 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
     } else if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
-        foot_add<C, true, kWin>(P, film, wbase, wn, f, wx, wy, vals, coalesce, fallback);
+        foot_add<C, true, kWin, false>(P, film, wbase, wn, f, wx, wy, vals, coalesce, fallback);
     }
 }
 
@@ -1197,7 +1230,7 @@ AD void wave_flush(const KParams &P, float *film, WinT *win, const Win &w) {
 #endif
             if ((v != 0.f || v != v) && !(AMVPT_ATTR_SKIP & 2)) {
                 if (inside) atomicAdd(film0 + ((uint32_t) cy * film_row + (uint32_t) r), v);   /* never deterministic */
-                else film_cell_add<kWin>(P, film, w.bx0 + cx, w.by0 + cy, k, v);
+                else film_cell_add<kWin, false>(P, film, w.bx0 + cx, w.by0 + cy, k, v);
             }
         }
     }
@@ -3108,6 +3141,10 @@ static uint32_t group_size(const amvpt_params &P) {
     return G;
 }
 
+/* default_filter()'s literals, for the host-side check */
+static const float kDefaultFilterHost[10] = {0x1.ff9d52p-1f, -0x1.fda5bcp+0f, 0x1.f4a20cp+0f, -0x1.3c9afep+0f,
+                                             0x1.181032p-1f, -0x1.604b8ap-3f, 0x1.34c5d4p-5f, -0x1.657e54p-8f,
+                                             0x1.e9dbd6p-12f, -0x1.2bffdp-16f};
 static void gaussian_coeffs(float stddev, FilterCoeffs &f) {
     static const double cd[10] = {9.992604880e-1, -4.977025247e-1, 1.222248550e-1, -1.932406282e-2,
                                   2.136713061e-3, -1.679873860e-4, 9.202145248e-6, -3.329417433e-7,
@@ -3419,7 +3456,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
     /* row-reduced splat (row_put): RGBW film, Gaussian filter, >= 16 samples per pixel and pass
      * (a 16-lane row = one pixel); AMVPT_ROW_SPLAT=0 keeps the per-lane splat (A/B) */
-    P.row_splat = (K.row_splat && P.C == 4 && !P.box && P.pow2 && spp_pp >= 16) ? 1u : 0u;
+    {
+        /* ... and the default Gaussian (its coefficients are literals in the row kernels, default_filter) */
+        FilterCoeffs d;
+        gaussian_coeffs(0.5f, d);
+        const bool def_filt = !P.box && std::memcmp(&d, &P.filt, sizeof(d)) == 0 &&
+                              std::memcmp(&d.c[0], &kDefaultFilterHost[0], sizeof(d.c)) == 0;
+        P.row_splat = (K.row_splat && P.C == 4 && def_filt && P.pow2 && spp_pp >= 16) ? 1u : 0u;
+    }
     /* tiled slots: whole 4-row bands of a quilt row width divisible by 4, 16 samples per pixel and pass,
      * contiguous lane sets whose chunks start and end on band boundaries */
     {
