@@ -1092,15 +1092,20 @@ AD FilterCoeffs default_filter() {
 #ifndef AMVPT_SPLAT_PK
 #define AMVPT_SPLAT_PK 1   /* row splat: packed-f32 products of the two row halves: config-M splat 101.8 -> 97.7 ms (r03y; 0: A/B) */
 #endif
+/* union box of the active footprints of the lane's 16-lane row (every lane of the wave active) */
+struct RowBox { int x0, y0, x1, y1; };
+AD RowBox row_box(const Foot &f, bool act) {
+    constexpr int kBig = 0x3fffffff;
+    return RowBox{row_min(act ? max(f.x0, 0) : kBig), row_min(act ? max(f.y0, 0) : kBig),
+                  row_max(act ? f.x0 + f.nx : -kBig), row_max(act ? f.y0 + f.ny : -kBig)};
+}
 template <int C, bool kWin = true>
 AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win &wn, const Foot &f, bool act,
-                    const float *vals, bool coalesce, uint32_t *fallback) {
+                    const float *vals, bool coalesce, uint32_t *fallback, const RowBox &ub) {
     const int x0c = max(f.x0, 0), y0c = max(f.y0, 0), x1 = f.x0 + f.nx, y1 = f.y0 + f.ny;
     const bool inw = x0c >= wn.bx0 && y0c >= wn.by0 && x1 <= wn.bx0 + wn.ww && y1 <= wn.by0 + wn.wh;
     const bool good = inw && win_fits<C>(vals);
-    constexpr int kBig = 0x3fffffff;
-    const int ux0 = row_min(act ? x0c : kBig), uy0 = row_min(act ? y0c : kBig);
-    const int ux1 = row_max(act ? x1 : -kBig), uy1 = row_max(act ? y1 : -kBig);
+    const int ux0 = ub.x0, uy0 = ub.y0, ux1 = ub.x1, uy1 = ub.y1;
     const int bad = row_max((act && !good) ? 1 : 0);
     const bool fast = C == 4 && ux1 > ux0 && bad == 0 && ux1 - ux0 <= 6 && uy1 - uy0 <= 6;
     if (fast) {
@@ -1181,18 +1186,6 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
     }
 }
 
-/* min / max over the wave (every lane active): DPP within the rows, then the 4 row results */
-AD int wave_min_dpp(int v) {
-    v = row_min(v);
-    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
-}
-AD int wave_max_dpp(int v) {
-    v = row_max(v);
-    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
-}
-
 /* the wave's window flush: one global float atomic per touched film float, re-zeroing the
  * window (wave-local, in LDS order after the wave's own adds).  A cell's row comes from a float
  * reciprocal with a one-step correction (e < 2^24), not an integer division.  (Batching four
@@ -1246,9 +1239,17 @@ AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float p
     f.x0 = f.y0 = 0; f.nx = f.ny = 0; f.rx = f.ry = 0.f;
     if (valid) f = footprint(P, px, py, coalesce);
     const bool act = valid && f.ok;
-    constexpr int kBig = 0x3fffffff;
-    const int bx0 = wave_min_dpp(act ? max(f.x0, 0) : kBig), by0 = wave_min_dpp(act ? max(f.y0, 0) : kBig);
-    const int bx1 = wave_max_dpp(act ? f.x0 + f.nx : -kBig), by1 = wave_max_dpp(act ? f.y0 + f.ny : -kBig);
+    /* the rows' union boxes (row_put_win's), then the wave's box from the four row results */
+    const RowBox ub = row_box(f, act);
+    auto rmin = [](int v) {
+        return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                   min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+    };
+    auto rmax = [](int v) {
+        return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                   max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+    };
+    const int bx0 = rmin(ub.x0), by0 = rmin(ub.y0), bx1 = rmax(ub.x1), by1 = rmax(ub.y1);
     if (bx1 <= bx0) return;   /* no active footprint in the wave (uniform) */
     Win wn;
     wn.bx0 = bx0; wn.by0 = by0;
@@ -1266,7 +1267,7 @@ AD void wave_put(const KParams &P, float *film, WaveLds<C> &L, float px, float p
     }
     WinT *const win = L.win + (threadIdx.x >> 6) * (kWavePlane * C);
     /* row_put reads the window through L.win: hand it this wave's window */
-    row_put_win<C, kWin>(P, film, win, wn, f, act, vals, coalesce, fallback);
+    row_put_win<C, kWin>(P, film, win, wn, f, act, vals, coalesce, fallback, ub);
     wave_flush<C, kWin>(P, film, win, wn);
 }
 
@@ -1287,7 +1288,7 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
     const Win wn = window_bbox(L, buf, act, max(f.x0, 0), max(f.y0, 0), f.x0 + f.nx, f.y0 + f.ny, (int) P.win_rs,
                                P.row_splat != 0);
     if (C == 4 && P.row_splat) {
-        row_put_win<C>(P, film, L.win, wn, f, act, vals, coalesce, fallback);
+        row_put_win<C>(P, film, L.win, wn, f, act, vals, coalesce, fallback, row_box(f, act));
     } else if (act) {
         float wx[kMaxFoot], wy[kMaxFoot];
         foot_weights(P, f, wx, wy);
@@ -2289,6 +2290,9 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * (0: read from LDS per pair, A/B r03g); reading view k's own fields from the register copies too
  * (uniform dynamic index) measured slower, 444 ms (r03h) */
 #define AMVPT_PAIR_REGS 1
+#endif
+#ifndef AMVPT_FUSED_TWO_STREAMS
+#define AMVPT_FUSED_TWO_STREAMS 0   /* 1: fused-suffix scenes alternate chunks over two streams too (A/B) */
 #endif
 #ifndef AMVPT_CHUNK_STREAMS
 #define AMVPT_CHUNK_STREAMS 2   /* chunk streams of a render (1: every chunk on the render stream, A/B) */
@@ -3534,7 +3538,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * and tails leave CUs idle that the other chunk's kernels fill (mesh 550 -> 599 Msamples/s).  The
      * fused-suffix scenes gain 0.0-0.5 % (r03i) and keep one stream, so their per-kernel HIP-event
      * times are not overlapped (AMVPT_OPT_ONE_STREAM forces one stream everywhere) */
-    const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && !fuse_suffix && !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? 2 : 1;
+    const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
+                        !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? 2 : 1;
     const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
     const size_t need = views_bytes + stats_bytes + set_bytes * n_sets;
     int dev = 0;
