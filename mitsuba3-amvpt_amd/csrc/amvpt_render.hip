@@ -2314,6 +2314,11 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * walks above kUniformNodeLimit nodes (A/B) */
 #define AMVPT_COH_UNI 1
 #endif
+#ifndef AMVPT_WAVE_DIFF
+/* 1: the generic k_mv_primary runs the all-diffuse body for waves whose primary hits are all plain
+ * diffuse (mixed-material scenes; A/B 0) */
+#define AMVPT_WAVE_DIFF 1
+#endif
 #ifndef AMVPT_PRIM_WAVES
 #define AMVPT_PRIM_WAVES 1
 #endif
@@ -2324,35 +2329,18 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * F_JP and one sign bit per view -- same values, a third of the LDS per thread.
  */
 template <int G> constexpr int prim_block() { return G ? kPrimBlock : 64; }   /* G = 0: LDS state grows with G */
-template <int G, bool kTab, bool kDiff>
-__global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
-    constexpr int kPB = prim_block<G>();
+/*
+ * The per-lane body of k_mv_primary.  kDiff: the all-diffuse computation (see below); kGenRec (with
+ * kDiff): a wave of the generic kernel whose primary hits are all plain `diffuse` runs the all-diffuse
+ * computation -- it reads the hit's BSDF only, so the values are the generic path's -- and writes the
+ * generic view records (result, weight), (bsdf value, flags) from its lane values, as k_splat_multi's
+ * all-diffuse branch would expand them.
+ */
+template <int G, bool kTab, bool kDiff, bool kGenRec>
+AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, const DView *V, const Bufs &B,
+                        float *const vs, const uint32_t vs_stride, const uint32_t slot, const uint32_t i, const bool ok) {
     const int Gn = group_size<G>(P);
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    DScene S = *Sp;
-    const uint32_t vs_off = kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u;
-    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
-    /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPB] */
-    /* (runtime groups too large for LDS: the chunk's global per-view state, field-major, slot-minor) */
-    const bool vs_glob = G == 0 && B.vstate != nullptr;
-    const uint32_t vs_stride = vs_glob ? P.vs_stride : (uint32_t) kPB;
-    float *const vs = vs_glob ? B.vstate + (blockIdx.x * blockDim.x + threadIdx.x)
-                              : reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
 #define VSF(f, k) vs[((f) * Gn + (k)) * vs_stride]
-#if AMVPT_PRIM_SLOT_ORDER
-    /* threads run in slot order (a wave = 64 pixels of one sample, see slot_lane), so every
-     * record store of a wave is 64 contiguous slots; the hit and the ballots are read at the
-     * lane (16-B loads 256 B apart) */
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    bool ok = slot < P.chunk_n;
-    const uint32_t i = ok ? slot_lane(P, slot) : 0u;
-#else
-    /* threads run in lane order (a wave = 4 pixels x 16 samples); records go to the
-     * lane's slot (see slot_lane) */
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool ok = i < P.chunk_n;
-    const uint32_t slot = ok ? lane_slot(P, i) : 0u;
-#endif
     PathState ps;
     bool push = false;
     unsigned long long st_reuse = 0, st_vis = 0;
@@ -2377,7 +2365,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
         auto view_of = [&](int k) -> uint32_t { return group_view_n((uint32_t) Gn, p_idx, k); };
         auto put_view = [&](int k, float w, C3 res, C3 bv, uint32_t vf) {
             const size_t o = (size_t) k * n + slot;
-            if (kDiff) {
+            if (kDiff && !kGenRec) {
                 vw[o] = w;
             } else {
                 vR[o] = make_float4(res.r, res.g, res.b, w);
@@ -2644,6 +2632,13 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
                     float bp;
                     if (kDiff) {
                         bp = (valid && mget(wpos, k)) ? bp_d : 0.f;
+                        if (kGenRec && k > 0) {
+                            /* the generic path's values: a diffuse eval is one of two per lane (Dp through
+                             * wi_k.z > 0, cfma(0, emis_mis, 0) otherwise), the BSDF value of an indirect view
+                             * is Bv */
+                            if (active_em && vk) res = mget(wpos, k) ? Dp : cfma(c3(0.f), emis_mis, c3(0.f));
+                            bv = (valid && mget(wpos, k)) ? Bv : c3(0.f);
+                        }
                     } else {
                         /* result: emission (slot 0) + direct light through this view's BSDF value */
                         res = csel(k == 0, emitted, c3(0.f));
@@ -2757,6 +2752,61 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
     }
 }
 #undef VSF
+
+/* every primary hit of the wave is on a plain `diffuse` BSDF, or a miss (wave-uniform) */
+AD bool wave_diffuse(const KParams &P, const DScene &S, const SceneRef &sc, const Bufs &B, uint32_t i, bool ok) {
+    bool dl = true;
+    if (ok && P.max_depth != 0) {
+        const int32_t prim = (int32_t) fbits(B.hit[i].w);
+        if (prim >= 0) {
+            const int32_t b = S.shapes[sc.prims[prim].shape].bsdf;
+            dl = b < 0 || S.bsdfs[b].type == BSDF_DIFFUSE;
+        }
+    }
+    return !wave_any(!dl);
+}
+/* kDiff: the all-diffuse scenes' kernel.  Otherwise (AMVPT_WAVE_DIFF) two launches of the generic stage:
+ * kDW = true runs the waves whose primary hits are all diffuse with the all-diffuse body at its own
+ * register budget (generic records), kDW = false the others with the generic body */
+template <int G, bool kTab, bool kDiff, bool kDW = false>
+__global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primary(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+    constexpr int kPB = prim_block<G>();
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    DScene S = *Sp;
+    const uint32_t vs_off = kTab ? S.tab_bytes + views_lds_bytes(P.n_views) : 0u;
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
+    /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPB] */
+    /* (runtime groups too large for LDS: the chunk's global per-view state, field-major, slot-minor) */
+    const bool vs_glob = G == 0 && B.vstate != nullptr;
+    const uint32_t vs_stride = vs_glob ? P.vs_stride : (uint32_t) kPB;
+    float *const vs = vs_glob ? B.vstate + (blockIdx.x * blockDim.x + threadIdx.x)
+                              : reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
+#if AMVPT_PRIM_SLOT_ORDER
+    /* threads run in slot order (a wave = 64 pixels of one sample, see slot_lane), so every
+     * record store of a wave is 64 contiguous slots; the hit and the ballots are read at the
+     * lane (16-B loads 256 B apart) */
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = slot < P.chunk_n;
+    const uint32_t i = ok ? slot_lane(P, slot) : 0u;
+#else
+    /* threads run in lane order (a wave = 4 pixels x 16 samples); records go to the
+     * lane's slot (see slot_lane) */
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = i < P.chunk_n;
+    const uint32_t slot = ok ? lane_slot(P, i) : 0u;
+#endif
+    if constexpr (kDiff) {
+        mv_primary_lane<G, kTab, true, false>(P, S, sc, V, B, vs, vs_stride, slot, i, ok);
+    } else if (kDW) {
+        /* the waves whose primary hits are all plain diffuse (or misses): the all-diffuse body */
+        if (wave_diffuse(P, S, sc, B, i, ok)) mv_primary_lane<G, kTab, true, true>(P, S, sc, V, B, vs, vs_stride, slot, i, ok);
+    } else {
+        /* the other waves (all of them without AMVPT_WAVE_DIFF) */
+        if (!(AMVPT_WAVE_DIFF && wave_diffuse(P, S, sc, B, i, ok)))
+            mv_primary_lane<G, kTab, false, false>(P, S, sc, V, B, vs, vs_stride, slot, i, ok);
+    }
+}
+
 
 /* ------------------------------------------------------------------ */
 /* k_splat_multi<G>: indirect accumulation + splats (mvpath_multi.h:343-368,44-76) */
@@ -3073,9 +3123,17 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     T.end(st);
     T.begin(AMVPT_K_MV_PRIMARY, st);
     if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
-    else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
     else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, true>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    else {
+        if (AMVPT_WAVE_DIFF) {
+            /* the all-diffuse waves first, with the all-diffuse body's smaller per-view LDS state */
+            const size_t lds_dw = B.vstate ? 0u : (size_t) kVsFieldsDiff * group_size_host<G>(P) * kPB * sizeof(float);
+            if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false, true>), gp, dim3(kPB), lds_tab + lds_dw, st, P, S, V, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false, true>), gp, dim3(kPB), lds_tab + lds_dw, st, P, S, V, B);
+        }
+        if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false>), gp, dim3(kPB), lds_tab + lds_view, st, P, S, V, B);
+    }
     T.end(st);
 }
 template <int G>
