@@ -2217,7 +2217,11 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
 /* ------------------------------------------------------------------ */
 
 enum : uint32_t { VF_VALID = 1u, VF_INDIRECT = 2u };
-enum : uint32_t { LF_VALIDRAY = 1u, LF_ADAPT = 2u, LF_REUSE = 4u, LF_MIS = 8u, LF_DIRECT = 16u };
+/* generic stage (AMVPT_WAVE_DIFF): the all-diffuse waves' compact records, one weight per view [G][n], after
+ * the two float4 planes of the generic view records */
+AD float *vrec_compact(const Bufs &B, int Gn, uint32_t n) { return reinterpret_cast<float *>(B.vrec + (size_t) 2 * Gn * n); }
+enum : uint32_t { LF_VALIDRAY = 1u, LF_ADAPT = 2u, LF_REUSE = 4u, LF_MIS = 8u, LF_DIRECT = 16u,
+                  LF_DIFFW = 32u /* an all-diffuse wave of the generic stage: compact view records, vrec_compact */ };
 
 struct SD {        /* SampleData (mvpath.h:150-167) without the derived fields */
     C3 result, bsdf_val;
@@ -2331,10 +2335,10 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 template <int G> constexpr int prim_block() { return G ? kPrimBlock : 64; }   /* G = 0: LDS state grows with G */
 /*
  * The per-lane body of k_mv_primary.  kDiff: the all-diffuse computation (see below); kGenRec (with
- * kDiff): a wave of the generic kernel whose primary hits are all plain `diffuse` runs the all-diffuse
- * computation -- it reads the hit's BSDF only, so the values are the generic path's -- and writes the
- * generic view records (result, weight), (bsdf value, flags) from its lane values, as k_splat_multi's
- * all-diffuse branch would expand them.
+ * kDiff): a wave of a mixed scene's generic stage whose primary hits are all plain `diffuse` runs the
+ * all-diffuse computation -- it reads the hit's BSDF only, so the values are the generic path's -- and
+ * writes the compact records (one weight per view, vrec_compact) with LF_DIFFW in its lane flags;
+ * k_splat_multi reads such a wave's records the all-diffuse way.
  */
 template <int G, bool kTab, bool kDiff, bool kGenRec>
 AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, const DView *V, const Bufs &B,
@@ -2360,12 +2364,12 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
         /* view records (see Bufs): kDiff -> one weight per view; generic -> (result, weight) and
          * (bsdf value, flags) per view.  Splat positions are not stored: k_splat_multi recomputes
          * them from the hit point (camera_uv) and the lane's jitter. */
-        float *const vw = reinterpret_cast<float *>(B.vrec);
+        float *const vw = kGenRec ? vrec_compact(B, Gn, n) : reinterpret_cast<float *>(B.vrec);
         float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
         auto view_of = [&](int k) -> uint32_t { return group_view_n((uint32_t) Gn, p_idx, k); };
         auto put_view = [&](int k, float w, C3 res, C3 bv, uint32_t vf) {
             const size_t o = (size_t) k * n + slot;
-            if (kDiff && !kGenRec) {
+            if (kDiff) {
                 vw[o] = w;
             } else {
                 vR[o] = make_float4(res.r, res.g, res.b, w);
@@ -2632,13 +2636,6 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                     float bp;
                     if (kDiff) {
                         bp = (valid && mget(wpos, k)) ? bp_d : 0.f;
-                        if (kGenRec && k > 0) {
-                            /* the generic path's values: a diffuse eval is one of two per lane (Dp through
-                             * wi_k.z > 0, cfma(0, emis_mis, 0) otherwise), the BSDF value of an indirect view
-                             * is Bv */
-                            if (active_em && vk) res = mget(wpos, k) ? Dp : cfma(c3(0.f), emis_mis, c3(0.f));
-                            bv = (valid && mget(wpos, k)) ? Bv : c3(0.f);
-                        }
                     } else {
                         /* result: emission (slot 0) + direct light through this view's BSDF value */
                         res = csel(k == 0, emitted, c3(0.f));
@@ -2724,7 +2721,7 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
         }
         const uint32_t lflags = (valid_ray ? LF_VALIDRAY : 0u) | (adapt_mask ? LF_ADAPT : 0u) |
                                 (should_mis ? LF_MIS : 0u) | (reuse_l ? LF_REUSE : 0u) | (direct_l ? LF_DIRECT : 0u) |
-                                (nf_bits << 8) | mlow16(smask);
+                                (nf_bits << 8) | mlow16(smask) | (kGenRec ? LF_DIFFW : 0u);
         B.lrec[0][slot] = make_float4(R0.r, R0.g, R0.b, pdfW);
         B.lrec[1][slot] = make_float4(Dp.r, Dp.g, Dp.b, bitsf(lflags));
         B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(mlow16(vmask) >> 16 | mlow16(imask)));
@@ -2879,14 +2876,17 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         if (P.needs_ap) { apx = rng.next_1d(); apy = rng.next_1d(); }
         p_idx = sensor_index(P, fmadd(sx, P.inv_w, P.adj_ox), fmadd(sy, P.inv_h, P.adj_oy));
     }
-    const float *const vw = reinterpret_cast<const float *>(B.vrec);
+    /* an all-diffuse wave of a mixed scene's generic stage (AMVPT_WAVE_DIFF) carries the compact
+     * records (vrec_compact): the all-diffuse reads below, at run time */
+    const bool kd = kDiff || (AMVPT_WAVE_DIFF && !wave_any(ok && !(lflags & LF_DIFFW)) && wave_any(ok));
+    const float *const vw = kDiff ? reinterpret_cast<const float *>(B.vrec) : vrec_compact(B, Gn, n);
     const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
     uint32_t splats = 0, fallback = 0, nonfinite = 0, negative = 0;   /* per lane, <= G each */
 #pragma unroll 1
     for (int k = 0; k < Gn; ++k) {
         /* a view no lane of the wave splats into: no reprojection, no put (all-diffuse records carry
          * the valid bits in the lane record; records / debug mode write every view's entry) */
-        if (AMVPT_SPLAT_SKIP && kDiff && k > 0 && !P.record && !P.debug) {
+        if (AMVPT_SPLAT_SKIP && (kRow ? kd : kDiff) && k > 0 && !P.record && !P.debug) {
             /* wave windows skip per wave; the block window's put has block barriers, so its skip must be
              * block-uniform (a wave skipping alone would pair its next barriers with the wrong view's) */
             const bool any = kRow ? wave_any(ok && mget(vmask, k)) : __syncthreads_or(ok && mget(vmask, k));
@@ -2911,7 +2911,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
             y += (float) (yy * P.sres_y);
         }
         if (ok) {
-            if (kDiff) {
+            if (kd) {
                 weight = vw[o];
                 valid = mget(vmask, k);
                 if (mis) {
@@ -3561,7 +3561,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds_tab_views = (AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views))
                                      ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;
     const bool vs_global = wide && lds_tab_views + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 65536;
-    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : 32) * G + (G + 7) / 8 +
+    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G + (G + 7) / 8 +
                             (wide ? 128 : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
     if (chunk_max == 0) {
@@ -3700,7 +3700,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
         B.cnt_nee = cs.cntN;
         B.qcap = qcap;
-        B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : 32) * G * chunk);
+        B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G * chunk);
         if (wide) {
             for (int k = 0; k < 2; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
             for (int k = 0; k < 6; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);

@@ -17,7 +17,6 @@ CONFIGS = {
     "M": dict(scene="cbox_grid.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),
     "C3": dict(scene="veach_grid.xml", res=1024, spp=256, gx=4, gy=2, reuse=8),
     "mesh": dict(scene="cbox_mesh.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),
-    "meshd": dict(scene="tmp_cbox_mesh_diffuse.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),  # diagnostic only
 }
 
 
