@@ -3,7 +3,7 @@
  *
  * One frame = n_passes passes (mvpath.cpp:36-41,222-246); one pass = L lanes
  * (lane -> pixel = lane >> log2(spp_per_pass), mvpath.cpp:173-190), processed
- * in chunks of at most g_chunk_lanes lanes (automatic: 2^23..2^25).  Per chunk:
+ * in chunks of at most g_chunk_lanes lanes (automatic: up to 2^26).  Per chunk:
  *
  *   k_mv_primary<G>  render_multisample + sample_multi up to the suffix
  *                    (jitter, sample_ray_idx, primary hit, emitter sample +
@@ -47,7 +47,9 @@
 namespace amvpt {
 
 #if !defined(AMVPT_SHADOW_TU) && !defined(AMVPT_GROUP_TU)
-/* 0 = automatic: 2^25 lanes, halved (not below 2^23) while the chunk's arena would exceed 24 GB.
+/* 0 = automatic: 2^26 lanes, halved while the chunk's arena would exceed 48 GB (of the 288 GB of HBM; config M:
+ * 26 GB at 2^26, 1598/1605 -> 1614/1621 Msamples/s against 2^25 chunks, r03zg: fewer fused-suffix tails).
+ * Earlier sweep at 24 GB:
  * Fewer, larger chunks mean fewer tails of the fused suffix and fewer kernel boundaries
  * (config M: 2^22 386, 2^23 373, 2^24 364, 2^25 363 ms per frame; r02fd) */
 uint64_t g_chunk_lanes = 0;
@@ -3565,8 +3567,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                             (wide ? 128 : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
     if (chunk_max == 0) {
-        chunk_max = 1ull << 25;
-        while (chunk_max > (1ull << 16) && chunk_max * per_lane > (24ull << 30)) chunk_max >>= 1;
+        chunk_max = 1ull << 26;
+        while (chunk_max > (1ull << 16) && chunk_max * per_lane > (48ull << 30)) chunk_max >>= 1;
     }
     const uint64_t chunk = std::min<uint64_t>(chunk_max, span);
     if (P.tile_w && chunk % (4ull * QW * 16ull) != 0) P.tile_w = 0;   /* chunks must hold whole tile bands */
