@@ -28,6 +28,9 @@ def child(steps=3, kernels=False):
         amvpt.set_chunk_lanes(int(os.environ["AB_CHUNK"]))
     if os.environ.get("AB_TRAV"):
         amvpt.set_traversal(int(os.environ["AB_TRAV"]))
+    if os.environ.get("AB_BVH"):   # "max_leaf_prims:traversal_cost" for the scene build (amvpt_set_bvh_build)
+        leaf, cost = os.environ["AB_BVH"].split(":")
+        amvpt.hip_lib().amvpt_set_bvh_build(int(leaf), float(cost))
     cfg = dict(CONFIGS[os.environ.get("AB_CONFIG", "M")])
     scene = cfg.pop("scene")
     s = amvpt.load_file(os.path.join(REPO, "scenes", scene), **cfg)
