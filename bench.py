@@ -148,11 +148,12 @@ def main():
             p.n_views // G // world, G, rect[2], rect[3], adist.FILTER_BORDER)
         film_bytes = ww * wh * C * 4
 
-        def step(counters=None):
+        def step(counters=None, flags=0):
             film.zero_()
             overflow[:4].zero_()
             c = dev.render_ex(vd, p, film.data_ptr(), lanes=lanes, window=win, overflow_ptr=overflow.data_ptr(),
-                              overflow_capacity=ov_cap, stream=stream, counters=counters, exchange=exchange)
+                              overflow_capacity=ov_cap, stream=stream, counters=counters, exchange=exchange,
+                              flags=flags)
             adist.gather_windows(film, win, overflow, quilt, [g[1] for g in groups], dst=0)
             return c
     else:
@@ -167,10 +168,11 @@ def main():
         film_bytes = quilt_bytes
         band = [lane_begin, lane_end]
 
-        def step(counters=None):
+        def step(counters=None, flags=0):
             film.zero_()
             c = dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt.LaneSet(band[0], band[1], 0, 0, 0, 0),
-                              stream=stream, counters=counters, exchange=exchange if world > 1 else None)
+                              stream=stream, counters=counters, exchange=exchange if world > 1 else None,
+                              flags=flags)
             adist.reduce_film(film, dst=0)
             return c
 
@@ -217,10 +219,13 @@ def main():
     total_samples = lanes_per_pass * n_passes * args.steps if lane_sharded else samples_per_rank * world * args.steps
     value = total_samples / elapsed / 1e6
 
-    # ---- one instrumented frame (outside the timed region): per-kernel HIP-event times + lane counters
+    # ---- one instrumented frame (outside the timed region): per-kernel HIP-event times + lane counters.
+    # Every chunk on the render stream (AMVPT_OPT_ONE_STREAM): with the second chunk stream the kernels of
+    # two chunks overlap and their event intervals would double-count the frame (the same kernels and
+    # results; the timed region above keeps the default two streams)
     cnt = amvpt.Counters()
     torch.cuda.synchronize()
-    step(cnt)
+    step(cnt, flags=amvpt.OPT_ONE_STREAM)
     torch.cuda.synchronize()
     c = cnt.as_dict()
     lanes = c["lanes"]
@@ -235,7 +240,7 @@ def main():
     launches = kl[dom]
     per_launch_bytes = bytes_kernel[dom] / launches
     achieved = per_launch_bytes / (kms[dom] / launches * 1e-3) / 1e9
-    kernel_name = {"k_splat": ("k_splat_multi<%d, %d>" % (G, C)) if G > 1 else "k_splat_single<%d>" % C,
+    kernel_name = {"k_splat": ("k_splat_multi<%d, %d," % (G, C)) if G > 1 else "k_splat_single<%d>" % C,
                    "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
                    "k_prim_req": "k_prim_req<%d," % G, "k_suffix": "k_suffix_fused<",
                    "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1
@@ -353,7 +358,7 @@ def rmse_window(dev, sd, vd, p, plan, n, stream):
     torch.cuda.synchronize()
     g = film.cpu().numpy()
     del film
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_cores()[0]
     O.build()
     o, _, st = O.render(sd, vd, p, lane_begin=b, lane_end=e, threads=threads)
     touched = (g[..., -1] != 0) | (o[..., -1] != 0)
@@ -374,7 +379,7 @@ def kernel_bytes(c, G, C):
     rec = c["record_bytes"] or 16         # lane records (4 x 16 B) + lane_out + view records (amvpt_counters)
     adapt = c["adaptive_lanes"]
     state = 80                            # path state: 5 float4 planes (store_state)
-    nee = 52                              # NEE record: origin + destination, light point + thr, thr + contribution
+    nee = 40                              # NEE record: origin + destination, light point + the visible result
     fused = c["kernel_launches"]["k_shadow"] == 0   # NEE traced inside k_bounce (brute-force scenes)
     return {
         # hit record out (+ the visibility requests when k_prim_req is fused into it)
@@ -386,7 +391,7 @@ def kernel_bytes(c, G, C):
         "k_extend": 48 * suffix,                                    # ray in, hit out
         # state + hit in; survivors' state out; terminated paths' result out; NEE records out (split)
         "k_bounce": (state + 16) * suffix + state * (suffix - pushed) + 16 * pushed + (0 if fused else nee * shadow),
-        "k_shadow": (nee + 32) * shadow,                            # NEE record in, result read-modify-write
+        "k_shadow": (nee + 12) * shadow,                            # NEE record in, the visible result written
         "k_splat": rec * lanes + 16 * adapt,                        # records in (film: PMC WRITE_SIZE)
         # fused suffix (brute-force scenes): each path's state in once, its result out once; the
         # vertices in between stay in registers
@@ -426,7 +431,7 @@ def pmc_traffic(kernel_name, config, rev):
     """HBM bytes per launch of `kernel_name` from a committed rocprofv3 PMC summary (profiles/r*_traffic.json,
     tools/pmc_traffic.py: separate FETCH_SIZE and WRITE_SIZE passes of this bench) of this config and
     source revision; (None, reason) otherwise."""
-    d, src = _profile("r*_traffic.json", config, rev)
+    d, src = _profile("r*_traffic*.json", config, rev)
     if d is None:
         return None, src
     key = kernel_name.replace(" ", "")
@@ -439,11 +444,11 @@ def pmc_traffic(kernel_name, config, rev):
 def pmc_valu(kms, kl, G, config, rev):
     """Per kernel: VALU wave-instructions per launch (committed profiles/r*_valu.json of this config and source
     revision, tools/pmc_valu.py) over this run's mean launch time, as a fraction of the chip's VALU issue peak."""
-    d, src = _profile("r*_valu.json", config, rev)
+    d, src = _profile("r*_valu*.json", config, rev)
     if d is None:
         return {"source": src, "kernels": {}}
     peak = d["peak_valu_ginst_s"]
-    sym = {"k_splat": "k_splat_multi<%d," % G, "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
+    sym = {"k_splat": ("k_splat_multi<%d," % G) if G > 1 else "k_splat_single<", "k_vis": "k_vis<%d," % G, "k_mv_primary": "k_mv_primary<%d," % G,
            "k_prim_req": "k_prim_req<%d," % G, "k_suffix": "k_suffix_fused<",
            "k_prim_hit": ("k_prim_hit_req<%d," % G) if kl.get("k_prim_req", 0) == 0 and G > 1 else "k_prim_hit<"}
     out = {"peak_Ginst_s": peak, "source": src, "kernels": {}}
@@ -460,10 +465,30 @@ def pmc_valu(kms, kl, G, config, rev):
     return out
 
 
+def host_cores():
+    """(usable, machine): the host CPUs this process may run on -- its affinity set, bounded by the cgroup
+    CPU quota when one is set (a GPU box's share of a larger machine) -- and os.cpu_count()."""
+    machine = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else machine
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and txt and txt[0] != "max":
+            usable = min(usable, max(1, int(int(txt[0]) / int(txt[1]))))
+        elif path.endswith("quota_us") and txt and int(txt[0]) > 0:
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            usable = min(usable, max(1, int(txt[0]) // period))
+        break
+    return usable, machine
+
+
 def cpu_baseline(sd, vd, p, target_seconds):
-    """Oracle (CPU restatement of mvpath, not Dr.Jit llvm_rgb) on a bounded lane sample of pass 0."""
+    """Oracle (CPU restatement of mvpath, not Dr.Jit llvm_rgb) on a bounded lane sample of pass 0, one
+    thread per usable host core."""
     from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, machine = host_cores()
     try:
         O.build()
         n = 1 << 16
@@ -473,7 +498,9 @@ def cpu_baseline(sd, vd, p, target_seconds):
                 break
             n = int(min(1 << 27, n * max(2.0, 1.2 * target_seconds / max(st["seconds"], 1e-3))))
             n = (n // 4096) * 4096
-        return {"value": round(n / st["seconds"] / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+        return {"value": round(n / st["seconds"] / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+                "host_cpus": machine, "cores_note": "threads = the CPUs this process may use (affinity set, "
+                "cgroup CPU quota); host_cpus = os.cpu_count() of the machine", "kind": "port",
                 "sample": "lanes [0, %d) of pass 0 of the same workload (%.1f s); CPU restatement of mvpath "
                           "(oracle/, brute-force intersection), not Dr.Jit llvm_rgb" % (n, st["seconds"])}
     except Exception as e:  # the baseline is reported, never the product path

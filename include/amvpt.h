@@ -153,6 +153,11 @@ typedef struct amvpt_params {
     uint32_t hide_emitters;
     uint32_t sa_reuse, sa_mis, fast_mis, debug;
     uint32_t adaptive;
+    /* mvpath: spp_pass_lim (mvpath.h:127, default 16).  The stock path integrator: its samples_per_pass
+     * (integrator.cpp:107, 0 = unset): a frame of several passes continues every lane's sampler stream
+     * from pass to pass as the reference's JIT render does (integrator.cpp:279-330); an spp it does not
+     * divide is refused with the reference's message.  Either integrator also splits a pass of more than
+     * 2^32 - 1 lanes (integrator.cpp:249-265). */
     uint32_t spp_pass_lim;
     uint32_t reuse_count;
     /* sampler (independent.cpp) */

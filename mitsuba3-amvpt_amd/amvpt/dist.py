@@ -106,7 +106,20 @@ def reduce_film(film, dst=0):
 # View-group partition (C5)
 # ---------------------------------------------------------------------------------------------------
 
-FILTER_BORDER = 4   # pixels around a rank's tiles its splats can reach (Gaussian radius 2 + jitter)
+FILTER_BORDER = 4   # the smallest border: the default Gaussian (radius 2) with a cell to spare
+
+
+def filter_border(params):
+    """Pixels around a rank's tiles its splats can reach (host/multi.cpp filter_border): ImageBlock::put's
+    footprint reaches ceil(radius - 1/2) cells coalesced, ceil(radius + 1/2) not coalesced, radius = 4
+    stddev (gaussian.cpp:48-60); the box filter stays in its pixel.  At least FILTER_BORDER."""
+    import math
+    import numpy as np
+    if params.rfilter == 0:   # AMVPT_RFILTER_BOX
+        return FILTER_BORDER
+    stddev = params.rfilter_stddev if params.rfilter_stddev > 0 else 0.5
+    radius = float(np.float32(4.0) * np.float32(stddev))
+    return max(FILTER_BORDER, int(math.ceil(np.float32(radius) + np.float32(0.5))))
 
 
 def view_tile(params, v):
@@ -150,9 +163,10 @@ def view_group_partition(params, group, world):
         if rect is None:
             return None
         x0, y0, w, h = rect
-        wx0, wy0 = max(0, x0 - FILTER_BORDER), max(0, y0 - FILTER_BORDER)
-        wx1 = min(params.film_width, x0 + w + FILTER_BORDER)
-        wy1 = min(params.film_height, y0 + h + FILTER_BORDER)
+        b = filter_border(params)
+        wx0, wy0 = max(0, x0 - b), max(0, y0 - b)
+        wx1 = min(params.film_width, x0 + w + b)
+        wy1 = min(params.film_height, y0 + h + b)
         out.append((rect, (wx0, wy0, wx1 - wx0, wy1 - wy0)))
     return out
 

@@ -119,7 +119,27 @@ struct KParams {
     uint32_t vs_stride;   /* Bufs::vstate: floats between a field's consecutive view slots (the chunk) */
     unsigned long long *film_fx;   /* deterministic mode: 32.32 fixed-point shadow of the film (else null) */
     float *film_base;              /* the film the shadow mirrors (film_fx index = film float index) */
+    /* stock `path` over several passes (integrator.cpp:279-330): the sampler is seeded once and every
+     * pass continues each lane's PCG32 stream -- rng_in (passes > 0) holds the state each lane starts the
+     * pass with, rng_out (all but the last pass) receives the state its path ends with; both indexed by
+     * the lane's virtual index in the render's lane set */
+    unsigned long long *rng_in, *rng_out;
 };
+
+/* the PCG32 a stock-path lane starts the pass with: TEA-seeded, or the previous pass's state (same
+ * stream increment) */
+AD Pcg pass_rng(const KParams &P, uint32_t lane, uint64_t v) {
+    uint32_t v0, v1;
+    tea4(P.seed_value, lane, v0, v1);
+    Pcg rng;
+    if (P.rng_in) {
+        rng.state = P.rng_in[v];
+        rng.inc = (((uint64_t) v1) << 1) | 1u;
+    } else {
+        rng.seed(v0, v1);
+    }
+    return rng;
+}
 
 /* SoA streams of one chunk */
 constexpr int kQPlanes = 5;   /* float4 planes of a path state (80 B, see store_state) */
@@ -143,8 +163,8 @@ struct Bufs {
                                 * render's flagged lanes below it): entry e of asel is entry
                                 * e + run_delta[run] of the pass's compressed array */
     float4 *hit;          /* k_extend / k_prim_hit -> shading: closest hit (t, u, v, prim) per entry */
-    float4 *nee[3];       /* k_bounce -> k_shadow: deferred emitter-sample shadow rays (NEE records), */
-    float *nee_cb;        /* + the contribution's blue channel as a float plane (52 B per record) */
+    float4 *nee[2];       /* k_bounce -> k_shadow: deferred emitter-sample shadow rays (NEE records), */
+    float2 *nee_gb;       /* + the visible result's green and blue channels (40 B per record) */
     uint32_t *cnt_nee;
     float4 *vreq[3];      /* k_prim_req -> k_vis: (p, bits), (n, ap.x), (emitter point, ap.y) per lane */
     unsigned long long *occ; /* k_vis -> k_mv_primary: occlusion ballots, word (i >> 6) * G + slot */
@@ -1428,7 +1448,8 @@ AD uint32_t push_slot(bool want, uint32_t *counters, uint32_t qcap) {
 struct PathState {
     Ray ray;
     C3 thr, res;
-    float eta, prev_pdf;
+    bool eta_zero;        /* the eta product is 0 (else 1: every supported BSDF samples eta 1, or 0 when empty) */
+    float prev_pdf;
     uint32_t depth;
     bool prev_delta, valid_ray;
     f3 prev_p;
@@ -1448,7 +1469,7 @@ struct PathState {
  * stored.  k_shadow adds NEE into q4's xyz in place.
  */
 AD void store_state(float4 *const *q, uint32_t slot, const PathState &s) {
-    const uint32_t bits = (s.depth & 0x1fffffffu) | (s.eta == 0.f ? 0x20000000u : 0u) |
+    const uint32_t bits = (s.depth & 0x1fffffffu) | (s.eta_zero ? 0x20000000u : 0u) |
                           (s.prev_delta ? 0x40000000u : 0u) | (s.valid_ray ? 0x80000000u : 0u);
     q[0][slot] = make_float4(s.ray.o.x, s.ray.o.y, s.ray.o.z, s.ray.d.x);
     q[1][slot] = make_float4(s.ray.d.y, s.ray.d.z, s.thr.r, s.thr.g);
@@ -1467,7 +1488,7 @@ AD PathState load_state(float4 *const *q, uint32_t slot) {
     s.prev_pdf = c.y;
     const uint32_t bits = fbits(c.z);
     s.depth = bits & 0x1fffffffu;
-    s.eta = (bits & 0x20000000u) ? 0.f : 1.f;
+    s.eta_zero = (bits & 0x20000000u) != 0;
     s.prev_delta = (bits & 0x40000000u) != 0;
     s.valid_ray = (bits & 0x80000000u) != 0;
     s.prev_p = mk(d.x, d.y, d.z);
@@ -1525,10 +1546,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
         const uint32_t lane = lane_of(P, P.chunk_begin + i);
         int px, py;
         lane_pixel(P, lane, px, py);
-        uint32_t v0, v1;
-        tea4(P.seed_value, lane, v0, v1);
-        Pcg rng;
-        rng.seed(v0, v1);
+        Pcg rng = pass_rng(P, lane, P.chunk_begin + i);
         float jx = rng.next_1d(), jy = rng.next_1d();
         float sx = (float) px + jx, sy = (float) py + jy;
         float apx = .5f, apy = .5f;
@@ -1536,13 +1554,14 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
         uint32_t index;
         s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, P.adj_ox), fmadd(sy, P.inv_h, P.adj_oy), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
-        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
+        s.eta_zero = false; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
         s.prev_p = mk(0.f, 0.f, 0.f);
         s.idx = slot;
         s.rng_state = rng.state;
-        s.rng_seq = v1;
+        s.rng_seq = (uint32_t) (rng.inc >> 1);
         if (P.max_depth == 0) {
             B.lane_out[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (P.rng_out) P.rng_out[P.chunk_begin + i] = rng.state;   /* path.cpp: no draw past the camera's */
             ok = false;
         }
     }
@@ -1587,7 +1606,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
         uint32_t index;
         s.ray = sample_ray_idx(P, V, fmadd(sx, P.inv_w, P.adj_ox), fmadd(sy, P.inv_h, P.adj_oy), index, apx, apy);
         s.thr = c3(1.f); s.res = c3(0.f);
-        s.eta = 1.f; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
+        s.eta_zero = false; s.prev_pdf = 1.f; s.depth = 0; s.prev_delta = true; s.valid_ray = P.valid_ray0 != 0;
         s.prev_p = mk(0.f, 0.f, 0.f);
         s.idx = slot;
         s.rng_state = rng.state;
@@ -1668,15 +1687,14 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
             d = d / dist;
             const Ray r{o, d, dist * (1.f - kShadowEps)};
             if (!walk_any<kWalk>(sc, r)) {
-                const float4 t = B.nee[2][i];
-                const float cb = B.nee_cb[i];
+                /* the light is visible: the path's result becomes the record's fma(throughput,
+                 * contribution, result), formed by k_bounce (its .w -- valid_ray / rng hi -- stays) */
+                const float2 gb = B.nee_gb[i];
                 const uint32_t dest = fbits(a.w);
-                float4 *const dp = (dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest];
-                float4 v = *dp;
-                v.x = fmadd(b.w, t.z, v.x);
-                v.y = fmadd(t.x, t.w, v.y);
-                v.z = fmadd(t.y, cb, v.z);
-                *dp = v;
+                float *const dp = (float *) ((dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest]);
+                dp[0] = b.w;
+                dp[1] = gb.x;
+                dp[2] = gb.y;
             }
         }
     }
@@ -1687,17 +1705,30 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
 #ifndef AMVPT_BOUNCE_WAVES
 #define AMVPT_BOUNCE_WAVES 5
 #endif
+/* bounce_vertex's state hooks when the whole path state stays in registers (k_bounce) */
+struct NoPark {
+    AD void in(PathState &, Pcg &) const {}
+    AD void res_out(const PathState &) const {}
+    AD void nee_out(C3 &, f3 &) const {}
+    AD void nee_to_in(f3 &) const {}
+    AD void out(const PathState &, const Pcg &) const {}
+};
+
 /*
  * One suffix vertex (mvpath_multi.h:563-686 == mvpath_single.h:130-275): emitter-hit MIS at the
  * ray's hit, emitter sample, BSDF eval/sample, Russian roulette.  s advances in place; returns
- * whether the path continues; nee = the emitter sample's shadow ray shr (to nee_to) carries
- * fma(nee_thr, nee_c, result) if unoccluded.  Shared by k_bounce and k_suffix_fused.
+ * whether the path continues; nee = the emitter sample's shadow ray shr (to nee_to) leaves the path
+ * with result res_nee if unoccluded.  Shared by k_bounce and k_suffix_fused.  pk moves the fields
+ * the vertex does not touch between its phases out of registers (k_suffix_fused's LdsPark): in()
+ * brings them in before the emitter-hit term, res_out() takes the result out once the NEE term is
+ * formed, out() the rest at the end.
  */
-template <bool kDiff>
+template <bool kDiff, class Pk = NoPark>
 AD bool bounce_vertex(const KParams &P, const DScene &S, const SceneRef &sc, PathState &s, Pcg &rng, const Hit &hit,
-                      bool &nee, Ray &shr, f3 &nee_to, C3 &nee_thr, C3 &nee_c) {
+                      bool &nee, Ray &shr, f3 &nee_to, C3 &res_nee, const Pk &pk = Pk()) {
     SI si = compute_si(sc, s.ray, hit);
     int32_t em = si_emitter(sc, si);
+    pk.in(s, rng);
     {
         DSamp ds = ds_zero();
         ds.p = si.p; ds.n = si.sh.n;
@@ -1713,41 +1744,54 @@ AD bool bounce_vertex(const KParams &P, const DScene &S, const SceneRef &sc, Pat
     int32_t b = si.valid() ? S.shapes[si.shape].bsdf : -1;
     bool active_em = active_next && (bsdf_flags(S.bsdfs, b) & BF_Smooth);
     float e1 = rng.next_1d(), e2 = rng.next_1d();
-    DSamp ds;
-    C3 em_w;
-    sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
-    active_em = active_em && ds.pdf != 0.f;   /* ds.pdf != 0 <=> the reference traces the ray */
-    f3 wo = si.sh.to_local(ds.d);
+    {
+        DSamp ds;
+        C3 em_w;
+        sample_emitter_direction(sc, si, e1, e2, active_em, ds, em_w);
+        active_em = active_em && ds.pdf != 0.f;   /* ds.pdf != 0 <=> the reference traces the ray */
+        f3 wo = si.sh.to_local(ds.d);
+        C3 bval;
+        float bpdf;
+        bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
+        /* the NEE term is settled before the BSDF sample (which does not read it), so the emitter
+         * sample, the BSDF value and pdf die here instead of living across the sample and the
+         * shadow walk: the caller keeps only the result the path has if the light is visible,
+         * fma(throughput, contribution, result) -- the reference's accumulation, evaluated early
+         * (s.res does not change again in this vertex) */
+        if (active_em) {
+            float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
+            nee = true;
+            res_nee = cfma(s.thr, bval * em_w * mis_em, s.res);
+            nee_to = ds.p;
+            pk.nee_out(res_nee, nee_to);
+        }
+    }
+    pk.res_out(s);
     float s1 = rng.next_1d();
     float s2a = rng.next_1d(), s2b = rng.next_1d();
     (void) s1;
-    C3 bval;
-    float bpdf;
-    bsdf_eval_pdf<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, wo, true, bval, bpdf);
     BSample bs;
     C3 bw;
     bsdf_sample<kDiff>(S.bsdfs, b, CTX_ALL, si.wi, s2a, s2b, true, bs, bw);
-    if (active_em) {
-        float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bpdf);
-        nee = true;
-        nee_thr = s.thr;
-        nee_c = bval * em_w * mis_em;
-        shr = spawn_ray_to(si.p, si.n, ds.p);
-        nee_to = ds.p;
-    }
     s.ray = spawn_ray(si.p, si.n, si.sh.to_world(bs.wo));
+    if (nee) {
+        pk.nee_to_in(nee_to);
+        shr = spawn_ray_to(si.p, si.n, nee_to);
+    }
     s.thr = s.thr * bw;
-    s.eta *= bs.eta;
+    s.eta_zero = s.eta_zero || bs.eta == 0.f;
     s.prev_p = si.p;
     s.prev_pdf = bs.pdf;
     s.prev_delta = (bs.type & BF_Delta) != 0;
     if (si.valid()) s.depth += 1;
     float tmax = cmax(s.thr);
-    float rr_prob = vmin(tmax * sqr(s.eta), .95f);
+    const float eta = s.eta_zero ? 0.f : 1.f;
+    float rr_prob = vmin(tmax * sqr(eta), .95f);
     bool rractive = s.depth >= P.rr_depth;
     bool rr_continue = rng.next_1d() < rr_prob;
     s.valid_ray = s.valid_ray || (si.valid() && !(bs.type & BF_Null));
     if (rractive) s.thr = s.thr * rcp(rr_prob);
+    pk.out(s, rng);
     return active_next && (!rractive || rr_continue) && (tmax != 0.f);
 }
 
@@ -1773,15 +1817,16 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
         bool keep = false, nee = false;
         Ray shr;
         f3 nee_to;
-        C3 nee_thr, nee_c;
+        C3 res_nee;
         if (ok) {
             s = load_state(B.q_in, i);
             Pcg rng;
             rng.state = s.rng_state;
             rng.inc = (((uint64_t) path_seq(P, B, s.idx)) << 1) | 1u;
             ++verts;
-            keep = bounce_vertex<kDiff>(P, S, sc, s, rng, hit_of(B.hit[i]), nee, shr, nee_to, nee_thr, nee_c);
+            keep = bounce_vertex<kDiff>(P, S, sc, s, rng, hit_of(B.hit[i]), nee, shr, nee_to, res_nee);
             s.rng_state = rng.state;
+            if (!keep && P.rng_out) P.rng_out[P.chunk_begin + slot_lane(P, s.idx)] = rng.state;
             if (kNee < 0 && !keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
         }
         shadows += nee ? 1 : 0;
@@ -1789,7 +1834,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             /* every lane of the wave walks (wave-uniform brute force); lanes without a shadow ray
              * start as found */
             const bool occluded = brute_any<kNee == WALK_BRUTE>(sc, shr, !nee);
-            if (nee && !occluded) s.res = cfma(nee_thr, nee_c, s.res);
+            if (nee && !occluded) s.res = res_nee;
             if (ok && !keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
         }
         const uint32_t slot = push_slot(keep, B.cnt_out, B.qcap);
@@ -1798,12 +1843,11 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
         const uint32_t ns = push_slot(nee, B.cnt_nee, B.qcap);
         if (nee) {
             const uint32_t dest = keep ? slot : (0x80000000u | s.idx);
-            /* (origin, destination), (light point, thr.r), (thr.gb, c.rg), c.b: k_shadow re-derives the
-             * direction and extent exactly as spawn_ray_to did */
+            /* (origin, destination), (light point, visible result .r), visible result .gb: k_shadow
+             * re-derives the direction and extent exactly as spawn_ray_to did */
             B.nee[0][ns] = make_float4(shr.o.x, shr.o.y, shr.o.z, bitsf(dest));
-            B.nee[1][ns] = make_float4(nee_to.x, nee_to.y, nee_to.z, nee_thr.r);
-            B.nee[2][ns] = make_float4(nee_thr.g, nee_thr.b, nee_c.r, nee_c.g);
-            B.nee_cb[ns] = nee_c.b;
+            B.nee[1][ns] = make_float4(nee_to.x, nee_to.y, nee_to.z, res_nee.r);
+            B.nee_gb[ns] = make_float2(res_nee.g, res_nee.b);
         }
     }
     if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
@@ -1839,17 +1883,87 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
  * 5 waves (no spills) 1480 vs 1510 Msamples/s at 6 (r03m) */
 #define AMVPT_FUSED_WAVES 6
 #endif
+#ifndef AMVPT_FUSED_PARK
+/* path-state groups k_suffix_fused keeps in LDS between the phases that use them (LdsPark) */
+#define AMVPT_FUSED_PARK 0x2f
+#endif
+enum : int { PK_RES = 1, PK_PREV = 2, PK_THR = 4, PK_RNG = 8, PK_RAY = 16, PK_NEE = 32 };
+/* LDS slots (floats) of a parked path: field f of block thread t at base[f * 256 + t] */
+enum : int { PF_RES = 0, PF_IDX = 3, PF_PREVP = 4, PF_PREVPDF = 7, PF_THR = 8, PF_DEPTH = 11, PF_RNG = 12, PF_RESNEE = 16,
+             PF_NEETO = 19, PF_RAY = 22 };
+/* slots in use: the ray's only with PK_RAY */
+constexpr int park_fields(int m) { return (m & PK_RAY) ? 28 : (m & PK_NEE) ? 22 : 16; }
+constexpr uint32_t kFusedBlock = 256;
+/*
+ * The fused suffix's path state between phases, one LDS slot per field and lane (field-major, so a
+ * wave's 64 accesses of one field hit 64 distinct banks).  A vertex needs its previous point and pdf
+ * only for the emitter-hit term, its result only there and for the NEE term, its lane slot only when
+ * the path ends, its throughput, depth and sampler state only inside bounce_vertex, and its ray only
+ * for the closest-hit walk: kept in registers across the walks and the BSDF sample, they made the
+ * 6-wave allocation spill to scratch (config M 60 B, the glossy C3 instance 120 B per lane, 1.8x /
+ * 5.6x the kernel's algorithmic HBM bytes, round 3).  Volatile accesses: the compiler must not keep a
+ * register copy of a value it stored (store-to-load forwarding would make the register live again).
+ */
+typedef __attribute__((address_space(3))) float lds_float;
+template <int kMask> struct LdsPark {
+    lds_float *b;   /* an LDS-space pointer: a generic one becomes 64-bit flat accesses */
+    AD void put(int f, float v) const { *(volatile lds_float *) (b + f * (int) kFusedBlock) = v; }
+    AD float get(int f) const { return *(volatile lds_float *) (b + f * (int) kFusedBlock); }
+    AD void put3(int f, f3 v) const { put(f, v.x); put(f + 1, v.y); put(f + 2, v.z); }
+    AD f3 get3(int f) const { return mk(get(f), get(f + 1), get(f + 2)); }
+    AD void putc(int f, C3 v) const { put(f, v.r); put(f + 1, v.g); put(f + 2, v.b); }
+    AD C3 getc(int f) const { return C3{get(f), get(f + 1), get(f + 2)}; }
+    AD void put_u64(int f, uint64_t v) const { put(f, bitsf((uint32_t) v)); put(f + 1, bitsf((uint32_t) (v >> 32))); }
+    AD uint64_t get_u64(int f) const { return (uint64_t) fbits(get(f)) | ((uint64_t) fbits(get(f + 1)) << 32); }
+    /* a path fetched from the queue: everything parked goes to LDS */
+    AD void fetch(const PathState &s, const Pcg &rng) const {
+        if (kMask & PK_RES) { putc(PF_RES, s.res); put(PF_IDX, bitsf(s.idx)); }
+        if (kMask & PK_PREV) { put3(PF_PREVP, s.prev_p); put(PF_PREVPDF, s.prev_pdf); }
+        if (kMask & PK_THR) { putc(PF_THR, s.thr); put(PF_DEPTH, bitsf(s.depth)); }
+        if (kMask & PK_RNG) { put_u64(PF_RNG, rng.state); put_u64(PF_RNG + 2, rng.inc); }
+    }
+    AD void in(PathState &s, Pcg &rng) const {
+        if (kMask & PK_PREV) { s.prev_p = get3(PF_PREVP); s.prev_pdf = get(PF_PREVPDF); }
+        if (kMask & PK_THR) { s.thr = getc(PF_THR); s.depth = fbits(get(PF_DEPTH)); }
+        if (kMask & PK_RES) s.res = getc(PF_RES);
+        if (kMask & PK_RNG) { rng.state = get_u64(PF_RNG); rng.inc = get_u64(PF_RNG + 2); }
+    }
+    AD void res_out(const PathState &s) const { if (kMask & PK_RES) putc(PF_RES, s.res); }
+    /* the NEE term waits in LDS during the BSDF sample (its result until the shadow walk's verdict) */
+    AD void nee_out(C3 &res_nee, f3 &nee_to) const {
+        if (kMask & PK_NEE) { putc(PF_RESNEE, res_nee); put3(PF_NEETO, nee_to); }
+    }
+    AD void nee_to_in(f3 &nee_to) const { if (kMask & PK_NEE) nee_to = get3(PF_NEETO); }
+    AD C3 res_nee(C3 r) const { return (kMask & PK_NEE) ? getc(PF_RESNEE) : r; }
+    AD void out(const PathState &s, const Pcg &rng) const {
+        if (kMask & PK_PREV) { put3(PF_PREVP, s.prev_p); put(PF_PREVPDF, s.prev_pdf); }
+        if (kMask & PK_THR) { putc(PF_THR, s.thr); put(PF_DEPTH, bitsf(s.depth)); }
+        if (kMask & PK_RNG) { put_u64(PF_RNG, rng.state); put_u64(PF_RNG + 2, rng.inc); }
+    }
+    /* the result after the NEE walk, and the lane slot, when the path ends */
+    AD C3 res(const PathState &s) const { return (kMask & PK_RES) ? getc(PF_RES) : s.res; }
+    AD void set_res(PathState &s, C3 v) const { if (kMask & PK_RES) putc(PF_RES, v); else s.res = v; }
+    AD uint32_t idx(const PathState &s) const { return (kMask & PK_RES) ? fbits(get(PF_IDX)) : s.idx; }
+    AD uint64_t rng_state(const Pcg &rng) const { return (kMask & PK_RNG) ? get_u64(PF_RNG) : rng.state; }
+};
+template <int kMask> constexpr uint32_t park_lds_bytes() { return kMask ? park_fields(kMask) * 4u * kFusedBlock : 0u; }
+constexpr uint32_t kFusedParkBytes = park_lds_bytes<AMVPT_FUSED_PARK>();
+
 template <bool kTab, bool kDiff, int kW>
-__global__ void __launch_bounds__(256, AMVPT_FUSED_WAVES) k_suffix_fused(KParams P, const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(kFusedBlock, AMVPT_FUSED_WAVES) k_suffix_fused(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int kPk = AMVPT_FUSED_PARK;
+    /* the parked state sits in front of the staged tables (dynamic LDS: [park][tables]) */
+    const LdsPark<kPk> pk{(lds_float *) (uint32_t) (uintptr_t) lds + threadIdx.x};
     DScene S = *Sp;
-    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<kTab, false>(S, lds + kFusedParkBytes, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     uint32_t *const work = B.cnt_out + part * kCntStride;
-    unsigned long long verts = 0, shadows = 0;
+    uint64_t verts = 0, shadows = 0;
     PathState s;
     s.ray = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), kLargest};
+    if (kPk & PK_RAY) { pk.put3(PF_RAY, s.ray.o); pk.put3(PF_RAY + 3, s.ray.d); }
     Pcg rng;
     bool live = false, drained = false;
     for (;;) {
@@ -1861,32 +1975,42 @@ __global__ void __launch_bounds__(256, AMVPT_FUSED_WAVES) k_suffix_fused(KParams
                 s = load_state(B.q_in, pbase + j);
                 rng.state = s.rng_state;
                 rng.inc = (((uint64_t) path_seq(P, B, s.idx)) << 1) | 1u;
+                pk.fetch(s, rng);
+                if (kPk & PK_RAY) { pk.put3(PF_RAY, s.ray.o); pk.put3(PF_RAY + 3, s.ray.d); }
                 live = true;
             }
         }
         if (!wave_any(live)) break;
         constexpr bool kBruteW = kW == WALK_BRUTE || kW == WALK_BRUTE_NS;
+        if (kPk & PK_RAY) s.ray = Ray{pk.get3(PF_RAY), pk.get3(PF_RAY + 3), kLargest};
         Hit h{kInf, 0.f, 0.f, -1};
         if (kBruteW || live) h = walk_closest<kW>(sc, s.ray);   /* brute force: every lane of the wave walks */
         bool keep = false, nee = false;
         Ray shr;
         f3 nee_to;
-        C3 nee_thr, nee_c;
-        if (live) {
-            ++verts;
-            keep = bounce_vertex<kDiff>(P, S, sc, s, rng, h, nee, shr, nee_to, nee_thr, nee_c);
-        }
-        shadows += nee ? 1 : 0;
+        C3 res_nee;
+        if (live) keep = bounce_vertex<kDiff>(P, S, sc, s, rng, h, nee, shr, nee_to, res_nee, pk);
+        /* the continuation ray waits in LDS during the shadow walk */
+        if ((kPk & PK_RAY) && live) { pk.put3(PF_RAY, s.ray.o); pk.put3(PF_RAY + 3, s.ray.d); }
+        /* wave-level counts in scalar registers (no per-lane 64-bit counters across the loop) */
+        verts += (uint32_t) __popcll(__ballot(live));
+        shadows += (uint32_t) __popcll(__ballot(nee));
         bool occluded = true;
         if constexpr (kBruteW) occluded = brute_any<kW == WALK_BRUTE>(sc, shr, !nee);
         else if (nee) occluded = walk_any<kW>(sc, shr);
-        if (nee && !occluded) s.res = cfma(nee_thr, nee_c, s.res);
+        if (nee && !occluded) pk.set_res(s, pk.res_nee(res_nee));
         if (live && !keep) {
-            B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
+            const C3 r = pk.res(s);
+            const uint32_t idx = pk.idx(s);
+            B.lane_out[idx] = make_float4(r.r, r.g, r.b, s.valid_ray ? 1.f : 0.f);
+            if (P.rng_out) P.rng_out[P.chunk_begin + slot_lane(P, idx)] = pk.rng_state(rng);
             live = false;
         }
     }
-    if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
+    if (B.stats && __lane_id() == 0) {
+        if (verts) atomicAdd(B.stats + 0 * kStatShards + blockIdx.x % kStatShards, (unsigned long long) verts);
+        if (shadows) atomicAdd(B.stats + 5 * kStatShards + blockIdx.x % kStatShards, (unsigned long long) shadows);
+    }
 }
 
 /* ------------------------------------------------------------------ */
@@ -1906,7 +2030,7 @@ __global__ void __launch_bounds__(kSplatBlock) k_splat_single(KParams P, Bufs B)
         const uint32_t lane = lane_of(P, P.chunk_begin + i);
         int px, py;
         lane_pixel(P, lane, px, py);
-        Pcg rng = lane_rng(P.seed_value, lane);
+        Pcg rng = pass_rng(P, lane, P.chunk_begin + i);
         float jx = rng.next_1d(), jy = rng.next_1d();
         float sx = (float) px + jx, sy = (float) py + jy;
         float4 lo = B.lane_out[slot];
@@ -2699,7 +2823,7 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                 ps.ray = pd_ray;
                 ps.thr = thr;
                 ps.res = c3(0.f);
-                ps.eta = bsmp.eta;
+                ps.eta_zero = bsmp.eta == 0.f;
                 ps.prev_pdf = bsmp.pdf;
                 ps.depth = p_hit ? 1u : 0u;
                 ps.prev_delta = flag_delta;
@@ -3178,8 +3302,10 @@ static void plan(const amvpt_params &P, uint32_t &spp, uint32_t &spp_pp, uint32_
         n_passes = s / spp_pp;
         s = n_passes * spp_pp;
     } else {
-        spp_pp = s;
-        n_passes = 1;
+        /* SamplingIntegrator::render (integrator.cpp:137-146): samples_per_pass travels in spp_pass_lim
+         * (0 = unset); render_impl refuses an spp it does not divide, as the reference throws */
+        spp_pp = P.spp_pass_lim ? std::min(P.spp_pass_lim, s) : s;
+        n_passes = s / spp_pp;
     }
     uint64_t wf = px * spp_pp;
     if (wf > 0xffffffffull) {
@@ -3268,6 +3394,8 @@ struct DevArena {
     hipEvent_t fork = nullptr, join = nullptr;
     void *fx = nullptr;   /* deterministic mode's fixed-point film */
     size_t fxbytes = 0;
+    void *carry = nullptr;   /* multi-pass stock path: two per-lane PCG32 state planes (rng_in / rng_out) */
+    size_t cbytes = 0;
 };
 static std::mutex g_arenas_mu;
 static std::map<int, std::unique_ptr<DevArena>> g_arenas;
@@ -3400,7 +3528,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const uint32_t G = reuse ? group_size(Pp) : 1;
     if (G > kMaxGWide) { set_error("amvpt_render: group size > 256 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
-    if (!is_mv && n_passes > 1) { set_error("path: more than 2^32 lanes per frame"); return AMVPT_ERR_UNSUPPORTED; }
+    if (!is_mv && Pp.spp_pass_lim && (Pp.spp ? Pp.spp : 1) % std::min(Pp.spp_pass_lim, Pp.spp ? Pp.spp : 1u)) {
+        set_error("sample_count (" + std::to_string(Pp.spp ? Pp.spp : 1) + ") must be a multiple of spp_per_pass (" +
+                  std::to_string(std::min(Pp.spp_pass_lim, Pp.spp ? Pp.spp : 1u)) + ").");
+        return AMVPT_ERR_INVALID;
+    }
+    /* the stock path's passes continue each lane's sampler (rng_in / rng_out) */
+    const bool rng_carry = !is_mv && n_passes > 1;
     if (Pp.multisensor && (Pp.grid_x == 0 || Pp.grid_y == 0 || Pp.film_width % Pp.grid_x || Pp.film_height % Pp.grid_y)) {
         set_error("Film size must be divisible by grid dimensions !");
         return AMVPT_ERR_INVALID;
@@ -3654,6 +3788,14 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         P.film_base = film;
     }
 
+    /* multi-pass stock path: the per-lane sampler states between passes, two planes used in turn */
+    unsigned long long *carry[2] = {nullptr, nullptr};
+    if (rng_carry) {
+        { const amvpt_status as_ = arena_reserve(A, A.carry, A.cbytes, (size_t) 16 * span, "sampler states"); if (as_ != AMVPT_OK) return as_; }
+        carry[0] = (unsigned long long *) A.carry;
+        carry[1] = carry[0] + span;
+    }
+
     /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
     uint8_t *d_amask = nullptr;
     uint32_t *d_asel = nullptr, *d_anum = nullptr, *d_runs = nullptr, *d_delta = nullptr;
@@ -3696,8 +3838,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.lane_out = (float4 *) carve(16 * chunk);
         for (int k = 0; k < 4; ++k) B.lrec[k] = (float4 *) carve(16 * chunk);
         B.hit = (float4 *) carve(16 * std::max<uint64_t>(chunk, qlen));
-        for (int k = 0; k < 3; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
-        B.nee_cb = (float *) carve(4 * qlen);
+        for (int k = 0; k < 2; ++k) B.nee[k] = (float4 *) carve(16 * qlen);
+        B.nee_gb = (float2 *) carve(8 * qlen);
         for (int k = 0; k < 3; ++k) B.vreq[k] = (float4 *) carve(16 * chunk);
         B.occ = (unsigned long long *) carve((size_t) 8 * G * ((chunk + 63) / 64));
         B.cnt_nee = cs.cntN;
@@ -3741,7 +3883,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.cnt_out = cntB;
             HIPCHK(hipMemsetAsync(cntB, 0, (size_t) kQParts * kCntStride * 4, st));
             T.begin(AMVPT_K_SUFFIX, st);
-            launch_suffix_fused(tab_b, diff, walk, dim3(kQParts * fused_blocks), lds, st, P, dS, B);
+            launch_suffix_fused(tab_b, diff, walk, dim3(kQParts * fused_blocks), kFusedParkBytes + lds, st, P, dS, B);
             T.end(st);
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);
@@ -3793,6 +3935,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         RoctxScope range_pass("amvpt pass");
         P.seed_value = Pp.base_seed + (is_mv ? (spp_pp * pass + Pp.seed) : Pp.seed);
         P.record = (records && pass == record_pass) ? 1u : 0u;
+        P.rng_in = rng_carry && pass > 0 ? carry[pass & 1u] : nullptr;
+        P.rng_out = rng_carry && pass + 1 < n_passes ? carry[(pass + 1) & 1u] : nullptr;
         for (uint64_t c0 = 0; c0 < span; c0 += chunk, ++chunk_index) {   /* virtual indices of the lane set */
             const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, span - c0);
             /* odd chunks on the side stream, which starts once the first chunk's primary stage is queued

@@ -28,6 +28,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <condition_variable>
 #include <cstring>
@@ -203,7 +204,15 @@ uint32_t group_size(const amvpt_params &p) {
     return G;
 }
 
-constexpr uint32_t kFilterBorder = 4;   /* amvpt.dist.FILTER_BORDER */
+/* pixels around a rank's tiles its splats can reach (amvpt.dist.filter_border): ImageBlock::put's footprint
+ * around a sample in the tile reaches ceil(radius - 1/2) cells (coalesced) or ceil(radius + 1/2) (not
+ * coalesced), radius = 4 stddev for the Gaussian (gaussian.cpp:48-60); the box filter stays in its pixel.
+ * At least 4, the default filter's border (radius 2) with a cell to spare. */
+static uint32_t filter_border(const amvpt_params &p) {
+    if (p.rfilter == AMVPT_RFILTER_BOX) return 4;
+    const float radius = 4.f * (p.rfilter_stddev > 0.f ? p.rfilter_stddev : .5f);
+    return std::max<uint32_t>(4, (uint32_t) std::ceil(radius + .5f));
+}
 
 }  // namespace
 
@@ -239,10 +248,11 @@ int amvpt_host_view_group_partition(const amvpt_params *p, uint32_t rank, uint32
     }
     if ((tx1 - tx0) * (ty1 - ty0) != v1 - v0) return 0;   /* not a rectangle of tiles */
     rect[0] = tx0 * sx; rect[1] = ty0 * sy; rect[2] = (tx1 - tx0) * sx; rect[3] = (ty1 - ty0) * sy;
-    const uint32_t wx0 = rect[0] > kFilterBorder ? rect[0] - kFilterBorder : 0;
-    const uint32_t wy0 = rect[1] > kFilterBorder ? rect[1] - kFilterBorder : 0;
-    const uint32_t wx1 = std::min(p->film_width, rect[0] + rect[2] + kFilterBorder);
-    const uint32_t wy1 = std::min(p->film_height, rect[1] + rect[3] + kFilterBorder);
+    const uint32_t border = filter_border(*p);
+    const uint32_t wx0 = rect[0] > border ? rect[0] - border : 0;
+    const uint32_t wy0 = rect[1] > border ? rect[1] - border : 0;
+    const uint32_t wx1 = std::min(p->film_width, rect[0] + rect[2] + border);
+    const uint32_t wy1 = std::min(p->film_height, rect[1] + rect[3] + border);
     window[0] = wx0; window[1] = wy0; window[2] = wx1 - wx0; window[3] = wy1 - wy0;
     return 1;
 }

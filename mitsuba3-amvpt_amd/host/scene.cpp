@@ -111,8 +111,18 @@ static FilmInfo make_film(const Properties &p) {
     if (pf == "rgb") f.alpha = false;
     else if (pf == "rgba") f.alpha = true;
     else Throw("hdrfilm: pixel_format \"" + pf + "\" is not implemented (rgb, rgba)");
+    /* output-file keys of hdrfilm (hdrfilm.cpp:172-215): they shape the written file, not the
+     * ImageBlock; the EXR writer (exr.cpp) writes float32 OpenEXR */
+    const std::string ff = lower(p.get_string("file_format", "openexr"));
+    if (ff != "openexr" && ff != "exr") Throw("hdrfilm: file_format \"" + ff + "\" is not implemented (openexr)");
+    (void) p.get_string("component_format", "float16");
+    (void) p.get_bool("banner", true);
+    (void) p.get_bool("compensate", false);
+    int n_filters = 0;
     for (auto &e : p.entries) {
         if (e.second.kind != Properties::Obj || e.second.o->tag != "rfilter") continue;
+        if (n_filters++) Throw("A film can only have one reconstruction filter.");
+        p.mark_queried(e.first);   /* film.cpp:34-42 */
         const Properties &rp = e.second.o->props;
         std::string t = lower(rp.plugin);
         if (t == "gaussian") { f.rfilter = AMVPT_RFILTER_GAUSSIAN; f.stddev = (float) rp.get_float("stddev", 0.5); }
@@ -151,9 +161,11 @@ static void sensor_parts(const Properties &p, FilmInfo &film, SamplerInfo &samp)
         if (o.tag == "film") {
             if (hf) Throw("Only one film can be specified per sensor.");
             film = make_film(o.props); hf = true;
+            p.mark_queried(e.first);   /* sensor.cpp:25-41 */
         } else if (o.tag == "sampler") {
             if (hs) Throw("Only one sampler can be specified per sensor.");
             samp = make_sampler(o.props); hs = true;
+            p.mark_queried(e.first);
         } else if (o.tag == "wrap") {
             std::string c = wrap_class(o);
             if (c == "film") { if (hf) Throw("Only one film can be specified per sensor."); film = make_film(unwrap(o)); hf = true; }
@@ -178,6 +190,12 @@ static amvpt_view_desc make_perspective_view(const Properties &p, const Transfor
     if (t == "thinlens") v.type = AMVPT_CAMERA_THINLENS;
     else if (t == "perspective") v.type = AMVPT_CAMERA_PERSPECTIVE;
     else Throw("Subsensor must be of type ThinLensCamera or PerspectiveCamera !");
+    /* Sensor base (sensor.cpp:14-22, 72-80): no time sample on the implemented path, no spectral response */
+    const float shutter_open = (float) p.get_float("shutter_open", 0.0);
+    const float shutter_time = (float) p.get_float("shutter_close", 0.0) - shutter_open;
+    if (shutter_time < 0.f) Throw("Shutter opening time must be less than or equal to the shutter closing time!");
+    if (shutter_time > 0.f) Throw("A shutter interval (time sample, motion blur) is not implemented");
+    if (p.has("srf")) Throw("A sensor response function ('srf') is not implemented (rgb variants)");
     float near_clip = (float) p.get_float("near_clip", 1e-2), far_clip = (float) p.get_float("far_clip", 1e4);
     if (near_clip <= 0.f) Throw("The 'near_clip' parameter must be greater than zero!");
     if (near_clip >= far_clip) Throw("The 'near_clip' parameter must be smaller than 'far_clip'.");
@@ -204,7 +222,7 @@ static amvpt_view_desc make_perspective_view(const Properties &p, const Transfor
     v.pp_offset[0] = (float) w * ppx / (float) cw;   /* film.size * principal_point_offset / crop_size */
     v.pp_offset[1] = (float) h * ppy / (float) ch;
     v.focus_distance = (float) p.get_float("focus_distance", far_clip);
-    v.aperture_radius = (float) p.get_float("aperture_radius", 0.0);
+    v.aperture_radius = v.type == AMVPT_CAMERA_THINLENS ? (float) p.get_float("aperture_radius", 0.0) : 0.f;
     if (v.type == AMVPT_CAMERA_THINLENS) {
         /* thinlens.cpp:156-162 */
         if (!p.has("aperture_radius")) Throw("Property \"aperture_radius\" has not been specified!");
@@ -242,9 +260,8 @@ static SensorInfo make_sensor(const Object &o) {
         s.rev_x = p.get_bool("reverse_x", false);
         s.rev_y = p.get_bool("reverse_y", false);
         std::vector<const Object *> kids;
-        for (auto &e : p.entries) {
-            if (e.second.kind != Properties::Obj) continue;
-            const Object &c = *e.second.o;
+        for (auto &e : p.objects()) {   /* batch.cpp:96: props.objects() */
+            const Object &c = *e.second;
             if (c.tag == "sensor") kids.push_back(&c);
             else if (c.tag == "shape")
                 Throw("BatchSensor: shapes can only be specified as children if a sensor is associated with them!");
@@ -353,7 +370,8 @@ static SensorInfo make_sensor(const Object &o) {
     }
     s.film.w = res_x;
     s.film.h = res_y;
-    s.film.reset_crop();   /* m_film->set_size(m_film_res) resets the crop window (grid.cpp:230, film.cpp:102-106) */
+    s.film.reset_crop();
+    p.mark_all_queried();   /* grid.cpp:231-232 */   /* m_film->set_size(m_film_res) resets the crop window (grid.cpp:230, film.cpp:102-106) */
     return s;
 }
 
@@ -365,6 +383,8 @@ struct IntegratorInfo {
     std::string type = "path";
     amvpt_params p{};
     std::string text;
+    float timeout = -1.f;                    /* accepted; unused by the JIT renders (see build) */
+    uint32_t samples_per_pass = 0xffffffffu; /* SamplingIntegrator::m_samples_per_pass */
 };
 
 struct MeshStore { std::vector<float> pos, nrm, uv; std::vector<uint32_t> faces; };
@@ -444,8 +464,9 @@ static int add_bsdf(amvpt_host_scene &S, std::map<const Object *, int> &seen, co
     } else if (t == "twosided") {
         d.type = AMVPT_BSDF_TWOSIDED;
         std::vector<const Object *> nested;
-        for (auto &e : p.entries)
-            if (e.second.kind == Properties::Obj && e.second.o->tag == "bsdf") nested.push_back(e.second.o.get());
+        for (auto &e : p.objects())   /* twosided.cpp:75: props.objects() */
+            if (e.second->tag == "bsdf") nested.push_back(e.second);
+            else Throw("twosided: nested object of type \"" + e.second->tag + "\" is not a BSDF");
         if (nested.empty()) Throw("A nested one-sided material is required!");
         if (nested.size() > 2) Throw("At most two nested BSDFs can be specified!");
         int a = add_bsdf(S, seen, *nested[0]);
@@ -490,9 +511,8 @@ static void build(amvpt_host_scene &S) {
     std::map<const Object *, int> seen;
     const Properties &rp = S.root->props;
     bool have_integrator = false;
-    for (auto &e : rp.entries) {
-        if (e.second.kind != Properties::Obj) continue;
-        const Object &o = *e.second.o;
+    for (auto &e : rp.objects()) {   /* scene.cpp:23: props.objects() */
+        const Object &o = *e.second;
         if (o.tag == "integrator") {
             if (have_integrator) Throw("Only one integrator can be specified per scene.");
             have_integrator = true;
@@ -507,6 +527,17 @@ static void build(amvpt_host_scene &S) {
             if (rr <= 0) Throw("\"rr_depth\" must be set to a value greater than zero!");
             I.p.rr_depth = (uint32_t) rr;
             I.p.hide_emitters = p.get_bool("hide_emitters", false);
+            /* Integrator / SamplingIntegrator keys (integrator.cpp:22-28, 96-116): the JIT render of both
+             * integrators never reads `timeout` or `block_size` (the scalar block renderer does);
+             * `samples_per_pass` splits the stock path integrator's frame into passes (integrator.cpp:137-146)
+             * and is ignored by mvpath, whose pass size is spp_pass_lim (mvpath.cpp:36) */
+            I.timeout = (float) p.get_float("timeout", -1.0);
+            long long bs = p.get_int("block_size", 0);
+            if (bs < 0) Throw("\"block_size\" must be a non-negative integer");
+            long long spp_pass = p.get_int("samples_per_pass", -1);
+            if (spp_pass < -1 || spp_pass == 0 || spp_pass > 0xffffffffll)
+                Throw("\"samples_per_pass\" must be a positive integer");
+            I.samples_per_pass = spp_pass == -1 ? 0xffffffffu : (uint32_t) spp_pass;
             if (I.type == "mvpath") {
                 I.p.integrator = AMVPT_INTEGRATOR_MVPATH;
                 I.p.sa_reuse = p.get_bool("sa_reuse", false);
@@ -525,6 +556,8 @@ static void build(amvpt_host_scene &S) {
                 I.text = os.str();
             } else if (I.type == "path") {
                 I.p.integrator = AMVPT_INTEGRATOR_PATH;
+                /* the path integrator's pass size travels in spp_pass_lim (amvpt.h) */
+                I.p.spp_pass_lim = I.samples_per_pass == 0xffffffffu ? 0u : I.samples_per_pass;
                 std::ostringstream os;
                 os << "PathIntegrator[\n  max_depth = " << (int) I.p.max_depth << ",\n  rr_depth = " << I.p.rr_depth << "\n]";
                 I.text = os.str();
@@ -535,6 +568,7 @@ static void build(amvpt_host_scene &S) {
             S.sensors.push_back(make_sensor(o));
         } else if (o.tag == "emitter") {
             std::string t = lower(o.props.plugin);
+            if (t == "area") Throw("Emitter \"area\" must be attached to a shape");
             if (t == "constant") {
                 /* ConstantBackgroundEmitter (constant.cpp:52-65): radiance (default 1), infinite */
                 if (S.has_env) Throw("Only one environment emitter can be specified per scene.");
@@ -563,10 +597,15 @@ static void build(amvpt_host_scene &S) {
             Transform4f T = p.get_transform("to_world");
             bool flip = p.get_bool("flip_normals", false);
             const Object *bsdf = nullptr, *emit = nullptr;
-            for (auto &c : p.entries) {
-                if (c.second.kind != Properties::Obj) continue;
-                if (c.second.o->tag == "bsdf") { if (bsdf) Throw("Only a single BSDF child object can be specified per shape."); bsdf = c.second.o.get(); }
-                else if (c.second.o->tag == "emitter") { if (emit) Throw("Only a single Emitter child object can be specified per shape."); emit = c.second.o.get(); }
+            (void) p.get_float("silhouette_sampling_weight", 1.0);   /* shape.cpp: only used by differentiable rendering */
+            for (auto &c : p.objects(false)) {   /* shape.cpp:26-64 */
+                const std::string &ct = c.second->tag;
+                if (ct == "bsdf") { if (bsdf) Throw("Only a single BSDF child object can be specified per shape."); bsdf = c.second; }
+                else if (ct == "emitter") { if (emit) Throw("Only a single Emitter child object can be specified per shape."); emit = c.second; }
+                else if (ct == "sensor" || ct == "medium" || ct == "texture")
+                    Throw("Shape: a child " + ct + " is outside the implemented path");
+                else continue;
+                p.mark_queried(c.first);
             }
             if (t == "rectangle") {
                 d.type = AMVPT_SHAPE_RECTANGLE;
@@ -580,7 +619,8 @@ static void build(amvpt_host_scene &S) {
                 d.vertex_count = 24;
                 d.face_count = 12;
                 d.positions = m->pos.data();
-                d.normals = m->nrm.data();
+                /* Mesh::m_face_normals (mesh.cpp): shading with the face normals, vertex normals dropped */
+                d.normals = p.get_bool("face_normals", false) ? nullptr : m->nrm.data();
                 d.texcoords = m->uv.data();
                 d.faces = m->faces.data();
                 fill_xform(T, d.to_world, d.to_object);
@@ -626,6 +666,9 @@ static void build(amvpt_host_scene &S) {
             if (emit) {
                 std::string et = lower(emit->props.plugin);
                 if (et != "area") Throw("Emitter \"" + emit->props.plugin + "\" cannot be attached to a shape (area only)");
+                if (emit->props.has("to_world"))
+                    Throw("Found a 'to_world' transformation -- this is not allowed. The area light inherits this "
+                          "transformation from its parent shape.");
                 amvpt_emitter_desc ed;
                 std::memset(&ed, 0, sizeof(ed));
                 ed.type = AMVPT_EMITTER_AREA;
@@ -678,6 +721,13 @@ static amvpt_params params_for(const amvpt_host_scene &S, const SensorInfo &sn, 
     if (p.integrator == AMVPT_INTEGRATOR_PATH && sn.multisensor)
         Throw("The stock `path` integrator on a grid sensor is outside the implemented path");
     p.spp = spp ? spp : sn.sampler.sample_count;
+    if (p.integrator == AMVPT_INTEGRATOR_PATH && p.spp_pass_lim) {
+        /* SamplingIntegrator::render (integrator.cpp:137-143) */
+        const uint32_t spp_per_pass = std::min(p.spp_pass_lim, p.spp);
+        if (p.spp % spp_per_pass)
+            Throw("sample_count (" + std::to_string(p.spp) + ") must be a multiple of spp_per_pass (" +
+                  std::to_string(spp_per_pass) + ").");
+    }
     p.seed = seed;
     p.base_seed = sn.sampler.seed;
     p.n_views = (uint32_t) sn.views.size();
@@ -738,6 +788,7 @@ static amvpt_host_scene *load_common(std::shared_ptr<mi::Object> root) {
     S->root = root;
     try {
         mi::build(*S);
+        mi::check_unqueried(*root);   /* xml.cpp:1089-1107 */
     } catch (...) {
         delete S;
         throw;

@@ -214,6 +214,7 @@ bool is_object_tag(const std::string &t) {
 }
 
 struct Loader {
+    std::string src = "<string>";   /* the scene file, for error messages */
     std::map<std::string, std::string> params;
     std::map<std::string, std::shared_ptr<Object>> ids;
     int unnamed = 0;
@@ -302,6 +303,8 @@ struct Loader {
     std::shared_ptr<Object> object(const XmlNode &n) {
         auto obj = std::make_shared<Object>();
         obj->tag = n.tag;
+        obj->src = src;
+        obj->line = n.line;
         if (n.tag != "scene") obj->props.plugin = attr(n, "type", n.tag != "wrap" || true);
         obj->props.id = n.attr("id") ? attr(n, "id") : "_unnamed_" + std::to_string(unnamed++);
         for (auto &cp : n.children) {
@@ -370,10 +373,12 @@ struct Loader {
 
 } // namespace
 
-std::shared_ptr<Object> load_scene_string(const std::string &xml, const std::map<std::string, std::string> &defines) {
+static std::shared_ptr<Object> load_scene(const std::string &xml, const std::map<std::string, std::string> &defines,
+                                          const std::string &src) {
     auto root = parse_xml(xml);
     if (root->tag != "scene") throw std::runtime_error("XML root must be <scene>");
     Loader L;
+    L.src = src;
     L.params = defines;
     /* <default> must be visible before use: pre-scan the root's <default> tags */
     for (auto &c : root->children)
@@ -385,15 +390,63 @@ std::shared_ptr<Object> load_scene_string(const std::string &xml, const std::map
     return L.object(*root);
 }
 
+std::shared_ptr<Object> load_scene_string(const std::string &xml, const std::map<std::string, std::string> &defines) {
+    return load_scene(xml, defines, "<string>");
+}
+
 std::shared_ptr<Object> load_scene_file(const std::string &path, const std::map<std::string, std::string> &defines) {
     std::ifstream f(path);
     if (!f) throw std::runtime_error("Unable to open scene file \"" + path + "\"");
     std::stringstream ss;
     ss << f.rdbuf();
-    auto root = load_scene_string(ss.str(), defines);
+    auto root = load_scene(ss.str(), defines, path);
     const size_t slash = path.find_last_of('/');
     root->base_dir = slash == std::string::npos ? std::string(".") : path.substr(0, slash);
     return root;
+}
+
+/* ------------------------------------------------------------------ */
+/* Unreferenced properties (xml.cpp:1089-1107)                         */
+/* ------------------------------------------------------------------ */
+
+/* the plugin class as the reference names it: string::to_lower(Class::name()) */
+static std::string class_name(const std::string &tag) {
+    if (tag == "rfilter") return "reconstructionfilter";
+    return tag;
+}
+
+static void check_object(const Object &o, std::vector<const Object *> &seen) {
+    for (const Object *s : seen)
+        if (s == &o) return;
+    seen.push_back(&o);
+    /* children first: the loader instantiates (and checks) them before their parent */
+    for (auto &e : o.props.entries)
+        if (e.second.kind == Properties::Obj) check_object(*e.second.o, seen);
+    if (o.wrapped || o.tag == "wrap") return;   /* Wrap marks its properties queried (wrap.cpp:12-14) */
+    const std::string near = "\"" + o.src + "\" (near line " + std::to_string(o.line) + ")";
+    const std::string type = o.tag == "scene" ? "scene" : o.props.plugin;
+    std::vector<std::string> names;
+    for (auto &e : o.props.entries) {
+        if (e.second.queried) continue;
+        if (e.second.kind == Properties::Obj) {
+            const Object &c = *e.second.o;
+            throw std::runtime_error("Error while loading " + near + ": unreferenced object " + c.tag + " of type \"" +
+                                     c.props.plugin + "\" (within " + class_name(o.tag) + " of type \"" + type + "\")");
+        }
+        names.push_back("\"" + e.first + "\"");
+    }
+    if (names.empty()) return;
+    std::string list = "[";
+    for (size_t i = 0; i < names.size(); ++i) list += (i ? ", " : "") + names[i];
+    list += "]";
+    throw std::runtime_error("Error while loading " + near + ": unreferenced " +
+                             (names.size() > 1 ? "properties" : "property") + " \"" + list + "\" in " +
+                             class_name(o.tag) + " plugin of type \"" + type + "\"");
+}
+
+void check_unqueried(const Object &root) {
+    std::vector<const Object *> seen;
+    check_object(root, seen);
 }
 
 } // namespace mi

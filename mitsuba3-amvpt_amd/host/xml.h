@@ -47,17 +47,44 @@ struct Properties {
         float v[3] = {0, 0, 0};
         Transform4f t;
         std::shared_ptr<Object> o;
+        /* read by the plugin that consumed these Properties (Properties::Entry::queried); the XML
+         * loader's check refuses unread ones (xml.cpp:1089-1107) */
+        mutable bool queried = false;
     };
     std::string plugin;   /* type="..." */
     std::string id;
     std::vector<std::pair<std::string, Value>> entries;  /* insertion order */
 
+    /* lookup that counts as a query (the typed getters), and one that does not (has_property) */
     const Value *find(const std::string &k) const {
+        const Value *v = peek(k);
+        if (v) v->queried = true;
+        return v;
+    }
+    const Value *peek(const std::string &k) const {
         for (auto &e : entries)
             if (e.first == k) return &e.second;
         return nullptr;
     }
-    bool has(const std::string &k) const { return find(k) != nullptr; }
+    bool has(const std::string &k) const { return peek(k) != nullptr; }
+    void mark_queried(const std::string &k) const { (void) find(k); }
+    void mark_all_queried() const { for (auto &e : entries) e.second.queried = true; }
+    /* Properties::objects(mark_queried): the object-valued entries in insertion order */
+    std::vector<std::pair<std::string, const Object *>> objects(bool mark = true) const {
+        std::vector<std::pair<std::string, const Object *>> r;
+        for (auto &e : entries)
+            if (e.second.kind == Obj) {
+                r.push_back({e.first, e.second.o.get()});
+                if (mark) e.second.queried = true;
+            }
+        return r;
+    }
+    std::vector<std::string> unqueried() const {
+        std::vector<std::string> r;
+        for (auto &e : entries)
+            if (!e.second.queried) r.push_back(e.first);
+        return r;
+    }
     void set(const std::string &k, const Value &v) {
         for (auto &e : entries)
             if (e.first == k) { e.second = v; return; }
@@ -87,8 +114,18 @@ struct Object {
     std::string tag;       /* object class: integrator, sensor, film, rfilter, sampler, bsdf, emitter, shape, wrap, scene */
     Properties props;
     std::string base_dir;  /* root only: directory of the scene file (FileResolver for `filename`) */
+    std::string src;       /* the scene file (or "<string>") and the line of the object's tag, for error messages */
+    int line = 0;
+    /* instantiated through a Wrap (Wrap::create_instance -> PluginManager, not the XML loader): no
+     * unreferenced-property check, as in the reference */
+    mutable bool wrapped = false;
     virtual ~Object() = default;
 };
+
+/* The XML loader's check after instantiating the scene (xml.cpp:1089-1107): every property and child
+ * object of every object the loader instantiated must have been read by its plugin, else the
+ * reference's "unreferenced property" / "unreferenced object" error. */
+void check_unqueried(const Object &root);
 
 std::shared_ptr<Object> load_scene_file(const std::string &path, const std::map<std::string, std::string> &defines);
 std::shared_ptr<Object> load_scene_string(const std::string &xml, const std::map<std::string, std::string> &defines);

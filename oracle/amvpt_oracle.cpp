@@ -1614,8 +1614,10 @@ static void plan(const amvpt_params &P, uint32_t &spp, uint32_t &spp_pp, uint32_
         n_passes = s / spp_pp;
         s = n_passes * spp_pp;
     } else {
-        spp_pp = s;
-        n_passes = 1;
+        /* SamplingIntegrator::render (integrator.cpp:137-146): samples_per_pass (spp_pass_lim here,
+         * 0 = unset); the host refuses an spp it does not divide */
+        spp_pp = P.spp_pass_lim ? std::min(P.spp_pass_lim, s) : s;
+        n_passes = s / spp_pp;
     }
     uint64_t wf = px * spp_pp;
     if (wf > 0xffffffffull) {
@@ -1739,7 +1741,12 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
     const float scale_x = 1.f / (float) W, scale_y = 1.f / (float) H;
     const float off_x = -(float) ox * scale_x, off_y = -(float) oy * scale_y;
     uint32_t n_adapt = std::min(P.adaptive, G - 1);
-    if (!is_mv && n_passes > 1) return 4; /* stock path: RNG state carried across passes (unsupported) */
+    /* stock path over several passes (integrator.cpp:279-330): the sampler is seeded once, every pass
+     * continues each lane's PCG32 stream where the previous pass left it (advance() only moves the
+     * sample index, which the independent sampler does not read) */
+    const bool carry = !is_mv && n_passes > 1;
+    if (carry && (lm.rect || spp % spp_pp)) return 4;
+    std::vector<uint64_t> carried(carry ? lane_end - lane_begin : 0);
     const bool partial = lm.rect || lane_begin != 0 || lane_end != L;
     if (n_adapt && partial && !(lm.rect ? (bool) g_run_exchange : (bool) g_exchange))
         return 4; /* adaptive needs the full frame or a count exchange */
@@ -1775,6 +1782,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                 tea(seed_value, idx32, 4, v0, v1);
                 PCG32 rng;
                 rng.seed(v0, v1);
+                if (carry && pass > 0) rng.state = carried[vi - lane_begin];
                 V2 jit{rng.next_1d(), 0.f};
                 jit.y = rng.next_1d();
                 V2 sample_pos{(float) px + jit.x, (float) py + jit.y};
@@ -1787,6 +1795,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                     uint32_t index;
                     Ray ray = R.sample_ray_idx(adj, index);
                     auto [spec, valid] = R.sample_single(rng, ray, verts);
+                    if (carry) carried[vi - lane_begin] = rng.state;
                     float alpha = valid ? 1.f : 0.f;
                     /* SamplingIntegrator::render_sample puts at the integer pixel under a box filter */
                     V2 put_pos = (!is_mv && film.box) ? V2{(float) px, (float) py} : sample_pos;

@@ -25,7 +25,7 @@ def _torch():
     return torch
 
 
-def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records=True, flags=0):
+def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records=True, flags=0, record_pass=0):
     """One frame through amvpt_render_ex (per-call options; records of pass 0 through the opts hook)."""
     torch = _torch()
     dev = amvpt_mod.DeviceScene(sd)
@@ -36,7 +36,7 @@ def _gpu_render(amvpt_mod, sd, vd, p, plan, lane_begin=0, lane_end=None, records
     if records:
         rec = torch.zeros((lane_end - lane_begin, plan["group"], 8), dtype=torch.float32, device="cuda")
     dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt_mod.LaneSet(lane_begin, lane_end, 0, 0, 0, 0), flags=flags,
-                  records_ptr=rec.data_ptr() if rec is not None else None)
+                  records_ptr=rec.data_ptr() if rec is not None else None, record_pass=record_pass)
     torch.cuda.synchronize()
     return film.cpu().numpy(), (rec.cpu().numpy() if rec is not None else None)
 
@@ -45,11 +45,11 @@ def _bit_equal(a, b):
     return (a == b) | (np.isnan(a) & np.isnan(b))
 
 
-def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0, flags=0):
+def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0, flags=0, record_pass=0):
     sd, vd, p = scene.describe(0, seed, spp)
     plan = oracle.plan(p)
-    gfilm, grec = _gpu_render(amvpt_mod, sd, vd, p, plan, flags=flags)
-    ofilm, orec, _ = oracle.render(sd, vd, p, threads=16, record_pass=0)
+    gfilm, grec = _gpu_render(amvpt_mod, sd, vd, p, plan, flags=flags, record_pass=record_pass)
+    ofilm, orec, _ = oracle.render(sd, vd, p, threads=16, record_pass=record_pass)
     eq = _bit_equal(grec, orec)
     match = eq.all(axis=(1, 2)).mean()
     if match < min_match:
@@ -123,6 +123,31 @@ def test_path_integrator_c1(gpu_ready, amvpt_mod, oracle, res):
     sd, vd, p = s.describe(0, 0, 0)
     assert (p.film_width, p.film_height, amvpt_mod.plan(p)[0]) == (res, res, 16)
     _check(amvpt_mod, oracle, s)
+
+
+def _path_with_samples_per_pass(amvpt_mod, n, **defines):
+    xml = open(CBOX_PATH).read().replace('<integrator type="path">',
+                                         '<integrator type="path"><integer name="samples_per_pass" value="%d"/>' % n)
+    return amvpt_mod.load_string(xml, **defines)
+
+
+@pytest.mark.parametrize("spp,per_pass,record_pass", [(16, 4, 3), (12, 6, 1), (8, 1, 5)])
+def test_path_passes_continue_the_sampler(gpu_ready, amvpt_mod, oracle, spp, per_pass, record_pass):
+    """The stock path integrator split into passes (samples_per_pass, the same mechanism as its split of a
+    frame above 2^32 - 1 samples, integrator.cpp:137-146,249-330): the sampler is seeded once and every pass
+    continues each lane's PCG32 stream, so the records of a later pass are bit-identical to the oracle's
+    only if the states are carried (rng_in / rng_out)."""
+    s = _path_with_samples_per_pass(amvpt_mod, per_pass, res=32, spp=spp)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert p.spp_pass_lim == per_pass and oracle.plan(p)["passes"] == spp // per_pass
+    gfilm, ofilm = _check(amvpt_mod, oracle, s, record_pass=record_pass)
+    # the whole frame: the same estimator as one pass of spp samples would be, different samples
+    one = amvpt_mod.load_file(CBOX_PATH, res=32, spp=spp)
+    sd1, vd1, p1 = one.describe(0, 0, 0)
+    f1, _ = _gpu_render(amvpt_mod, sd1, vd1, p1, oracle.plan(p1), records=False)
+    assert not np.array_equal(f1, gfilm)
+    w, w1 = gfilm[..., -1].sum(), f1[..., -1].sum()
+    assert abs(w / w1 - 1) < 2e-2   # splat weights: spp samples per pixel either way
 
 
 @pytest.mark.parametrize("scene,defines", [

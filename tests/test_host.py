@@ -209,7 +209,7 @@ def test_obj_transform_and_normals(amvpt_mod):
     ref = p0 / [2, 1, 1]
     ref /= np.linalg.norm(ref, axis=1, keepdims=True)
     assert np.abs(nrm - ref).max() < 1e-4
-    _, d2, _, _, nrm2 = _mesh(amvpt_mod, xml.replace('<transform', '<boolean name="face_normals" value="true"/><transform'))
+    _, d2, _, _, nrm2 = _mesh(amvpt_mod, xml.replace('<string name="filename"', '<boolean name="face_normals" value="true"/><string name="filename"'))
     assert not d2.normals and nrm2 is None
 
 
@@ -255,3 +255,90 @@ def test_crop_window_descriptors_and_projection(amvpt_mod, oracle):
     g = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=16)
     gp = g.describe()[2]
     assert (gp.crop_offset_x, gp.full_width) == (0, gp.film_width)
+
+
+_STRICT_BASE = """<scene version="3.0.0">
+  <integrator type="{itype}">{iprops}</integrator>
+  <sensor type="perspective">{sprops}
+    <float name="fov" value="45"/>
+    <transform name="to_world"><lookat origin="0, 0, 4" target="0, 0, 0" up="0, 1, 0"/></transform>
+    <sampler type="independent"><integer name="sample_count" value="16"/></sampler>
+    <film type="hdrfilm"><integer name="width" value="8"/><integer name="height" value="8"/>{fprops}</film>
+  </sensor>
+  <shape type="sphere"><float name="radius" value="1"/>{shprops}<bsdf type="diffuse">{bprops}</bsdf></shape>
+  <shape type="rectangle">
+    <transform name="to_world"><translate value="0, 3, 0"/></transform>
+    <emitter type="area"><rgb name="radiance" value="4, 4, 4"/>{eprops}</emitter>
+  </shape>{extra}
+</scene>"""
+
+
+def _strict(amvpt_mod, itype="path", iprops="", sprops="", fprops="", shprops="", bprops="", eprops="", extra=""):
+    return amvpt_mod.load_string(_STRICT_BASE.format(itype=itype, iprops=iprops, sprops=sprops, fprops=fprops,
+                                                     shprops=shprops, bprops=bprops, eprops=eprops, extra=extra))
+
+
+def test_xml_unreferenced_properties_are_errors(amvpt_mod):
+    """The XML loader refuses properties and child objects that no plugin read (xml.cpp:1089-1107), with the
+    reference's message; a typo'd key no longer renders silently with defaults."""
+    _strict(amvpt_mod)   # the base scene itself is clean
+    cases = [
+        (dict(iprops='<integer name="max_detph" value="3"/>'), r'unreferenced property "\["max_detph"\]" in '
+                                                               r'integrator plugin of type "path"'),
+        (dict(itype="mvpath", iprops='<boolean name="sa_resue" value="true"/>'), r'"\["sa_resue"\]" in integrator'),
+        (dict(sprops='<float name="fov_x" value="3"/>'), r'"\["fov_x"\]" in sensor plugin of type "perspective"'),
+        (dict(fprops='<integer name="widht" value="8"/>'), r'"\["widht"\]" in film plugin of type "hdrfilm"'),
+        (dict(shprops='<float name="raduis" value="2"/>'), r'"\["raduis"\]" in shape plugin of type "sphere"'),
+        (dict(bprops='<rgb name="reflectence" value="0.5"/>'), r'in bsdf plugin of type "diffuse"'),
+        (dict(eprops='<float name="sampling_wieght" value="2"/>'), r'in emitter plugin of type "area"'),
+        (dict(iprops='<integer name="a" value="1"/><integer name="b" value="1"/>'),
+         r'unreferenced properties "\["a", "b"\]"'),
+        (dict(extra='<integer name="stray" value="1"/>'), r'"\["stray"\]" in scene plugin'),
+        (dict(fprops='<rfilter type="gaussian"><float name="stdev" value="1"/></rfilter>'),
+         r'in reconstructionfilter plugin of type "gaussian"'),
+        # a perspective camera has no aperture (thinlens.cpp reads it, perspective.cpp does not)
+        (dict(sprops='<float name="aperture_radius" value="0.1"/>'), r'"\["aperture_radius"\]" in sensor'),
+        (dict(bprops='<rfilter type="box"/>'), r'unreferenced object rfilter of type "box" \(within bsdf'),
+    ]
+    for kw, msg in cases:
+        with pytest.raises(RuntimeError, match=msg):
+            _strict(amvpt_mod, **kw)
+
+
+def test_xml_accepts_every_key_the_reference_plugins_read(amvpt_mod):
+    """Keys the reference's plugins query (so its loader accepts them) load here too, with the reference's
+    meaning or its documented no-op on the JIT render path."""
+    s = _strict(amvpt_mod,
+                iprops='<float name="timeout" value="10"/><integer name="block_size" value="16"/>'
+                       '<integer name="samples_per_pass" value="4"/><boolean name="hide_emitters" value="false"/>',
+                sprops='<float name="near_clip" value="0.01"/><float name="far_clip" value="100"/>'
+                       '<float name="focus_distance" value="4"/><float name="shutter_open" value="0"/>'
+                       '<float name="shutter_close" value="0"/><float name="principal_point_offset_x" value="0"/>',
+                fprops='<string name="component_format" value="float32"/><string name="file_format" value="openexr"/>'
+                       '<boolean name="banner" value="false"/><string name="pixel_format" value="rgb"/>'
+                       '<boolean name="sample_border" value="false"/>',
+                shprops='<boolean name="flip_normals" value="false"/><point name="center" value="0, 0, 0"/>'
+                        '<float name="silhouette_sampling_weight" value="1"/>',
+                eprops='<float name="sampling_weight" value="1"/>')
+    sd, vd, p = s.describe(0, 0, 0)
+    assert p.spp_pass_lim == 4   # the path integrator's samples_per_pass (amvpt.h)
+    for kw, msg in [
+        (dict(sprops='<float name="shutter_open" value="1"/><float name="shutter_close" value="0.5"/>'),
+         "Shutter opening time must be less than or equal to the shutter closing time"),
+        (dict(sprops='<float name="shutter_close" value="0.5"/>'), "shutter interval"),
+        (dict(fprops='<string name="file_format" value="pfm"/>'), "file_format"),
+        (dict(eprops='<transform name="to_world"><translate value="0, 1, 0"/></transform>'),
+         "Found a 'to_world' transformation -- this is not allowed"),
+        (dict(iprops='<integer name="samples_per_pass" value="0"/>'), "samples_per_pass"),
+    ]:
+        with pytest.raises(RuntimeError, match=msg):
+            _strict(amvpt_mod, **kw)
+
+
+def test_path_samples_per_pass_must_divide_spp(amvpt_mod):
+    """SamplingIntegrator::render: 'sample_count (%d) must be a multiple of spp_per_pass (%d).'"""
+    s = _strict(amvpt_mod, iprops='<integer name="samples_per_pass" value="4"/>')
+    assert s.describe(0, 0, 16)[2].spp_pass_lim == 4
+    with pytest.raises(RuntimeError, match=r"sample_count \(10\) must be a multiple of spp_per_pass \(4\)\."):
+        s.describe(0, 0, 10)
+    s.describe(0, 0, 3)   # spp_per_pass = min(4, 3) = 3

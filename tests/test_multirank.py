@@ -73,7 +73,9 @@ def _group_worker(rank, world, port, out_dir, kw):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        s = amvpt.load_file(CBOX, **kw)
+        kw = dict(kw)
+        xml = kw.pop("xml", None)
+        s = amvpt.load_string(xml, **kw) if xml else amvpt.load_file(CBOX, **kw)
         sd, vd, p = s.describe(0, 0, 0)
         G = O.plan(p)["group"]
         part = adist.view_group_partition(p, G, world)
@@ -123,6 +125,27 @@ def test_view_group_partition_equals_single_process(oracle, amvpt_mod, world):
     sd, vd, p = s.describe(0, 0, 0)
     ref, _, st = oracle.render(sd, vd, p, threads=4)
     assert st["adaptive_lanes"] > 0
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def _wide_filter_xml(stddev):
+    return open(CBOX).read().replace('<rfilter type="$rfilter"/>',
+                                     '<rfilter type="gaussian"><float name="stddev" value="%g"/></rfilter>' % stddev)
+
+
+def test_view_group_partition_with_a_wide_filter(oracle, amvpt_mod):
+    """A Gaussian of stddev 1.5 (radius 6) splats up to 7 cells past a rank's tiles: the window border
+    follows the filter (a fixed 4-px border sent those cells to the overflow list, past its cap
+    at C5 sizes), and the gathered frame still equals the single-process one."""
+    from amvpt import dist as adist
+    kw = dict(C5_SMALL, adaptive=0, xml=_wide_filter_xml(1.5))
+    s = amvpt_mod.load_string(kw["xml"], **{k: v for k, v in kw.items() if k != "xml"})
+    sd, vd, p = s.describe(0, 0, 0)
+    assert abs(p.rfilter_stddev - 1.5) < 1e-7 and adist.filter_border(p) == 7
+    (x0, y0, w, h), (wx, wy, ww, wh) = adist.view_group_partition(p, 4, 2)[1]
+    assert x0 - wx in (0, 7) and wy == max(0, y0 - 7)
+    got = _run_groups(2, kw)
+    ref, _, _ = oracle.render(sd, vd, p, threads=4)
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
@@ -250,9 +273,12 @@ def test_host_view_group_partition_matches_dist(amvpt_mod):
     amvpt.dist.view_group_partition (the bench's), including the configurations where neither applies."""
     from amvpt import dist as adist
     cases = [dict(C5_SMALL), dict(res=16, spp=16, gx=4, gy=2, reuse=4), dict(res=16, spp=16, gx=4, gy=2, reuse=2),
-             dict(res=16, spp=16, gx=4, gy=2, reuse=8), dict(res=16, spp=16, gx=3, gy=2, reuse=2)]
+             dict(res=16, spp=16, gx=4, gy=2, reuse=8), dict(res=16, spp=16, gx=3, gy=2, reuse=2),
+             dict(C5_SMALL, xml=_wide_filter_xml(1.5)), dict(C5_SMALL, xml=_wide_filter_xml(2.2)),
+             dict(C5_SMALL, rfilter="box")]
     for kw in cases:
-        _, _, p = amvpt_mod.load_file(CBOX, **kw).describe(0, 0, 0)
+        xml = kw.pop("xml", None)
+        _, _, p = (amvpt_mod.load_string(xml, **kw) if xml else amvpt_mod.load_file(CBOX, **kw)).describe(0, 0, 0)
         from oracle import oracle as O
         G = O.plan(p)["group"]
         for world in (1, 2, 3, 4, 8):
