@@ -50,6 +50,19 @@ int amvpt_host_render(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t s
                       int raw, float *out_host, amvpt_counters *counters);
 
 /*
+ * amvpt_host_render on a caller stream (hipStream_t; NULL: the default stream).  Both run through
+ * amvpt_render_ex with explicit default options (no process-global knob), keep the device scene
+ * (BVH build + upload) and the film / image buffers on the host scene per device for the next frame,
+ * and serialise renders of one host scene (its cached buffers); renders of different host scenes from
+ * different threads are independent.  Returns once the image is in out_host.
+ */
+int amvpt_host_render_stream(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t seed, uint32_t spp,
+                             int raw, float *out_host, void *stream, amvpt_counters *counters);
+/* amvpt_host_render's cache counters: device-scene creations, buffer allocations, renders */
+int amvpt_host_render_stats(amvpt_host_scene *scene, uint64_t *scene_creates, uint64_t *buffer_allocs,
+                            uint64_t *renders);
+
+/*
  * Integrator::render over n_devices GPUs of one node, one host thread per device.
  * View groups, when they divide among the devices (C5): devices[r] renders the lanes of its groups'
  * quilt tiles into a film window (tiles + filter border), the windows and overflow cells go to

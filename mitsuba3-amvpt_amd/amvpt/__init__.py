@@ -202,6 +202,9 @@ def host_lib():
         L.amvpt_host_film_info.argtypes = [ctypes.c_void_p, u32] + [ctypes.POINTER(u32)] * 4
         L.amvpt_host_render.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.POINTER(Counters)]
+        L.amvpt_host_render_stream.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.POINTER(Counters)]
+        L.amvpt_host_render_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(u64)] * 3
         L.amvpt_host_render_multi.argtypes = [ctypes.c_void_p, u32, u32, u32, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_void_p,
                                               ctypes.POINTER(Counters)]
@@ -288,16 +291,26 @@ def load_string(xml, **defines):
     return Scene(h)
 
 
-def render(scene, sensor=0, seed=0, spp=0, raw=False, counters=None):
-    """Integrator::render(scene, sensor, seed, spp, develop=not raw) -> numpy (H, W, C)."""
+def render(scene, sensor=0, seed=0, spp=0, raw=False, counters=None, stream=None):
+    """Integrator::render(scene, sensor, seed, spp, develop=not raw) -> numpy (H, W, C), on the current
+    device and `stream` (a hipStream_t handle; None: the default stream).  The device scene and the film
+    are cached on the scene (render_stats)."""
     w, h, c, _ = scene.film_info(sensor)
     _, _, p = scene.describe(sensor, seed, spp)
     ch = (5 if p.film_alpha else 4) if raw else c
     out = np.zeros((h, w, ch), dtype=np.float32)
     cnt = counters if counters is not None else Counters()
-    _check(scene._lib.amvpt_host_render(scene._h, sensor, seed, spp, 1 if raw else 0,
-                                        out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cnt)), scene._lib)
+    _check(scene._lib.amvpt_host_render_stream(scene._h, sensor, seed, spp, 1 if raw else 0,
+                                               out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream or 0),
+                                               ctypes.byref(cnt)), scene._lib)
     return out
+
+
+def render_stats(scene):
+    """render's cache counters on this scene: device-scene creations, film buffer allocations, renders."""
+    a, b, c = u64(), u64(), u64()
+    _check(scene._lib.amvpt_host_render_stats(scene._h, a, b, c), scene._lib)
+    return {"scene_creates": a.value, "buffer_allocs": b.value, "renders": c.value}
 
 
 def render_multi(scene, devices, sensor=0, seed=0, spp=0, raw=False, counters=None):

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <sstream>
 #include <stdexcept>
@@ -402,11 +403,31 @@ struct amvpt_host_scene {
     std::vector<std::unique_ptr<mi::MeshStore>> meshes;
     amvpt_scene_desc desc{};
     bool has_env = false;
-    amvpt_scene *dev = nullptr;
-    int dev_id = -1;
+    /* amvpt_host_render's per-device state, kept for the next frame: the device scene (BVH build +
+     * upload happen once per device, not per frame) and the ImageBlock / developed-image buffers */
+    struct DeviceCache {
+        int device = -1;
+        amvpt_scene *scene = nullptr;
+        float *film = nullptr, *image = nullptr;
+        size_t film_bytes = 0, image_bytes = 0;
+    };
+    std::mutex render_mu;                 /* one render of this scene at a time (its cached buffers) */
+    std::vector<DeviceCache> devices;
+    uint64_t scene_creates = 0, buffer_allocs = 0, renders = 0;
     std::vector<amvpt_view_desc> last_views;
     std::shared_ptr<amvpt_multi_cache> multi;
-    ~amvpt_host_scene() { multi.reset(); if (dev) amvpt_scene_destroy(dev); }
+    ~amvpt_host_scene() {
+        multi.reset();
+        for (auto &d : devices) {
+            int cur = 0;
+            const bool have = hipGetDevice(&cur) == hipSuccess;
+            if (have) (void) hipSetDevice(d.device);
+            if (d.scene) amvpt_scene_destroy(d.scene);
+            if (d.film) (void) hipFree(d.film);
+            if (d.image) (void) hipFree(d.image);
+            if (have) (void) hipSetDevice(cur);
+        }
+    }
 };
 
 /* multi.cpp's cache slot on the host scene */
@@ -845,40 +866,85 @@ int amvpt_host_describe(amvpt_host_scene *s, uint32_t si, uint32_t seed, uint32_
 
 const char *amvpt_host_integrator_string(amvpt_host_scene *s) { return s ? s->integrator.text.c_str() : ""; }
 
-int amvpt_host_render(amvpt_host_scene *s, uint32_t si, uint32_t seed, uint32_t spp, int raw, float *out,
-                      amvpt_counters *counters) {
+/* a device buffer of at least `bytes`, grown (never shrunk) across frames */
+static void ensure_buffer(float *&buf, size_t &have, size_t bytes, uint64_t &allocs) {
+    if (have >= bytes) return;
+    if (buf) (void) hipFree(buf);
+    buf = nullptr;
+    have = 0;
+    if (hipMalloc(&buf, bytes) != hipSuccess) throw std::runtime_error("hipMalloc of the film failed");
+    have = bytes;
+    ++allocs;
+}
+
+int amvpt_host_render_stream(amvpt_host_scene *s, uint32_t si, uint32_t seed, uint32_t spp, int raw, float *out,
+                             void *stream, amvpt_counters *counters) {
     return guarded([&] {
         if (!s || si >= s->sensors.size()) throw std::runtime_error("Scene::render(): sensor index out of bounds!");
         const mi::SensorInfo &sn = s->sensors[si];
         amvpt_params p = mi::params_for(*s, sn, seed, spp);
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-        if (!s->dev || s->dev_id != dev) {
-            if (s->dev) amvpt_scene_destroy(s->dev);
-            s->dev = nullptr;
-            if (amvpt_scene_create(&s->desc, &s->dev) != AMVPT_OK) throw std::runtime_error(amvpt_last_error());
-            s->dev_id = dev;
+        std::lock_guard<std::mutex> lock(s->render_mu);
+        amvpt_host_scene::DeviceCache *dc = nullptr;
+        for (auto &d : s->devices)
+            if (d.device == dev) dc = &d;
+        if (!dc) {
+            s->devices.emplace_back();
+            dc = &s->devices.back();
+            dc->device = dev;
         }
+        if (!dc->scene) {
+            if (amvpt_scene_create(&s->desc, &dc->scene) != AMVPT_OK) throw std::runtime_error(amvpt_last_error());
+            ++s->scene_creates;
+        }
+        const hipStream_t st = (hipStream_t) stream;
         const uint32_t C = amvpt_film_channels(&p);
         const size_t npx = (size_t) p.film_width * p.film_height;
-        float *film = nullptr, *dev_out = nullptr;
-        if (hipMalloc(&film, npx * C * sizeof(float)) != hipSuccess) throw std::runtime_error("hipMalloc(film) failed");
-        struct Free { float *a; float *b; ~Free() { if (a) (void) hipFree(a); if (b) (void) hipFree(b); } } fr{film, nullptr};
-        if (hipMemset(film, 0, npx * C * sizeof(float)) != hipSuccess) throw std::runtime_error("hipMemset(film) failed");
-        if (amvpt_render(s->dev, sn.views.data(), &p, 0, UINT64_MAX, film, nullptr, counters) != AMVPT_OK)
+        ensure_buffer(dc->film, dc->film_bytes, npx * C * sizeof(float), s->buffer_allocs);
+        if (hipMemsetAsync(dc->film, 0, npx * C * sizeof(float), st) != hipSuccess)
+            throw std::runtime_error("hipMemsetAsync(film) failed");
+        /* the whole frame with explicit per-call options: no process-global knob takes part */
+        amvpt_lane_set lanes{};
+        lanes.lane_begin = 0;
+        lanes.lane_end = UINT64_MAX;
+        amvpt_film_window win{};
+        win.film = dc->film;
+        win.width = p.film_width;
+        win.height = p.film_height;
+        amvpt_render_opts opts{};
+        if (amvpt_render_ex(dc->scene, sn.views.data(), &p, &lanes, &win, stream, &opts, counters) != AMVPT_OK)
             throw std::runtime_error(amvpt_last_error());
-        if (raw) {
-            if (hipMemcpy(out, film, npx * C * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
-                throw std::runtime_error("hipMemcpy(film) failed");
-            return 0;
+        ++s->renders;
+        const float *src = dc->film;
+        size_t bytes = npx * C * sizeof(float);
+        if (!raw) {
+            const uint32_t T = p.film_alpha ? 4u : 3u;
+            bytes = npx * T * sizeof(float);
+            ensure_buffer(dc->image, dc->image_bytes, bytes, s->buffer_allocs);
+            if (amvpt_develop(dc->film, dc->image, p.film_width, p.film_height, p.film_alpha, stream) != AMVPT_OK)
+                throw std::runtime_error(amvpt_last_error());
+            src = dc->image;
         }
-        const uint32_t T = p.film_alpha ? 4u : 3u;
-        if (hipMalloc(&dev_out, npx * T * sizeof(float)) != hipSuccess) throw std::runtime_error("hipMalloc(out) failed");
-        fr.b = dev_out;
-        if (amvpt_develop(film, dev_out, p.film_width, p.film_height, p.film_alpha, nullptr) != AMVPT_OK)
-            throw std::runtime_error(amvpt_last_error());
-        if (hipMemcpy(out, dev_out, npx * T * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
-            throw std::runtime_error("hipMemcpy(out) failed");
+        if (hipMemcpyAsync(out, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            throw std::runtime_error("copying the image to the host failed");
+        return 0;
+    });
+}
+
+int amvpt_host_render(amvpt_host_scene *s, uint32_t si, uint32_t seed, uint32_t spp, int raw, float *out,
+                      amvpt_counters *counters) {
+    return amvpt_host_render_stream(s, si, seed, spp, raw, out, nullptr, counters);
+}
+
+int amvpt_host_render_stats(amvpt_host_scene *s, uint64_t *scene_creates, uint64_t *buffer_allocs, uint64_t *renders) {
+    return guarded([&] {
+        if (!s) throw std::runtime_error("amvpt_host_render_stats: null scene");
+        std::lock_guard<std::mutex> lock(s->render_mu);
+        if (scene_creates) *scene_creates = s->scene_creates;
+        if (buffer_allocs) *buffer_allocs = s->buffer_allocs;
+        if (renders) *renders = s->renders;
         return 0;
     });
 }

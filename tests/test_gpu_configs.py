@@ -303,3 +303,40 @@ def test_counters_report_records_and_invalid_samples(gpu_ready, amvpt_mod, scene
     assert cnt.record_bytes == 80 + (4 if compact else 32) * G
     assert cnt.nonfinite_samples == 0 and cnt.negative_samples == 0
     assert cnt.view_splats > 0
+
+
+def test_host_render_threads_and_cache(gpu_ready, amvpt_mod):
+    """The drop-in host render (Integrator::render -> amvpt_host_render_stream) is stateless and per-frame
+    cheap: two host threads rendering two different scenes at once get the films of the same renders run
+    one after the other, and each scene creates its device scene and its film / image buffers once, not
+    per frame (ADVICE / VERDICT r03: the host path rebuilt and re-allocated per frame through globals)."""
+    import threading
+    a = amvpt_mod.load_file(CBOX, res=32, spp=16)                                  # mvpath, 8 views
+    b = amvpt_mod.load_file(os.path.join(SCENES, "cbox_path.xml"), res=48, spp=8)  # stock path
+    ref = {"a": amvpt_mod.render(a), "b": amvpt_mod.render(b)}
+    got = {"a": [], "b": []}
+    errors = []
+
+    def work(name, scene):
+        try:
+            for _ in range(3):
+                got[name].append(amvpt_mod.render(scene))
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=(n, sc)) for n, sc in (("a", a), ("b", b))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors and all(not t.is_alive() for t in threads)
+    for name in ("a", "b"):
+        assert len(got[name]) == 3
+        for img in got[name]:   # the same frame: equal up to the order of the float splat sums
+            assert np.abs(img - ref[name]).max() <= 1e-5 * max(1.0, np.abs(ref[name]).max())
+    for scene in (a, b):
+        st = amvpt_mod.render_stats(scene)
+        assert st == {"scene_creates": 1, "buffer_allocs": 2, "renders": 4}, st
+    # the raw ImageBlock comes straight from the cached film: no new allocation
+    amvpt_mod.render(a, raw=True)
+    assert amvpt_mod.render_stats(a)["buffer_allocs"] == 2
