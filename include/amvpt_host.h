@@ -92,6 +92,16 @@ int amvpt_host_view_group_partition(const amvpt_params *params, uint32_t rank, u
 int amvpt_host_multi_stats(amvpt_host_scene *scene, uint64_t *scene_creates, uint64_t *comm_inits, uint64_t *renders);
 
 /*
+ * Test hook (CPU, no device): amvpt_host_render_multi's rank coordination (host/ranks.h: phase barriers,
+ * the in-process count exchange and its abort) with n rank threads that each make `passes` count
+ * exchanges in the render phase; rank fail_rank fails in phase fail_phase (0 setup, 1 render before its
+ * exchanges, 2 render between them, 3 render after them, 4 before the gather, 5 finish; -1 none).
+ * Returns 0 when every rank succeeded, 1 with the reported (first own) failure in
+ * amvpt_host_last_error(), 2 if an exchange returned a wrong prefix.  Never leaves a thread blocked.
+ */
+int amvpt_host_test_ranks(int n, int passes, int fail_rank, int fail_phase);
+
+/*
  * The exact descriptors render() hands to the C-ABI (for the parity tests: the oracle
  * consumes the same scene, views and params).  Pointers stay valid until the scene is freed.
  */

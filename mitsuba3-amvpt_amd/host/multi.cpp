@@ -41,80 +41,11 @@
 
 #include "../../include/amvpt.h"
 #include "../../include/amvpt_host.h"
+#include "ranks.h"
 
 namespace {
 
-/* in-process barrier of the device threads; each thread reports whether it is healthy and learns
- * whether all were */
-struct Barrier {
-    std::mutex mu;
-    std::condition_variable cv;
-    int world = 1, arrived = 0;
-    uint64_t generation = 0;
-    bool all_ok = true, published_ok = true;
-    bool wait(bool ok) {
-        std::unique_lock<std::mutex> lk(mu);
-        const uint64_t gen = generation;
-        all_ok = all_ok && ok;
-        if (++arrived == world) {
-            published_ok = all_ok;
-            all_ok = true;
-            arrived = 0;
-            ++generation;
-            cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != gen; });
-        }
-        return published_ok;
-    }
-};
-
-/* per-pass all-gather of the adaptive fill's per-run counts between the device threads
- * (amvpt_run_exchange_fn); a failed device aborts it so no peer waits */
-struct RunExchange {
-    std::mutex mu;
-    std::condition_variable cv;
-    int world = 1, arrived = 0;
-    bool aborted = false;
-    uint64_t generation = 0;
-    std::vector<std::vector<uint64_t>> begins, counts, pub_b, pub_c;
-
-    int exchange(int rank, uint32_t n, const uint64_t *b, const uint64_t *c, uint64_t *prefix, uint64_t *total) {
-        std::unique_lock<std::mutex> lk(mu);
-        if (aborted) return -1;
-        const uint64_t gen = generation;
-        begins[(size_t) rank].assign(b, b + n);
-        counts[(size_t) rank].assign(c, c + n);
-        if (++arrived == world) {
-            pub_b = begins;
-            pub_c = counts;
-            arrived = 0;
-            ++generation;
-            cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != gen || aborted; });
-            if (generation == gen) return -1;
-        }
-        /* runs of different devices are disjoint: a run's prefix is every count that starts below it */
-        uint64_t t = 0;
-        for (int r = 0; r < world; ++r)
-            for (uint64_t x : pub_c[(size_t) r]) t += x;
-        for (uint32_t i = 0; i < n; ++i) {
-            uint64_t p = 0;
-            for (int r = 0; r < world; ++r)
-                for (size_t j = 0; j < pub_b[(size_t) r].size(); ++j)
-                    if (pub_b[(size_t) r][j] < b[i]) p += pub_c[(size_t) r][j];
-            prefix[i] = p;
-        }
-        *total = t;
-        return 0;
-    }
-    void abort() {
-        std::lock_guard<std::mutex> lk(mu);
-        aborted = true;
-        cv.notify_all();
-    }
-};
+using amvpt_ranks::RunExchange;
 struct RankExchange { RunExchange *ex; int rank; };
 int run_exchange_cb(void *ctx, uint32_t n, const uint64_t *b, const uint64_t *c, uint64_t *prefix, uint64_t *total) {
     const RankExchange *x = static_cast<const RankExchange *>(ctx);
@@ -321,48 +252,41 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
                                                      wins[(size_t) r].data()) == 1;
         const uint64_t ov_cap = 1u << 20;
 
-        Barrier bar;
-        bar.world = n;
-        RunExchange ex;
-        ex.world = n;
-        ex.begins.resize((size_t) n);
-        ex.counts.resize((size_t) n);
+        amvpt_ranks::Ranks ranks;
+        RunExchange &ex = ranks.ex;
         std::vector<RankExchange> rx((size_t) n);
-        std::vector<std::string> errors((size_t) n);
         std::vector<amvpt_counters> cnt((size_t) n);
         std::vector<uint64_t> ov_count((size_t) n, 0);
-        std::vector<std::thread> threads;
-        for (int r = 0; r < n; ++r) {
-            threads.emplace_back([&, r] {
-                DevState &D = cache->dev[(size_t) r];
-                std::string &err = errors[(size_t) r];
-                auto fail = [&](const std::string &m) { if (err.empty()) err = m; };
-                /* -- setup (nothing collective) -- */
-                if (hipSetDevice(D.device) != hipSuccess) fail("hipSetDevice failed");
-                if (err.empty() && !D.st && hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking) != hipSuccess) fail("hipStreamCreate failed");
-                if (err.empty() && !D.scene) {
-                    if (amvpt_scene_create(sd, &D.scene) != AMVPT_OK) fail(amvpt_last_error());
-                    else {
-                        std::lock_guard<std::mutex> lk(bar.mu);
-                        ++cache->scene_creates;
-                    }
+        std::mutex stat_mu;
+        auto wfloats_of = [&](int r) { return groups ? (size_t) wins[(size_t) r][2] * wins[(size_t) r][3] * C : nfloat; };
+        const std::string failure = ranks.run(n, [&](int r, int ph) -> std::string {
+            DevState &D = cache->dev[(size_t) r];
+            const size_t wfloats = wfloats_of(r);
+            switch (ph) {
+            case amvpt_ranks::SETUP: {   /* nothing collective */
+                if (hipSetDevice(D.device) != hipSuccess) return "hipSetDevice failed";
+                if (!D.st && hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking) != hipSuccess) return "hipStreamCreate failed";
+                if (!D.scene) {
+                    if (amvpt_scene_create(sd, &D.scene) != AMVPT_OK) return amvpt_last_error();
+                    std::lock_guard<std::mutex> lk(stat_mu);
+                    ++cache->scene_creates;
                 }
-                const size_t wfloats = groups ? (size_t) wins[(size_t) r][2] * wins[(size_t) r][3] * C : nfloat;
-                if (err.empty() && !grow(D.film, D.film_bytes, wfloats * sizeof(float))) fail("hipMalloc(film) failed");
-                if (err.empty() && groups && !grow(D.ovf, D.ovf_bytes, 16 * (ov_cap + 1))) fail("hipMalloc(overflow) failed");
-                if (err.empty() && hipMemsetAsync(D.film, 0, wfloats * sizeof(float), D.st) != hipSuccess) fail("hipMemset(film) failed");
-                if (err.empty() && groups && hipMemsetAsync(D.ovf, 0, 16, D.st) != hipSuccess) fail("hipMemset(overflow) failed");
-                if (r == 0 && err.empty() && groups) {
-                    if (!grow(D.quilt, D.quilt_bytes, nfloat * sizeof(float))) fail("hipMalloc(quilt) failed");
+                if (!grow(D.film, D.film_bytes, wfloats * sizeof(float))) return "hipMalloc(film) failed";
+                if (groups && !grow(D.ovf, D.ovf_bytes, 16 * (ov_cap + 1))) return "hipMalloc(overflow) failed";
+                if (hipMemsetAsync(D.film, 0, wfloats * sizeof(float), D.st) != hipSuccess) return "hipMemset(film) failed";
+                if (groups && hipMemsetAsync(D.ovf, 0, 16, D.st) != hipSuccess) return "hipMemset(overflow) failed";
+                if (r == 0 && groups) {
+                    if (!grow(D.quilt, D.quilt_bytes, nfloat * sizeof(float))) return "hipMalloc(quilt) failed";
                     D.recv.resize((size_t) n, nullptr); D.recv_bytes.resize((size_t) n, 0);
                     D.recv_ov.resize((size_t) n, nullptr); D.recv_ov_bytes.resize((size_t) n, 0);
-                    for (int q = 1; q < n && err.empty(); ++q)
-                        if (!grow(D.recv[(size_t) q], D.recv_bytes[(size_t) q], (size_t) wins[(size_t) q][2] * wins[(size_t) q][3] * C * sizeof(float)))
-                            fail("hipMalloc(window receive) failed");
+                    for (int q = 1; q < n; ++q)
+                        if (!grow(D.recv[(size_t) q], D.recv_bytes[(size_t) q], wfloats_of(q) * sizeof(float)))
+                            return "hipMalloc(window receive) failed";
                 }
-                if (!bar.wait(err.empty())) { if (err.empty()) err = "a peer device failed during setup"; return; }
-
-                /* -- render this device's share (the count exchange is the only cross-device step) -- */
+                return "";
+            }
+            case amvpt_ranks::RENDER: {   /* this device's share; the count exchange is the only cross-device step */
+                if (hipSetDevice(D.device) != hipSuccess) return "hipSetDevice failed";
                 amvpt_lane_set lanes{};
                 amvpt_film_window fw{};
                 fw.film = D.film;
@@ -380,29 +304,26 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
                 rx[(size_t) r] = RankExchange{&ex, r};
                 amvpt_render_opts o{};
                 if (n > 1) { o.exchange = run_exchange_cb; o.exchange_ctx = &rx[(size_t) r]; }
-                if (amvpt_render_ex(D.scene, views, &p, &lanes, &fw, D.st, &o, counters ? &cnt[(size_t) r] : nullptr) != AMVPT_OK) {
-                    fail(amvpt_last_error());
-                    ex.abort();
-                }
-                if (err.empty() && groups &&
-                    (hipMemcpyAsync(&ov_count[(size_t) r], D.ovf, 8, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
-                     hipStreamSynchronize(D.st) != hipSuccess))
-                    fail("overflow count read failed");
-                if (!bar.wait(err.empty())) { if (err.empty()) err = "a peer device failed during the render"; return; }
-
-                /* -- combine on devices[0]: every device is healthy here, so every collective completes -- */
+                if (amvpt_render_ex(D.scene, views, &p, &lanes, &fw, D.st, &o, counters ? &cnt[(size_t) r] : nullptr) != AMVPT_OK)
+                    return amvpt_last_error();
+                if (groups && (hipMemcpyAsync(&ov_count[(size_t) r], D.ovf, 8, hipMemcpyDeviceToHost, D.st) != hipSuccess ||
+                               hipStreamSynchronize(D.st) != hipSuccess))
+                    return "overflow count read failed";
+                return "";
+            }
+            case amvpt_ranks::PREPARE:   /* devices[0]: room for the peers' overflow cells */
+                if (groups && r == 0)
+                    for (int q = 1; q < n; ++q)
+                        if (!grow(D.recv_ov[(size_t) q], D.recv_ov_bytes[(size_t) q], 16 * std::max<uint64_t>(1, ov_count[(size_t) q])))
+                            return "hipMalloc(overflow receive) failed";
+                return "";
+            case amvpt_ranks::COMBINE: {   /* every device is healthy here, so every collective completes */
                 if (groups) {
-                    if (r == 0)
-                        for (int q = 1; q < n && err.empty(); ++q)
-                            if (!grow(D.recv_ov[(size_t) q], D.recv_ov_bytes[(size_t) q], 16 * std::max<uint64_t>(1, ov_count[(size_t) q])))
-                                fail("hipMalloc(overflow receive) failed");
-                    if (!bar.wait(err.empty())) { if (err.empty()) err = "a peer device failed before the gather"; return; }
                     ncclComm_t comm = cache->comms[(size_t) r];
                     bool ok = ncclGroupStart() == ncclSuccess;
                     if (r == 0) {
                         for (int q = 1; q < n; ++q) {
-                            const size_t wf = (size_t) wins[(size_t) q][2] * wins[(size_t) q][3] * C;
-                            ok = ok && ncclRecv(D.recv[(size_t) q], wf, ncclFloat, q, comm, D.st) == ncclSuccess;
+                            ok = ok && ncclRecv(D.recv[(size_t) q], wfloats_of(q), ncclFloat, q, comm, D.st) == ncclSuccess;
                             if (ov_count[(size_t) q])
                                 ok = ok && ncclRecv(D.recv_ov[(size_t) q], 4 * ov_count[(size_t) q], ncclUint32, q, comm, D.st) == ncclSuccess;
                         }
@@ -412,43 +333,49 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
                             ok = ok && ncclSend(D.ovf + 4, 4 * ov_count[(size_t) r], ncclUint32, 0, comm, D.st) == ncclSuccess;
                     }
                     ok = (ncclGroupEnd() == ncclSuccess) && ok;
-                    if (!ok) fail("ncclSend / ncclRecv of the film windows failed");
-                    if (r == 0 && err.empty()) {
-                        if (hipMemsetAsync(D.quilt, 0, nfloat * sizeof(float), D.st) != hipSuccess) fail("hipMemset(quilt) failed");
-                        for (int q = 0; q < n && err.empty(); ++q) {
+                    if (!ok) return "ncclSend / ncclRecv of the film windows failed";
+                    if (r == 0) {
+                        if (hipMemsetAsync(D.quilt, 0, nfloat * sizeof(float), D.st) != hipSuccess) return "hipMemset(quilt) failed";
+                        for (int q = 0; q < n; ++q) {
                             const auto &w = wins[(size_t) q];
                             const float *win = q == 0 ? D.film : D.recv[(size_t) q];
                             const uint32_t *ov = q == 0 ? D.ovf + 4 : D.recv_ov[(size_t) q];
                             if (amvpt_film_accumulate(D.quilt, p.film_width, p.film_height, C, win, w[0], w[1], w[2], w[3], ov,
                                                       ov_count[(size_t) q], D.st) != AMVPT_OK)
-                                fail(amvpt_last_error());
+                                return amvpt_last_error();
                         }
                     }
                 } else if (n > 1) {
                     if (ncclReduce(D.film, D.film, nfloat, ncclFloat, ncclSum, 0, cache->comms[(size_t) r], D.st) != ncclSuccess)
-                        fail("ncclReduce failed");
+                        return "ncclReduce failed";
                 }
-                if (D.st && hipStreamSynchronize(D.st) != hipSuccess) fail("hipStreamSynchronize failed");
-                /* -- develop / copy out on devices[0] -- */
-                if (r == 0 && err.empty()) {
-                    const float *frame = groups ? D.quilt : D.film;
-                    if (raw) {
-                        if (hipMemcpy(out, frame, nfloat * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) fail("hipMemcpy(film) failed");
-                    } else {
-                        const uint32_t T = p.film_alpha ? 4u : 3u;
-                        if (!grow(D.out, D.out_bytes, npx * T * sizeof(float))) fail("hipMalloc(out) failed");
-                        else if (amvpt_develop(frame, D.out, p.film_width, p.film_height, p.film_alpha, D.st) != AMVPT_OK)
-                            fail(amvpt_last_error());
-                        else if (hipStreamSynchronize(D.st) != hipSuccess ||
-                                 hipMemcpy(out, D.out, npx * T * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
-                            fail("develop / copy-out failed");
-                    }
+                if (D.st && hipStreamSynchronize(D.st) != hipSuccess) return "hipStreamSynchronize failed";
+                return "";
+            }
+            default: {   /* FINISH: develop / copy out on devices[0] */
+                if (r != 0) return "";
+                const float *frame = groups ? D.quilt : D.film;
+                if (raw) {
+                    if (hipMemcpy(out, frame, nfloat * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return "hipMemcpy(film) failed";
+                    return "";
                 }
-            });
+                const uint32_t T = p.film_alpha ? 4u : 3u;
+                if (!grow(D.out, D.out_bytes, npx * T * sizeof(float))) return "hipMalloc(out) failed";
+                if (amvpt_develop(frame, D.out, p.film_width, p.film_height, p.film_alpha, D.st) != AMVPT_OK)
+                    return amvpt_last_error();
+                if (hipStreamSynchronize(D.st) != hipSuccess ||
+                    hipMemcpy(out, D.out, npx * T * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+                    return "develop / copy-out failed";
+                return "";
+            }
+            }
+        });
+        if (!failure.empty()) {
+            /* name the device of the failing rank */
+            const size_t sp = failure.find(':');
+            const int fr = std::atoi(failure.c_str() + 5);
+            throw std::runtime_error("device " + std::to_string(devices[fr]) + failure.substr(sp));
         }
-        for (auto &t : threads) t.join();
-        for (int r = 0; r < n; ++r)
-            if (!errors[(size_t) r].empty()) throw std::runtime_error("device " + std::to_string(devices[r]) + ": " + errors[(size_t) r]);
         ++cache->renders;
         if (counters) {
             /* lane statistics sum over the shards; per-kernel and wall times: the slowest device */
@@ -474,6 +401,49 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
         }
         return 0;
     });
+}
+
+int amvpt_host_test_ranks(int n, int passes, int fail_rank, int fail_phase) {
+    int status = 0;
+    const int rc = amvpt_host_guarded([&] {
+        if (n < 1 || n > 64 || passes < 0) throw std::runtime_error("amvpt_host_test_ranks: 1 <= n <= 64, passes >= 0");
+        amvpt_ranks::Ranks ranks;
+        std::mutex mu;
+        bool bad_prefix = false;
+        const std::string failure = ranks.run(n, [&](int r, int ph) -> std::string {
+            const bool fails = r == fail_rank;
+            switch (ph) {
+            case amvpt_ranks::SETUP:
+                return fails && fail_phase == 0 ? "injected setup failure" : "";
+            case amvpt_ranks::RENDER:
+                if (fails && fail_phase == 1) return "injected render failure before the exchanges";
+                for (int k = 0; k < passes; ++k) {
+                    if (fails && fail_phase == 2 && k == passes / 2) return "injected render failure between exchanges";
+                    /* one run per rank: begin 1000 r, (r + 1)(k + 1) flagged lanes */
+                    const uint64_t b = 1000ull * (uint64_t) r, c = (uint64_t) (r + 1) * (uint64_t) (k + 1);
+                    uint64_t prefix = 0, total = 0;
+                    if (ranks.ex.exchange(r, 1, &b, &c, &prefix, &total) != 0) return "amvpt_render: adaptive count exchange failed";
+                    const uint64_t want_p = (uint64_t) r * (uint64_t) (r + 1) / 2 * (uint64_t) (k + 1);
+                    const uint64_t want_t = (uint64_t) n * (uint64_t) (n + 1) / 2 * (uint64_t) (k + 1);
+                    if (prefix != want_p || total != want_t) {
+                        std::lock_guard<std::mutex> lk(mu);
+                        bad_prefix = true;
+                    }
+                }
+                return fails && fail_phase == 3 ? "injected render failure after the exchanges" : "";
+            case amvpt_ranks::PREPARE:
+                return fails && fail_phase == 4 ? "injected failure before the gather" : "";
+            case amvpt_ranks::COMBINE:
+                return "";
+            default:
+                return fails && fail_phase == 5 ? "injected finish failure" : "";
+            }
+        });
+        if (bad_prefix) { status = 2; throw std::runtime_error("amvpt_host_test_ranks: wrong exchange prefix"); }
+        if (!failure.empty()) { status = 1; throw std::runtime_error(failure); }
+        return 0;
+    });
+    return rc == 0 ? 0 : (status ? status : 1);
 }
 
 }  // extern "C"

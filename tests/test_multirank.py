@@ -296,3 +296,33 @@ def test_render_multi_fails_fast_on_a_bad_device(amvpt_mod):
     s = amvpt_mod.load_file(CBOX, res=16, spp=16)
     with pytest.raises(RuntimeError, match="not visible"):
         amvpt_mod.render_multi(s, [0, 99])
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_render_multi_rank_failures_never_block(amvpt_mod, n):
+    """Failure injection into amvpt_host_render_multi's rank coordination (host/ranks.h, on the CPU): one
+    rank failing in setup, before / between / after its count exchanges, before the gather or at the end
+    makes the call return that rank's own error -- not a peer's "a peer failed" echo -- and no thread stays
+    blocked in a barrier or in the exchange (each case runs under a watchdog)."""
+    import ctypes
+    import threading
+    L = amvpt_mod.host_lib()
+    L.amvpt_host_test_ranks.argtypes = [ctypes.c_int] * 4
+    L.amvpt_host_test_ranks.restype = ctypes.c_int
+    msgs = {0: "injected setup failure", 1: "before the exchanges", 2: "between exchanges",
+            3: "after the exchanges", 4: "before the gather", 5: "injected finish failure"}
+
+    def run(*args):
+        out = {}
+        t = threading.Thread(target=lambda: out.update(rc=L.amvpt_host_test_ranks(*args),
+                                                       err=L.amvpt_host_last_error().decode()))
+        t.start()
+        t.join(timeout=30)
+        assert not t.is_alive(), "rank coordination blocked: %r" % (args,)
+        return out["rc"], out["err"]
+
+    assert run(n, 4, -1, -1)[0] == 0                       # healthy: every exchange prefix checked
+    for phase, msg in msgs.items():
+        for rank in sorted({0, n // 2, n - 1}):
+            rc, err = run(n, 4, rank, phase)
+            assert rc == 1 and err.startswith("rank %d: " % rank) and msg in err, (phase, rank, rc, err)
