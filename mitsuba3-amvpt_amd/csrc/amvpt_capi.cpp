@@ -76,6 +76,12 @@ struct BNode { Box box; uint32_t left_or_first, count, axis = 0; };
  * of the children's tests (amvpt_set_bvh_build). */
 static uint32_t g_bvh_max_leaf = 4;
 static float g_bvh_trav_cost = 0.f;
+/* depth of the LDS treelets (dscene.h DScene::tnodes), 0: none (A/B builds: EXTRA=-DAMVPT_TREELET_DEPTH=n);
+ * 2^depth - 1 nodes at most, 32 B each */
+#ifndef AMVPT_TREELET_DEPTH
+#define AMVPT_TREELET_DEPTH 8
+#endif
+static const uint32_t g_treelet_depth = AMVPT_TREELET_DEPTH;
 
 struct Builder {
     std::vector<BuildPrim> &prims;
@@ -163,17 +169,39 @@ struct Builder {
      * axis first for a positive direction, the upper one first for a negative direction.  The
      * skip links are local to the copy, so octant copy o is the array at o * n_nodes.
      */
-    void flatten(uint32_t ni, std::vector<DNode> &out, uint32_t oct = 0, uint32_t base = 0) const {
+    void flatten(uint32_t ni, std::vector<DNode> &out, uint32_t oct = 0, uint32_t base = 0,
+                 std::vector<uint32_t> *pos = nullptr) const {
         const BNode &bn = nodes[ni];
         const uint32_t at = (uint32_t) out.size();
+        if (pos) (*pos)[ni] = at;
         DNode d{};
         for (int i = 0; i < 3; ++i) { d.lo[i] = bn.box.lo[i]; d.hi[i] = bn.box.hi[i]; }
         d.first = bn.count ? bn.left_or_first : 0u;
         out.push_back(d);
         if (!bn.count) {
             const uint32_t near = (oct >> bn.axis) & 1u;
-            flatten(bn.left_or_first + near, out, oct, base);
-            flatten(bn.left_or_first + (near ^ 1u), out, oct, base);
+            flatten(bn.left_or_first + near, out, oct, base, pos);
+            flatten(bn.left_or_first + (near ^ 1u), out, oct, base, pos);
+        }
+        out[at].skip_count = (((uint32_t) out.size() - base) & kNodeSkipMask) | (bn.count << kNodeCountShift);
+    }
+    /* the treelet of one ordering: the nodes of depth < depth_cut in the same depth-first order, skip links
+     * local to the treelet; an inner node at depth depth_cut - 1 is a portal to its subtree in the global
+     * copy (gpos: each builder node's index in that copy's array, including the copy's base) */
+    void flatten_top(uint32_t ni, std::vector<DNode> &out, uint32_t oct, uint32_t depth, uint32_t depth_cut,
+                     const std::vector<uint32_t> &gpos, uint32_t gbase, uint32_t base) const {
+        const BNode &bn = nodes[ni];
+        const uint32_t at = (uint32_t) out.size();
+        DNode d{};
+        for (int i = 0; i < 3; ++i) { d.lo[i] = bn.box.lo[i]; d.hi[i] = bn.box.hi[i]; }
+        d.first = bn.count ? bn.left_or_first : 0u;
+        const bool portal = !bn.count && depth + 1 >= depth_cut;
+        if (portal) d.first = kPortal | (gpos[ni] - gbase);   /* index local to the copy, as its skip links */
+        out.push_back(d);
+        if (!bn.count && !portal) {
+            const uint32_t near = (oct >> bn.axis) & 1u;
+            flatten_top(bn.left_or_first + near, out, oct, depth + 1, depth_cut, gpos, gbase, base);
+            flatten_top(bn.left_or_first + (near ^ 1u), out, oct, depth + 1, depth_cut, gpos, gbase, base);
         }
         out[at].skip_count = (((uint32_t) out.size() - base) & kNodeSkipMask) | (bn.count << kNodeCountShift);
     }
@@ -520,9 +548,10 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (!vnrm.empty()) vnrm.resize(vpos.size(), 0.f);
     if (!vuv.empty()) vuv.resize(2 * (vpos.size() / 3), 0.f);
 
-    std::vector<DNode> nodes;
+    std::vector<DNode> nodes, tnodes;
     std::vector<DPrim> prims;
     uint32_t oct_stride = 0;   /* nodes per octant copy (0: one copy) */
+    uint32_t t_stride = 0;     /* treelet nodes per ordering (0: no treelets) */
     if (bprims.empty()) {
         /* one inner node with an empty box: every ray misses it and skips to the end */
         DNode root{};
@@ -536,7 +565,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         b.nodes.resize(1);
         b.build(0, 0, (uint32_t) bprims.size(), 0);
         nodes.reserve(b.nodes.size());
-        b.flatten(0, nodes);
+        std::vector<std::vector<uint32_t>> gpos(8, std::vector<uint32_t>(b.nodes.size(), 0u));
+        b.flatten(0, nodes, 0, 0, &gpos[0]);
         if (nodes.size() > kNodeSkipMask) {
             set_error("BVH too large (more than 2^28 nodes)");
             return AMVPT_ERR_INVALID;
@@ -549,8 +579,18 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         const uint64_t lds_b = (uint64_t) n0 * sizeof(DNode) + bprims.size() * sizeof(DPrim);
         if (!(e && e[0] == '0') && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes && (uint64_t) n0 * 8 <= kNodeSkipMask) {
             nodes.reserve((size_t) n0 * 8);
-            for (uint32_t o = 1; o < 8; ++o) b.flatten(0, nodes, o, o * n0);
+            for (uint32_t o = 1; o < 8; ++o) b.flatten(0, nodes, o, o * n0, &gpos[o]);
             oct_stride = n0;
+        }
+        /* LDS treelets for BVHs the walks read from global memory (neither wave-uniform-small nor staged
+         * whole): one per node ordering */
+        if (g_treelet_depth > 0 && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes) {
+            const uint32_t copies = oct_stride ? 8u : 1u;
+            for (uint32_t o = 0; o < copies; ++o) {
+                const uint32_t base = (uint32_t) tnodes.size();
+                b.flatten_top(0, tnodes, o, 0, g_treelet_depth, gpos[o], o * n0, base);
+                if (o == 0) t_stride = (uint32_t) tnodes.size();
+            }
         }
         prims.resize(bprims.size());
         for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
@@ -613,7 +653,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", (int) e);
         return AMVPT_OK;
     };
-    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea;
+    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes;
+    if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
     amvpt_status st;
 #define UP(vec, ptr)                                                                      \
     if ((st = upload(vec.data(), vec.size() * sizeof(vec[0]), &ptr)) != AMVPT_OK) {       \
@@ -621,7 +662,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         return st;                                                                        \
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
-    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea)
+    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -636,6 +677,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.face_area = (const float *) p_farea;
     D.n_nodes = oct_stride ? oct_stride : (uint32_t) nodes.size();
     D.oct_stride = oct_stride;
+    D.tnodes = (const DNode *) p_tnodes;
+    D.t_stride = t_stride;
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;

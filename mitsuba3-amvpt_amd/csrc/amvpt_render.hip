@@ -193,6 +193,11 @@ __host__ __device__ inline bool scene_staged(uint32_t n_nodes, uint32_t lds_byte
 __host__ __device__ inline uint32_t scene_lds_bytes(const DScene &S, uint32_t mode) {
     return scene_staged(S.n_nodes, S.lds_bytes, mode) ? (S.lds_bytes + 15u) & ~15u : 0u;
 }
+/* the LDS treelet of the first node ordering (any-hit walks of BVHs read from global memory) */
+__host__ __device__ inline uint32_t tree_lds_bytes(const DScene &S, uint32_t mode) {
+    return (S.t_stride && !scene_staged(S.n_nodes, S.lds_bytes, mode) && !scene_uniform(S.n_nodes, mode))
+               ? S.t_stride * (uint32_t) sizeof(DNode) : 0u;
+}
 
 __host__ __device__ inline uint32_t views_lds_bytes(uint32_t n_views) {
     const uint32_t b = n_views * (uint32_t) sizeof(DView);
@@ -224,10 +229,12 @@ template <typename T> AD T *copy_to_lds(const T *src, uint32_t bytes, char *&dst
  * lane-divergent reads then hit LDS instead of L1/L2.  S is the kernel's local
  * copy of the scene header; its table pointers are redirected.
  */
-template <bool kTab, bool kBvh = true>
+template <bool kTab, bool kBvh = true, bool kTree = false>
 AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0) {
     SceneRef sc;
     sc.g = &S;
+    sc.tnodes = nullptr;
+    sc.t_n = 0;
     sc.n_nodes = S.n_nodes;
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
@@ -247,6 +254,16 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
         sc.oct_stride = 0;   /* only the first ordering is staged */
         sc.prims = (const DPrim *) (lds + (size_t) nn * 16);
         dst = lds + scene_lds_bytes(S, mode);
+        sync = true;
+    } else if (kTree && tree_lds_bytes(S, mode)) {
+        /* the treelet of the first node ordering (any-hit walks: trace_any_tl / trace_any_uni_tl) */
+        const uint32_t n4 = S.t_stride * (uint32_t) sizeof(DNode) / 16;
+        float4 *d4 = (float4 *) lds;
+        const float4 *st = (const float4 *) S.tnodes;
+        for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = st[i];
+        sc.tnodes = (const DNode *) lds;
+        sc.t_n = S.t_stride;
+        dst = lds + tree_lds_bytes(S, mode);
         sync = true;
     }
     /* compile-time choice (the host launches the kTab variant only when the tables fit),
@@ -1645,6 +1662,9 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #ifndef AMVPT_EXTEND_WAVES
 #define AMVPT_EXTEND_WAVES 6
 #endif
+#ifndef AMVPT_TREELETS
+#define AMVPT_TREELETS 1   /* the any-hit walks (k_vis, k_shadow) of large BVHs start in an LDS treelet (0: A/B) */
+#endif
 #ifndef AMVPT_SHADOW_WAVES
 #define AMVPT_SHADOW_WAVES 1
 #endif
@@ -1673,7 +1693,7 @@ template <int kWalk>
 __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, AMVPT_TREELETS != 0>(S, lds, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_nee[part * kCntStride], pbase = part * B.qcap;
     for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
@@ -2278,7 +2298,7 @@ template <int G, bool kUni>
 __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>())) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, AMVPT_TREELETS != 0>(S, lds, P.trav_mode);
     const int Gn = group_size<G>(P);
     if constexpr (vis_pairs<G, kUni>()) {
         const int k = (int) (threadIdx.x >> 6);
@@ -3862,6 +3882,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const uint32_t fused_blocks = K.fused_blocks;
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
+    const size_t lds_any = lds_ext + (AMVPT_TREELETS ? tree_lds_bytes(scene->dev, trav) : 0u);     /* + any-hit treelet */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
     KTimer T;
     T.init(counters != nullptr);
@@ -3911,7 +3932,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             T.end(st);
             if (!fuse_nee) {
                 T.begin(AMVPT_K_SHADOW, st);
-                launch_shadow(walk, dim3(bgrid), lds_ext, st, P, dS, B);
+                launch_shadow(walk, dim3(bgrid), lds_any, st, P, dS, B);
                 T.end(st);
             }
             HIPCHK(hipGetLastError());
@@ -3966,7 +3987,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                     hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
                     T.end(st);
                 } else {
-                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_ext, st, P, dS, dviews, B, tab_p, uni_coh, diff, T);
+                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_any, st, P, dS, dviews, B, tab_p, uni_coh, diff, T);
                 }
             }
             HIPCHK(hipGetLastError());

@@ -33,6 +33,8 @@ struct SceneRef {
     uint32_t n_nodes;
     uint32_t oct_stride;      /* per-lane walks: octant copy o of the nodes at nodes + o * oct_stride (0: one copy) */
     bool uniform;             /* small BVH: the kernels run their kUni = true instance (see trace_closest) */
+    const DNode *tnodes;      /* LDS treelet of the first node ordering (stage_scene kTree), t_n nodes; 0: none */
+    uint32_t t_n;
 };
 
 
@@ -296,8 +298,130 @@ template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const
     return best;
 }
 
+/*
+ * Any-hit walks over an LDS treelet (large BVHs, DScene::tnodes): the top levels of the first node
+ * ordering sit in LDS (staged per block), so the first node visits of a walk -- the ones every ray makes
+ * -- are LDS reads instead of dependent loads from L2; a portal (a treelet node whose children lie below
+ * the cut) continues the threaded walk in the global array at the same node, whose skip link is the end
+ * of its subtree, and the walk returns to the treelet there.  The nodes tested are the same as the
+ * global walk's (same boxes, same order), so the verdict is the same.
+ */
+constexpr uint32_t kNoEnd = 0xffffffffu;
+AD bool trace_any_tl(const SceneRef &sc, const Ray &ray) {
+    const BoxRay br = box_ray(ray);
+    auto leaf_any = [&](uint32_t first, uint32_t count) {
+        bool f = false;
+        for (uint32_t i = 0; i < count && !f; ++i) {
+            const DPrim p = sc.prims[first + i];
+            float t, u, v;
+            f = prim_hit(p, ray, t, u, v);
+        }
+        return f;
+    };
+    const uint32_t nt = sc.t_n;
+    uint32_t node = 0, gend = 0, tres = 0;
+    bool glob = false, found = false;
+    /* speculative while-while (trace_any kWW = 2): a lane holding a leaf steps on until the wave's
+     * other lanes hold one too, and stops at a second leaf */
+    for (;;) {
+        uint32_t lf = 0, lc = 0;
+        bool stop = false;
+        for (;;) {
+            const bool open = !found && (glob || node < nt);
+            if (!wave_any(open && lc == 0u)) break;
+            if (open && !stop) {
+                const DNode n = glob ? sc.gnodes[node] : sc.tnodes[node];
+                if (glob && gend == kNoEnd) gend = n.skip_count & kNodeSkipMask;   /* the portal's own node */
+                const bool hit = box_hit(n, br, ray.maxt);
+                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                uint32_t next;
+                if (hit && count) {
+                    if (lc == 0u) { lf = n.first; lc = count; next = skip; }
+                    else { stop = true; next = node; }   /* the second leaf: revisit it next round */
+                } else if (hit && !glob && (n.first & kPortal)) {
+                    tres = skip;
+                    glob = true;
+                    gend = kNoEnd;
+                    next = n.first & ~kPortal;
+                } else {
+                    next = hit ? node + 1 : skip;
+                }
+                if (glob && next == gend) { glob = false; next = tres; }
+                node = next;
+            }
+        }
+        if (!wave_any(lc != 0u)) break;
+        if (lc) found = found || leaf_any(lf, lc);
+    }
+    return found;
+}
+
+/* the wave-uniform any-hit walk over the treelet for one or two rays per lane (trace_any<true> /
+ * trace_any2_uni): the treelet node is one LDS broadcast read per wave */
+AD void trace_any_uni_tl(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool two, bool &f0,
+                         bool &f1) {
+    const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
+    f0 = !act0;
+    f1 = !act1 || !two;
+    const uint32_t nt = ufirst(sc.t_n);
+    uint32_t t = 0, g = 0, gend = 0, tres = 0;
+    bool glob = false;
+    for (;;) {
+        DNode n;
+        if (!glob) {
+            if (t >= nt) break;
+            n = sc.tnodes[t];
+        } else {
+            n = load_uniform(sc.gnodes, g);
+            if (gend == kNoEnd) gend = ufirst(n.skip_count) & kNodeSkipMask;
+        }
+        const bool enter = wave_any((!f0 && box_hit(n, b0, r0.maxt)) || (!f1 && box_hit(n, b1, r1.maxt)));
+        const uint32_t skc = ufirst(n.skip_count), first = ufirst(n.first);
+        const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
+        if (enter && count) {
+            for (uint32_t i = 0; i < count; ++i) {
+                const DPrim p = load_uniform(sc.gprims, first + i);
+                const uint32_t type = ufirst(p.type);
+                float tt, u, v;
+                const bool h0 = prim_hit_u(p, type, r0, tt, u, v);
+                f0 = f0 || h0;
+                if (two) {
+                    const bool h1 = prim_hit_u(p, type, r1, tt, u, v);
+                    f1 = f1 || h1;
+                }
+            }
+            if (!wave_any(!f0 || !f1)) break;
+        }
+        if (enter && !count && !glob && (first & kPortal)) {
+            tres = skip;
+            glob = true;
+            gend = kNoEnd;
+            g = first & ~kPortal;
+            continue;
+        }
+        const uint32_t cur = glob ? g : t;
+        const uint32_t next = (enter && !count) ? cur + 1 : skip;
+        if (glob) {
+            if (next == gend) { glob = false; t = tres; }
+            else g = next;
+        } else {
+            t = next;
+        }
+    }
+    f0 = f0 && act0;
+    f1 = f1 && act1 && two;
+}
+
 /* Any hit in [0, maxt] (Scene::ray_test); same two walks as trace_closest. */
 template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
+    if (sc.t_n) {
+        if (kUni) {
+            bool f0, f1;
+            trace_any_uni_tl(sc, ray, true, ray, false, false, f0, f1);
+            return f0;
+        }
+        return trace_any_tl(sc, ray);
+    }
     const BoxRay br = box_ray(ray);
     if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
@@ -378,6 +502,7 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
  * same reason as trace_any: a primitive tested for a ray whose box test failed cannot hit it.
  */
 AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
+    if (sc.t_n) { trace_any_uni_tl(sc, r0, act0, r1, act1, true, f0, f1); return; }
     const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
     const uint32_t nn = ufirst(sc.n_nodes);
     f0 = !act0; f1 = !act1;

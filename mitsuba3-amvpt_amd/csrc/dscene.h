@@ -111,6 +111,13 @@ struct DScene {
     uint32_t n_bsdfs;
     uint32_t tab_bytes;     /* shapes+bsdfs+emitters footprint if <= kTabBytes (staged in LDS), else 0 */
     uint32_t oct_stride;    /* != 0: nodes[] holds 8 direction-octant orderings of n_nodes each (amvpt_capi.cpp) */
+    /* LDS treelets of large BVHs (the walks stage them per block, dgeom.h trace_*_tl): the nodes of depth
+     * < treelet_depth of each node ordering in depth-first order with treelet-local skip links; a node whose
+     * children lie below the cut is a portal (count 0, first = kPortal | its index in `nodes`), where the walk
+     * continues in the global copy.  t_stride nodes per ordering (1 or 8 of them, as oct_stride); 0: none */
+    const DNode *tnodes;
+    uint32_t t_stride;
 };
+constexpr uint32_t kPortal = 0x80000000u;
 
 } // namespace amvpt

@@ -49,8 +49,12 @@ def child(steps=3, kernels=False):
     out = {"variant": os.environ.get("AB_VARIANT", "lib"), "msamples_s": round(lanes * steps / dt / 1e6, 2),
            "ms_per_frame": round(dt * 1e3 / steps, 2)}
     if kernels:
+        # one instrumented frame with every chunk on one stream (per-kernel event times do not overlap)
         c = amvpt.Counters()
-        dev.render(vd, p, film.data_ptr(), counters=c)
+        if hasattr(amvpt, "OPT_ONE_STREAM"):
+            dev.render_ex(vd, p, film.data_ptr(), counters=c, flags=amvpt.OPT_ONE_STREAM)
+        else:
+            dev.render(vd, p, film.data_ptr(), counters=c)
         torch.cuda.synchronize()
         d = c.as_dict()
         out["kernel_ms"] = {k: round(v, 2) for k, v in d["kernel_ms"].items() if v}
