@@ -81,7 +81,10 @@ static float g_bvh_trav_cost = 0.f;
 #ifndef AMVPT_TREELET_DEPTH
 #define AMVPT_TREELET_DEPTH 8
 #endif
-static const uint32_t g_treelet_depth = AMVPT_TREELET_DEPTH;
+#ifndef AMVPT_OCT_TREELET_DEPTH
+#define AMVPT_OCT_TREELET_DEPTH 6   /* the 8 octant treelets of the closest-hit walks: 8 x 63 nodes, 16 KB */
+#endif
+static const uint32_t g_treelet_depth = AMVPT_TREELET_DEPTH, g_oct_treelet_depth = AMVPT_OCT_TREELET_DEPTH;
 
 struct Builder {
     std::vector<BuildPrim> &prims;
@@ -548,10 +551,11 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (!vnrm.empty()) vnrm.resize(vpos.size(), 0.f);
     if (!vuv.empty()) vuv.resize(2 * (vpos.size() / 3), 0.f);
 
-    std::vector<DNode> nodes, tnodes;
+    std::vector<DNode> nodes, tnodes, onodes;
     std::vector<DPrim> prims;
     uint32_t oct_stride = 0;   /* nodes per octant copy (0: one copy) */
-    uint32_t t_stride = 0;     /* treelet nodes per ordering (0: no treelets) */
+    uint32_t t_stride = 0;     /* nodes of the first ordering's treelet (0: none) */
+    uint32_t o_stride = 0;     /* nodes per octant treelet (0: none) */
     if (bprims.empty()) {
         /* one inner node with an empty box: every ray misses it and skips to the end */
         DNode root{};
@@ -585,11 +589,14 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         /* LDS treelets for BVHs the walks read from global memory (neither wave-uniform-small nor staged
          * whole): one per node ordering */
         if (g_treelet_depth > 0 && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes) {
-            const uint32_t copies = oct_stride ? 8u : 1u;
-            for (uint32_t o = 0; o < copies; ++o) {
-                const uint32_t base = (uint32_t) tnodes.size();
-                b.flatten_top(0, tnodes, o, 0, g_treelet_depth, gpos[o], o * n0, base);
-                if (o == 0) t_stride = (uint32_t) tnodes.size();
+            b.flatten_top(0, tnodes, 0, 0, g_treelet_depth, gpos[0], 0, 0);
+            t_stride = (uint32_t) tnodes.size();
+        }
+        if (g_oct_treelet_depth > 0 && oct_stride) {
+            for (uint32_t o = 0; o < 8; ++o) {
+                const uint32_t base = (uint32_t) onodes.size();
+                b.flatten_top(0, onodes, o, 0, g_oct_treelet_depth, gpos[o], o * n0, base);
+                if (o == 0) o_stride = (uint32_t) onodes.size();
             }
         }
         prims.resize(bprims.size());
@@ -653,8 +660,9 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", (int) e);
         return AMVPT_OK;
     };
-    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes;
+    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
+    if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
 #define UP(vec, ptr)                                                                      \
     if ((st = upload(vec.data(), vec.size() * sizeof(vec[0]), &ptr)) != AMVPT_OK) {       \
@@ -662,7 +670,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         return st;                                                                        \
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
-    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes)
+    UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -679,6 +687,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.oct_stride = oct_stride;
     D.tnodes = (const DNode *) p_tnodes;
     D.t_stride = t_stride;
+    D.onodes = (const DNode *) p_onodes;
+    D.o_stride = o_stride;
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;

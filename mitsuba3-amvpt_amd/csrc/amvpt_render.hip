@@ -198,6 +198,11 @@ __host__ __device__ inline uint32_t tree_lds_bytes(const DScene &S, uint32_t mod
     return (S.t_stride && !scene_staged(S.n_nodes, S.lds_bytes, mode) && !scene_uniform(S.n_nodes, mode))
                ? S.t_stride * (uint32_t) sizeof(DNode) : 0u;
 }
+/* the 8 octant treelets (per-lane closest-hit walks) */
+__host__ __device__ inline uint32_t oct_tree_lds_bytes(const DScene &S, uint32_t mode) {
+    return (S.o_stride && S.oct_stride && !scene_staged(S.n_nodes, S.lds_bytes, mode) && !scene_uniform(S.n_nodes, mode))
+               ? 8u * S.o_stride * (uint32_t) sizeof(DNode) : 0u;
+}
 
 __host__ __device__ inline uint32_t views_lds_bytes(uint32_t n_views) {
     const uint32_t b = n_views * (uint32_t) sizeof(DView);
@@ -229,12 +234,14 @@ template <typename T> AD T *copy_to_lds(const T *src, uint32_t bytes, char *&dst
  * lane-divergent reads then hit LDS instead of L1/L2.  S is the kernel's local
  * copy of the scene header; its table pointers are redirected.
  */
-template <bool kTab, bool kBvh = true, bool kTree = false>
+template <bool kTab, bool kBvh = true, bool kTree = false, bool kOct = false>
 AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0) {
     SceneRef sc;
     sc.g = &S;
     sc.tnodes = nullptr;
     sc.t_n = 0;
+    sc.onodes = nullptr;
+    sc.o_n = 0;
     sc.n_nodes = S.n_nodes;
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
@@ -264,6 +271,16 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
         sc.tnodes = (const DNode *) lds;
         sc.t_n = S.t_stride;
         dst = lds + tree_lds_bytes(S, mode);
+        sync = true;
+    } else if (kOct && oct_tree_lds_bytes(S, mode)) {
+        /* the 8 octant treelets (closest-hit walks: trace_closest_tl) */
+        const uint32_t n4 = 8u * S.o_stride * (uint32_t) sizeof(DNode) / 16;
+        float4 *d4 = (float4 *) lds;
+        const float4 *st = (const float4 *) S.onodes;
+        for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = st[i];
+        sc.onodes = (const DNode *) lds;
+        sc.o_n = S.o_stride;
+        dst = lds + oct_tree_lds_bytes(S, mode);
         sync = true;
     }
     /* compile-time choice (the host launches the kTab variant only when the tables fit),
@@ -1672,7 +1689,7 @@ template <int kWalk>
 __global__ void __launch_bounds__(256, AMVPT_EXTEND_WAVES) k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, false, AMVPT_TREELETS != 0>(S, lds, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
@@ -3883,6 +3900,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
     const size_t lds_any = lds_ext + (AMVPT_TREELETS ? tree_lds_bytes(scene->dev, trav) : 0u);     /* + any-hit treelet */
+    const size_t lds_close = lds_ext + (AMVPT_TREELETS ? oct_tree_lds_bytes(scene->dev, trav) : 0u); /* + octant treelets */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
     KTimer T;
     T.init(counters != nullptr);
@@ -3925,7 +3943,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
-            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             T.end(st);
             T.begin(AMVPT_K_BOUNCE, st);
             launch_bounce(tab_b, diff, fuse_nee ? walk : -1, dim3(bgrid), lds, st, P, dS, B);

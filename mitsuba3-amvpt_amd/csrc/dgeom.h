@@ -35,10 +35,13 @@ struct SceneRef {
     bool uniform;             /* small BVH: the kernels run their kUni = true instance (see trace_closest) */
     const DNode *tnodes;      /* LDS treelet of the first node ordering (stage_scene kTree), t_n nodes; 0: none */
     uint32_t t_n;
+    const DNode *onodes;      /* LDS treelets of the 8 octant orderings (stage_scene kOct), o_n nodes each; 0: none */
+    uint32_t o_n;
 };
 
 
 struct Hit { float t, u, v; int32_t prim; };
+constexpr uint32_t kNoEnd = 0xffffffffu;   /* treelet walks: the portal's subtree end, not read yet */
 
 AD bool rect_hit(const DPrim &p, const Ray &r, float &t, float &lx, float &ly) {
     /* to_object.transform_affine(ray) then plane z=0 (rectangle.cpp:447-467) */
@@ -203,7 +206,72 @@ AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float 
  * Testing a primitive for a lane whose own box test failed cannot change that
  * lane's result (its box is padded and inclusive), so both walks are exact.
  */
+/*
+ * Closest hit over the octant treelets (per-lane walks of large BVHs): the ray's direction-octant
+ * ordering starts in its LDS treelet and continues at a portal in the same ordering's global copy
+ * (indices local to the copy), returning to the treelet at the end of the portal's subtree.  The node
+ * sequence is the global walk's, so the hit is the same; speculative while-while as trace_closest.
+ */
+AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
+    Hit best{kInf, 0.f, 0.f, -1};
+    uint32_t best_orig = 0xffffffffu;
+    const BoxRay br = box_ray(ray);
+    float tmax_box = ray.maxt;
+    const uint32_t o = (fbits(ray.d.x) >> 31) | ((fbits(ray.d.y) >> 31) << 1) | ((fbits(ray.d.z) >> 31) << 2);
+    const DNode *const tn = sc.onodes + (size_t) o * sc.o_n;
+    const DNode *const gn = sc.gnodes + (size_t) o * sc.oct_stride;
+    auto leaf_test = [&](uint32_t first, uint32_t count) {
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t pi = first + i;
+            const DPrim p = sc.prims[pi];
+            float t, u, v;
+            if (prim_hit(p, ray, t, u, v)) {
+                if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                    best_orig = p.pad;
+                    tmax_box = t;
+                }
+            }
+        }
+    };
+    const uint32_t nt = sc.o_n;
+    uint32_t node = 0, gend = 0, tres = 0;
+    bool glob = false;
+    for (;;) {
+        uint32_t lf = 0, lc = 0;
+        bool stop = false;
+        for (;;) {
+            const bool open = glob || node < nt;
+            if (!wave_any(open && lc == 0u)) break;
+            if (open && !stop) {
+                const DNode n = glob ? gn[node] : tn[node];
+                if (glob && gend == kNoEnd) gend = n.skip_count & kNodeSkipMask;   /* the portal's own node */
+                const bool hit = box_hit(n, br, tmax_box);
+                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                uint32_t next;
+                if (hit && count) {
+                    if (lc == 0u) { lf = n.first; lc = count; next = skip; }
+                    else { stop = true; next = node; }
+                } else if (hit && !glob && (n.first & kPortal)) {
+                    tres = skip;
+                    glob = true;
+                    gend = kNoEnd;
+                    next = n.first & ~kPortal;
+                } else {
+                    next = hit ? node + 1 : skip;
+                }
+                if (glob && next == gend) { glob = false; next = tres; }
+                node = next;
+            }
+        }
+        if (!wave_any(lc != 0u)) break;
+        leaf_test(lf, lc);
+    }
+    return best;
+}
+
 template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
+    if (!kUni && sc.o_n) return trace_closest_tl(sc, ray);
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
     const BoxRay br = box_ray(ray);
@@ -306,7 +374,6 @@ template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const
  * of its subtree, and the walk returns to the treelet there.  The nodes tested are the same as the
  * global walk's (same boxes, same order), so the verdict is the same.
  */
-constexpr uint32_t kNoEnd = 0xffffffffu;
 AD bool trace_any_tl(const SceneRef &sc, const Ray &ray) {
     const BoxRay br = box_ray(ray);
     auto leaf_any = [&](uint32_t first, uint32_t count) {

@@ -117,6 +117,10 @@ struct DScene {
      * continues in the global copy.  t_stride nodes per ordering (1 or 8 of them, as oct_stride); 0: none */
     const DNode *tnodes;
     uint32_t t_stride;
+    /* the same for the 8 direction-octant orderings (closest-hit walks, trace_closest_tl): o_stride nodes
+     * each, a shallower cut (all 8 are staged together); 0: none */
+    const DNode *onodes;
+    uint32_t o_stride;
 };
 constexpr uint32_t kPortal = 0x80000000u;
 
