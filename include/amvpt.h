@@ -334,7 +334,9 @@ typedef struct amvpt_lane_set {
  * ImageBlock::put does (imageblock.cpp:265-558); a footprint cell of the quilt outside the
  * window is appended to `overflow` (device): a 16-byte header whose first u64 counts the cells,
  * then entries of 4 u32 {quilt float index lo, hi, f32 value bits, 0}, at most overflow_capacity
- * of them (the count keeps counting past it: the caller checks count <= capacity).  A window
+ * of them (the count keeps counting past it).  Renders APPEND to the list: the caller zeroes the
+ * 16-byte header before the first render into it; a render fails with AMVPT_ERR_OOM when the list's
+ * count passes its capacity, and counters.film_overflow reports the cells this render added.  A window
  * smaller than the quilt needs an overflow buffer.  Summing every window into its rectangle and
  * every overflow entry into its float gives the whole-quilt ImageBlock (float summation order aside).
  */
@@ -368,8 +370,10 @@ enum {
     AMVPT_OPT_ONE_STREAM = 8u,        /* every chunk on the render stream (no second chunk stream) */
     AMVPT_OPT_DETERMINISTIC = 16u     /* bitwise-reproducible film: splats summed as 32.32 fixed point with
                                        * integer atomics (order-independent), added to the film once at the
-                                       * end; non-finite splat values are dropped (nonfinite_samples counts
-                                       * them); needs a whole-quilt film window */
+                                       * end; each footprint-cell add is rounded to a multiple of 2^-32 and
+                                       * must stay below 2^31 in magnitude: non-finite values (counted by
+                                       * nonfinite_samples) and finite ones of |v| >= 2^31 (not counted) are
+                                       * dropped; needs a whole-quilt film window */
 };
 typedef struct amvpt_render_opts {
     uint64_t chunk_lanes;             /* 0: automatic (see amvpt_set_chunk_lanes) */

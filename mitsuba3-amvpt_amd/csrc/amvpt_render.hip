@@ -168,8 +168,8 @@ struct Bufs {
     uint32_t *cnt_nee;
     float4 *vreq[3];      /* k_prim_req -> k_vis: (p, bits), (n, ap.x), (emitter point, ap.y) per lane */
     unsigned long long *occ; /* k_vis -> k_mv_primary: occlusion ballots, word (i >> 6) * G + slot */
-    uint4 *vreq_w[2];     /* groups > 16 views (G = 0 instances): the lane's visibility-request mask (mstore) */
-    uint4 *lmask_w[6];    /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (two planes each) */
+    uint4 *vreq_w[8];     /* groups > 16 views (G <= 0 instances): the lane's visibility-request mask (mstore) */
+    uint4 *lmask_w[24];   /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (mask_planes<G>() each) */
     float *vstate;        /* runtime groups whose per-view state exceeds LDS: VS_FIELDS x G x vs_stride floats */
 };
 
@@ -2140,48 +2140,64 @@ AD PrimRay primary_raygen(const KParams &P, const DView *V, uint32_t i) {
     return r;
 }
 /*
- * Group sizes.  G = 2..16 are compile-time instances; G = 0 is the runtime instance for groups
- * of 17..256 views (KParams::G): 256-bit per-view masks (WMask) kept in their own planes (vreq_w,
- * lmask_w), 64-thread primary blocks with the per-view state in LDS while it fits in 64 KB and in
- * a global plane per chunk beyond (Bufs::vstate), k_vis waves that walk several slots.
+ * Group sizes.  G = 2..16 are compile-time instances; G = 0 and G = -1 are the runtime instances for
+ * groups of 17..256 and 257..1024 views (KParams::G): 256- / 1024-bit per-view masks (WMask<4>,
+ * WMask<16>) kept in their own planes (vreq_w, lmask_w), 64-thread primary blocks with the per-view
+ * state in LDS while it fits in 64 KB and in a global plane per chunk beyond (Bufs::vstate), k_vis waves
+ * that walk several slots.  The reference has no cap (mvpath.cpp:192-217); groups beyond 1024 views
+ * (over a million MIS pair terms per lane) are refused.
  */
-constexpr uint32_t kMaxGWide = 256;
-template <int G> AD int group_size(const KParams &P) { return G ? G : (int) P.G; }
-/* per-view bit masks: 32 bits for G <= 16 (bits 16+ carry other fields), four 64-bit words for the
- * runtime instance (17..256 views), indexed with a wave-uniform view slot k */
-struct WMask {
-    unsigned long long w[4];
-    AD WMask(uint32_t v = 0u) : w{v, 0ull, 0ull, 0ull} {}
+constexpr uint32_t kMaxGWide = 256, kMaxGHuge = 1024;
+template <int G> AD int group_size(const KParams &P) { return G > 0 ? G : (int) P.G; }
+/* per-view bit masks: 32 bits for G <= 16 (bits 16+ carry other fields), NW 64-bit words for the
+ * runtime instances, indexed with a wave-uniform view slot k */
+template <int NW> struct WMask {
+    unsigned long long w[NW];
+    AD WMask(uint32_t v = 0u) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) w[q] = q ? 0ull : (unsigned long long) v;
+    }
 };
-template <int G> using VMask = typename std::conditional<G == 0, WMask, uint32_t>::type;
+template <int G> constexpr int mask_words() { return G == 0 ? 4 : 16; }
+template <int G> using VMask = typename std::conditional<(G > 0), uint32_t, WMask<mask_words<G>()>>::type;
+/* uint4 planes per runtime-instance mask (two 64-bit words each) */
+template <int G> constexpr int mask_planes() { return G > 0 ? 0 : mask_words<G>() / 2; }
+constexpr int kMaxMaskPlanes = 8;
 AD bool mget(uint32_t m, int k) { return (m >> k) & 1u; }
-AD bool mget(const WMask &m, int k) {
-    const unsigned long long x = k < 128 ? (k < 64 ? m.w[0] : m.w[1]) : (k < 192 ? m.w[2] : m.w[3]);
+template <int NW> AD bool mget(const WMask<NW> &m, int k) {
+    unsigned long long x = 0ull;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) x = (k >> 6) == q ? m.w[q] : x;
     return (x >> (k & 63)) & 1ull;
 }
 AD void mset(uint32_t &m, int k, bool b) { m |= b ? 1u << k : 0u; }
-AD void mset(WMask &m, int k, bool b) {
+template <int NW> AD void mset(WMask<NW> &m, int k, bool b) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) m.w[q] |= (b && (k >> 6) == q) ? 1ull << (k & 63) : 0ull;
+    for (int q = 0; q < NW; ++q) m.w[q] |= (b && (k >> 6) == q) ? 1ull << (k & 63) : 0ull;
 }
 AD void mclr(uint32_t &m, int k) { m &= ~(1u << k); }
-/* a compile-time group's mask in bits 16..31 of a record word (0 for the runtime instance) */
+/* a compile-time group's mask in bits 16..31 of a record word (0 for the runtime instances) */
 AD uint32_t mlow16(uint32_t m) { return m << 16; }
-AD uint32_t mlow16(const WMask &) { return 0u; }
-AD void mclr(WMask &m, int k) {
+template <int NW> AD uint32_t mlow16(const WMask<NW> &) { return 0u; }
+template <int NW> AD void mclr(WMask<NW> &m, int k) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) m.w[q] &= (k >> 6) == q ? ~(1ull << (k & 63)) : ~0ull;
+    for (int q = 0; q < NW; ++q) m.w[q] &= (k >> 6) == q ? ~(1ull << (k & 63)) : ~0ull;
 }
-/* a runtime-instance mask through two uint4 planes (words 0-1, 2-3) */
-AD void mstore(uint4 *const *pl, uint32_t slot, const WMask &m) {
-    pl[0][slot] = make_uint4((uint32_t) m.w[0], (uint32_t) (m.w[0] >> 32), (uint32_t) m.w[1], (uint32_t) (m.w[1] >> 32));
-    pl[1][slot] = make_uint4((uint32_t) m.w[2], (uint32_t) (m.w[2] >> 32), (uint32_t) m.w[3], (uint32_t) (m.w[3] >> 32));
+/* a runtime-instance mask through NW / 2 uint4 planes (words 2j, 2j + 1 in plane j) */
+template <int NW> AD void mstore(uint4 *const *pl, uint32_t slot, const WMask<NW> &m) {
+#pragma unroll
+    for (int j = 0; j < NW / 2; ++j)
+        pl[j][slot] = make_uint4((uint32_t) m.w[2 * j], (uint32_t) (m.w[2 * j] >> 32), (uint32_t) m.w[2 * j + 1],
+                                 (uint32_t) (m.w[2 * j + 1] >> 32));
 }
-AD WMask mload(const uint4 *const *pl, uint32_t slot) {
-    const uint4 a = pl[0][slot], b = pl[1][slot];
-    WMask m;
-    m.w[0] = ((unsigned long long) a.y << 32) | a.x; m.w[1] = ((unsigned long long) a.w << 32) | a.z;
-    m.w[2] = ((unsigned long long) b.y << 32) | b.x; m.w[3] = ((unsigned long long) b.w << 32) | b.z;
+template <int NW> AD WMask<NW> mload(const uint4 *const *pl, uint32_t slot) {
+    WMask<NW> m;
+#pragma unroll
+    for (int j = 0; j < NW / 2; ++j) {
+        const uint4 a = pl[j][slot];
+        m.w[2 * j] = ((unsigned long long) a.y << 32) | a.x;
+        m.w[2 * j + 1] = ((unsigned long long) a.w << 32) | a.z;
+    }
     return m;
 }
 /* view index of group slot k of a lane whose primary view is p_idx (mvpath_multi.h:31-38) */
@@ -2252,7 +2268,7 @@ AD void prim_requests(const KParams &P, const SceneRef &sc, const DScene &S, con
         p = si.p; n = si.n; dsp = ds.p;
     }
     uint32_t w0 = 0;
-    if constexpr (G == 0) {
+    if constexpr (G <= 0) {
         mstore(B.vreq_w, i, bits);
         w0 = pr.p_idx;   /* the runtime instance keeps the primary view in the first plane */
     } else {
@@ -2302,8 +2318,8 @@ __global__ void __launch_bounds__(256) k_prim_hit_req(KParams P, const DScene *S
 #ifndef AMVPT_VIS_PAIRS
 #define AMVPT_VIS_PAIRS 1
 #endif
-template <int G> constexpr int vis_waves() { return G ? G : 16; }
-template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS && kUni && G != 0; }
+template <int G> constexpr int vis_waves() { return G > 0 ? G : 16; }
+template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS && kUni && G > 0; }
 /* waves per SIMD the paired walk's register allocation must allow (0: no bound).  Measured at
  * config M (r02ac): unbounded 96 VGPRs / 5 waves 69.3 ms, 6 waves (80 VGPRs, 12 B scratch)
  * 63.5 ms, 8 waves (64 VGPRs, 52 B scratch) 74.1 ms; one ray per lane, 8 waves: 72.3 ms */
@@ -2352,8 +2368,8 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
     uint32_t p_idx = 0;
     if (i < P.chunk_n) {
         a = B.vreq[0][i];
-        if constexpr (G == 0) {
-            bits = mload(B.vreq_w, i);
+        if constexpr (G <= 0) {
+            bits = mload<mask_words<G>()>(B.vreq_w, i);
             p_idx = fbits(a.w);
         } else {
             bits = fbits(a.w);
@@ -2362,7 +2378,7 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
     }
     /* G > 0: exactly one slot per wave (block = 64 x G threads), a straight-line body */
 #pragma unroll 1
-    for (int k = (int) (threadIdx.x >> 6); G ? true : k < Gn; k += vis_waves<G>()) {
+    for (int k = (int) (threadIdx.x >> 6); G > 0 ? true : k < Gn; k += vis_waves<G>()) {
         bool occ = false;
         if (i < P.chunk_n && mget(bits, k)) {
             nn = B.vreq[1][i]; d = B.vreq[2][i];
@@ -2371,7 +2387,7 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
         }
         const unsigned long long m = __ballot(occ);
         if ((threadIdx.x & 63u) == 0u) B.occ[(size_t) blockIdx.x * Gn + (uint32_t) k] = m;
-        if (G) break;
+        if (G > 0) break;
     }
 }
 
@@ -2495,7 +2511,7 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * own (cosine_hemisphere(rand_2) whatever wi), so the per-view state reduces to F_PDF,
  * F_JP and one sign bit per view -- same values, a third of the LDS per thread.
  */
-template <int G> constexpr int prim_block() { return G ? kPrimBlock : 64; }   /* G = 0: LDS state grows with G */
+template <int G> constexpr int prim_block() { return G > 0 ? kPrimBlock : 64; }   /* G <= 0: LDS state grows with G */
 /*
  * The per-lane body of k_mv_primary.  kDiff: the all-diffuse computation (see below); kGenRec (with
  * kDiff): a wave of a mixed scene's generic stage whose primary hits are all plain `diffuse` runs the
@@ -2888,10 +2904,11 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
         B.lrec[0][slot] = make_float4(R0.r, R0.g, R0.b, pdfW);
         B.lrec[1][slot] = make_float4(Dp.r, Dp.g, Dp.b, bitsf(lflags));
         B.lrec[2][slot] = make_float4(Bv.r, Bv.g, Bv.b, bitsf(mlow16(vmask) >> 16 | mlow16(imask)));
-        if constexpr (G == 0) {   /* planes: valid (0-1), indirect (2-3), wi.z > 0 (4-5) */
+        if constexpr (G <= 0) {   /* planes: valid, indirect, wi.z > 0 (mask_planes<G>() each) */
+            constexpr int NP = mask_planes<G>();
             mstore(B.lmask_w, slot, vmask);
-            mstore(B.lmask_w + 2, slot, imask);
-            mstore(B.lmask_w + 4, slot, smask);
+            mstore(B.lmask_w + NP, slot, imask);
+            mstore(B.lmask_w + 2 * NP, slot, smask);
         }
         B.lrec[3][slot] = make_float4(hp.x, hp.y, hp.z, 0.f);
         /* slot 0 (generic: its bsdf value rides in L2), and the views the MIS loop did not write */
@@ -2937,7 +2954,7 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
     SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
     /* per-view state: field f of view slot k of this thread at vs[(f * G + k) * kPB] */
     /* (runtime groups too large for LDS: the chunk's global per-view state, field-major, slot-minor) */
-    const bool vs_glob = G == 0 && B.vstate != nullptr;
+    const bool vs_glob = G <= 0 && B.vstate != nullptr;
     const uint32_t vs_stride = vs_glob ? P.vs_stride : (uint32_t) kPB;
     float *const vs = vs_glob ? B.vstate + (blockIdx.x * blockDim.x + threadIdx.x)
                               : reinterpret_cast<float *>(lds + vs_off) + threadIdx.x;
@@ -3006,8 +3023,9 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     const int Gn = group_size<G>(P);
     const uint32_t lflags = fbits(l1.w);
     VMask<G> vmask = 0u, imask = 0u, smask = 0u;
-    if constexpr (G == 0) {
-        if (ok) { vmask = mload(B.lmask_w, slot); imask = mload(B.lmask_w + 2, slot); smask = mload(B.lmask_w + 4, slot); }
+    if constexpr (G <= 0) {
+        constexpr int NP = mask_planes<G>(), NW = mask_words<G>();
+        if (ok) { vmask = mload<NW>(B.lmask_w, slot); imask = mload<NW>(B.lmask_w + NP, slot); smask = mload<NW>(B.lmask_w + 2 * NP, slot); }
     } else {
         vmask = fbits(l2.w) & 0xffffu; imask = fbits(l2.w) >> 16; smask = lflags >> 16;
     }
@@ -3252,7 +3270,7 @@ void launch_prim_hit(bool uni, dim3 grid, size_t lds_bvh, hipStream_t st, const 
 ;
 #endif
 #ifdef AMVPT_GROUP_TU
-template <int G> inline int group_size_host(const KParams &P) { return G ? G : (int) P.G; }
+template <int G> inline int group_size_host(const KParams &P) { return G > 0 ? G : (int) P.G; }
 /* the primary wavefronts of one chunk: k_prim_hit -> k_prim_req -> k_vis -> k_mv_primary */
 template <int G>
 void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st, const KParams &P,
@@ -3503,17 +3521,18 @@ typedef void (*primary_fn)(uint32_t, size_t, size_t, hipStream_t, const KParams 
 typedef void (*splat_fn)(dim3, hipStream_t, const KParams &, const DView *, const Bufs &, bool);
 /* group sizes 2..16: the per-view bit masks (k_prim_req's request bits below the view index at
  * bit 16, k_mv_primary's valid / indirect flags at bits k and 16 + k) hold 16 views; entry 0 is
- * the runtime instance for 17..256 views (256-bit masks in vreq_w / lmask_w) */
-static const primary_fn kPrimary[] = {launch_primary<0>, nullptr, launch_primary<2>, launch_primary<3>, launch_primary<4>,
+ * the runtime instance for 17..256 views (256-bit masks in vreq_w / lmask_w), entry 1 the one for
+ * 257..1024 views (1024-bit masks) */
+static const primary_fn kPrimary[] = {launch_primary<0>, launch_primary<-1>, launch_primary<2>, launch_primary<3>, launch_primary<4>,
                                       launch_primary<5>, launch_primary<6>, launch_primary<7>, launch_primary<8>,
                                       launch_primary<9>, launch_primary<10>, launch_primary<11>, launch_primary<12>,
                                       launch_primary<13>, launch_primary<14>, launch_primary<15>, launch_primary<16>};
-static const splat_fn kSplat[] = {launch_splat<0>, nullptr, launch_splat<2>, launch_splat<3>, launch_splat<4>,
+static const splat_fn kSplat[] = {launch_splat<0>, launch_splat<-1>, launch_splat<2>, launch_splat<3>, launch_splat<4>,
                                   launch_splat<5>, launch_splat<6>, launch_splat<7>, launch_splat<8>,
                                   launch_splat<9>, launch_splat<10>, launch_splat<11>, launch_splat<12>,
                                   launch_splat<13>, launch_splat<14>, launch_splat<15>, launch_splat<16>};
 constexpr uint32_t kMaxG = 16;
-static uint32_t dispatch_g(uint32_t G) { return G > kMaxG ? 0u : G; }
+static uint32_t dispatch_g(uint32_t G) { return G > kMaxGWide ? 1u : G > kMaxG ? 0u : G; }
 constexpr uint64_t kSelectChunk = 1ull << 30;
 
 /* adaptive fill: flagged lanes of each run of a rectangular lane set (one block per run) */
@@ -3563,7 +3582,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool is_mv = Pp.integrator == AMVPT_INTEGRATOR_MVPATH;
     const bool reuse = is_mv && Pp.sa_reuse && Pp.n_views > 1 && Pp.reuse_count != 1;
     const uint32_t G = reuse ? group_size(Pp) : 1;
-    if (G > kMaxGWide) { set_error("amvpt_render: group size > 256 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
+    if (G > kMaxGHuge) { set_error("amvpt_render: group size > 1024 not implemented"); return AMVPT_ERR_UNSUPPORTED; }
     const uint32_t n_adapt = reuse ? std::min(Pp.adaptive, G - 1) : 0;
     if (!is_mv && Pp.spp_pass_lim && (Pp.spp ? Pp.spp : 1) % std::min(Pp.spp_pass_lim, Pp.spp ? Pp.spp : 1u)) {
         set_error("sample_count (" + std::to_string(Pp.spp ? Pp.spp : 1) + ") must be a multiple of spp_per_pass (" +
@@ -3687,6 +3706,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.fx0 = fwin.x0; P.fy0 = fwin.y0; P.fw = fwin.width; P.fh = fwin.height;
     P.overflow = whole_film ? nullptr : fwin.overflow;
     P.ov_cap = whole_film ? 0 : fwin.overflow_capacity;
+    /* the list's count before this render: renders append (amvpt_film_window), film_overflow reports the
+     * cells this one added */
+    uint64_t overflow_before = 0, overflow_added = 0;
+    if (P.overflow) {
+        HIPCHK(hipMemcpyAsync(&overflow_before, P.overflow, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     P.valid_ray0 = (!Pp.hide_emitters && scene->dev.environment >= 0) ? 1u : 0u;
     if (!P.box) gaussian_coeffs(Pp.rfilter_stddev, P.filt);
     /* row-reduced splat (row_put): RGBW film, Gaussian filter, >= 16 samples per pixel and pass
@@ -3727,7 +3753,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
 
     /* lane arena: queues (2 x 5 x 16 B), lane_out + hit (32 B), NEE queue (52 B), visibility requests
      * (48 B), lane records (64 B), view records (4 B x G all-diffuse, else 32 B x G), ballots (G / 8 B) */
-    const bool wide = G > kMaxG;   /* the runtime group-size instance (256-bit view masks) */
+    const bool wide = G > kMaxG;   /* the runtime group-size instances (256- / 1024-bit view masks) */
+    const int mplanes = G > kMaxGWide ? mask_planes<-1>() : mask_planes<0>();   /* uint4 planes per mask */
     const bool diff_rec = scene->all_diffuse && diffuse_spec && !wide;   /* kDiff instances, compact view records */
     /* the runtime instance's per-view state: LDS (64-thread blocks) while it fits, else a global
      * VS_FIELDS x G float plane per lane */
@@ -3735,7 +3762,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                                      ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;
     const bool vs_global = wide && lds_tab_views + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 65536;
     const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G + (G + 7) / 8 +
-                            (wide ? 128 : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
+                            (wide ? (size_t) 4 * 16 * mplanes : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
     if (chunk_max == 0) {
         chunk_max = 1ull << 26;
@@ -3883,8 +3910,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.qcap = qcap;
         B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G * chunk);
         if (wide) {
-            for (int k = 0; k < 2; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
-            for (int k = 0; k < 6; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
+            for (int k = 0; k < mplanes; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
+            for (int k = 0; k < 3 * mplanes; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
             if (vs_global) B.vstate = (float *) carve((size_t) VS_FIELDS * 4 * G * chunk);
         }
         B.film = film;
@@ -4138,6 +4165,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         /* the caller sums the list; a list that ran out of room lost cells: fail loudly */
         HIPCHK(hipMemcpyAsync(&overflow_cells, P.overflow, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        overflow_added = overflow_cells - std::min(overflow_cells, overflow_before);
         if (overflow_cells > P.ov_cap) {
             set_error("amvpt_render: film overflow list full (" + std::to_string(overflow_cells) + " cells > capacity " +
                       std::to_string(P.ov_cap) + "): widen the film window or the list");
@@ -4166,7 +4194,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.nonfinite_samples = hs[6];
         c.negative_samples = hs[7];
         c.pushed_paths = hs[8];
-        c.film_overflow = overflow_cells;
+        c.film_overflow = overflow_added;   /* this render's cells (renders append to the list) */
         T.flush();
         HIPCHK(T.err);
         for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }

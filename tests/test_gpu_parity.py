@@ -437,11 +437,12 @@ def test_large_view_groups(gpu_ready, amvpt_mod, oracle, gx, gy, reuse):
     ("cbox_grid.xml", 16, 8, 128, 6),   # 128 views: masks beyond one 64-bit word
     ("cbox_grid.xml", 16, 16, 256, 4),  # 256 views: the largest group (four mask words)
     ("veach_grid.xml", 10, 8, 80, 6),   # glossy, 80 views, global per-view state
-], ids=["cbox_g32", "cbox_g64", "veach_g20", "cbox_g128", "cbox_g256", "veach_g80"])
+    ("cbox_grid.xml", 32, 16, 512, 2),  # 512 views: the 1024-bit instance (G = -1), a 32 x 16 light field
+], ids=["cbox_g32", "cbox_g64", "veach_g20", "cbox_g128", "cbox_g256", "veach_g80", "cbox_g512"])
 def test_groups_above_16_views(gpu_ready, amvpt_mod, oracle, scene, gx, gy, reuse, res):
-    """Groups of 17..256 views (the reference has no cap,
-    mvpath.cpp:192-217): the runtime group-size instance with 256-bit view masks (WMask in the
-    vreq_w / lmask_w planes), 16-wave k_vis blocks walking several slots each, 64-thread
+    """Groups of 17..1024 views (the reference has no cap,
+    mvpath.cpp:192-217): the runtime group-size instances with 256- / 1024-bit view masks (WMask<4>,
+    WMask<16> in the vreq_w / lmask_w planes), 16-wave k_vis blocks walking several slots each, 64-thread
     k_mv_primary blocks whose per-view state leaves LDS for a global plane past 64 KB."""
     s = amvpt_mod.load_file(os.path.join(SCENES, scene), res=res, spp=16, gx=gx, gy=gy, reuse=reuse)
     sd, vd, p = s.describe(0, 0, 0)
@@ -449,14 +450,15 @@ def test_groups_above_16_views(gpu_ready, amvpt_mod, oracle, scene, gx, gy, reus
     _check(amvpt_mod, oracle, s)
 
 
-def test_group_above_256_views_refused(gpu_ready, amvpt_mod):
-    """Groups past 256 views (four mask words) fail loudly instead of rendering wrong."""
+def test_group_above_1024_views_refused(gpu_ready, amvpt_mod):
+    """Groups past 1024 views (sixteen mask words; over a million MIS pair terms per lane) fail loudly
+    instead of rendering wrong."""
     torch = _torch()
-    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=2, spp=16, gx=20, gy=16, reuse=320)
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=1, spp=16, gx=33, gy=32, reuse=1056)
     sd, vd, p = s.describe(0, 0, 0)
     dev = amvpt_mod.DeviceScene(sd)
     film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
-    with pytest.raises(Exception, match="256"):
+    with pytest.raises(Exception, match="1024"):
         dev.render(vd, p, film.data_ptr())
 
 
