@@ -1986,8 +1986,13 @@ template <int kMask> struct LdsPark {
 template <int kMask> constexpr uint32_t park_lds_bytes() { return kMask ? park_fields(kMask) * 4u * kFusedBlock : 0u; }
 constexpr uint32_t kFusedParkBytes = park_lds_bytes<AMVPT_FUSED_PARK>();
 
+#ifndef AMVPT_FUSED_WAVES_GLOSSY
+/* the instance with microfacet BSDFs (kDiff = false): its own register budget (A/B 5 vs 6) */
+#define AMVPT_FUSED_WAVES_GLOSSY AMVPT_FUSED_WAVES
+#endif
 template <bool kTab, bool kDiff, int kW>
-__global__ void __launch_bounds__(kFusedBlock, AMVPT_FUSED_WAVES) k_suffix_fused(KParams P, const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(kFusedBlock, kDiff ? AMVPT_FUSED_WAVES : AMVPT_FUSED_WAVES_GLOSSY)
+    k_suffix_fused(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int kPk = AMVPT_FUSED_PARK;
     /* the parked state sits in front of the staged tables (dynamic LDS: [park][tables]) */
