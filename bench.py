@@ -91,6 +91,9 @@ def main():
                     help="multi-GPU partition of the frame (auto: view groups when they divide among the ranks)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="every chunk on the render stream in the timed frames too (kernel-trace profiles: "
+                         "per-kernel durations that do not overlap; the default keeps the second chunk stream)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     for k in ("res", "spp", "gx", "gy", "reuse", "adaptive"):
@@ -130,6 +133,7 @@ def main():
         # pass sharding: this rank's passes are [rank*n_passes, (rank+1)*n_passes) of a world*spp frame
         p = adist.pass_shard(p, rank, world, plan)
     dev = amvpt.DeviceScene(sd)
+    base_flags = amvpt.OPT_ONE_STREAM if args.one_stream else 0
     C = 5 if p.film_alpha else 4
     stream = torch.cuda.current_stream().cuda_stream
     quilt_bytes = p.film_width * p.film_height * C * 4
@@ -153,7 +157,7 @@ def main():
             overflow[:4].zero_()
             c = dev.render_ex(vd, p, film.data_ptr(), lanes=lanes, window=win, overflow_ptr=overflow.data_ptr(),
                               overflow_capacity=ov_cap, stream=stream, counters=counters, exchange=exchange,
-                              flags=flags)
+                              flags=flags | base_flags)
             adist.gather_windows(film, win, overflow, quilt, [g[1] for g in groups], dst=0)
             return c
     else:
@@ -172,7 +176,7 @@ def main():
             film.zero_()
             c = dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt.LaneSet(band[0], band[1], 0, 0, 0, 0),
                               stream=stream, counters=counters, exchange=exchange if world > 1 else None,
-                              flags=flags)
+                              flags=flags | base_flags)
             adist.reduce_film(film, dst=0)
             return c
 
@@ -276,6 +280,7 @@ def main():
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "strong" if lane_sharded else "weak",
+            "chunk_streams": 1 if args.one_stream else "auto (2 for the per-depth wavefront suffix of BVH scenes)",
             "rmse_vs_oracle": rmse,
             "vs_baseline": None,
             "dtype": "f32",
