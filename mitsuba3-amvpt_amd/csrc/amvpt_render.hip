@@ -3035,8 +3035,6 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
         vmask = fbits(l2.w) & 0xffffu; imask = fbits(l2.w) >> 16; smask = lflags >> 16;
     }
     const float qnan = __builtin_nanf("");
-    /* cfma(0, emis_mis, 0) of a valid view whose wi.z <= 0 (kDiff, see k_mv_primary) */
-    const C3 Dn = {(lflags & 0x100u) ? qnan : 0.f, (lflags & 0x200u) ? qnan : 0.f, (lflags & 0x400u) ? qnan : 0.f};
     const float pdfW = l0.w;
     const C3 R0 = C3{l0.x, l0.y, l0.z}, Dp = C3{l1.x, l1.y, l1.z}, Bv = C3{l2.x, l2.y, l2.z};
     const f3 hp = mk(l3.x, l3.y, l3.z);
@@ -3101,6 +3099,12 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
                 weight = vw[o];
                 valid = mget(vmask, k);
                 if (mis) {
+                    /* cfma(0, emis_mis, 0) of a valid view whose wi.z <= 0 (kDiff, see k_mv_primary): three
+                     * selects per view from the lane flags instead of three registers held across the view
+                     * loop (the 5-wave allocation spilled them; the asm keeps the compiler from hoisting them) */
+                    uint32_t lf = lflags;
+                    asm volatile("" : "+v"(lf));
+                    const C3 Dn = {(lf & 0x100u) ? qnan : 0.f, (lf & 0x200u) ? qnan : 0.f, (lf & 0x400u) ? qnan : 0.f};
                     result = k == 0 ? R0 : csel(direct && valid, csel(mget(smask, k), Dp, Dn), c3(0.f));
                     if (mget(imask, k)) result = cfma(Bv * pdfW, indirect, result);
                 } else {
