@@ -45,7 +45,7 @@ def _bit_equal(a, b):
     return (a == b) | (np.isnan(a) & np.isnan(b))
 
 
-def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0, flags=0, record_pass=0):
+def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0, flags=0, record_pass=0, film_tol=1e-5):
     sd, vd, p = scene.describe(0, seed, spp)
     plan = oracle.plan(p)
     gfilm, grec = _gpu_render(amvpt_mod, sd, vd, p, plan, flags=flags, record_pass=record_pass)
@@ -59,7 +59,7 @@ def _check(amvpt_mod, oracle, scene, seed=0, spp=0, min_match=1.0, flags=0, reco
     assert match >= min_match, "lane records: %.6f bit-identical" % match
     scale = np.abs(ofilm).max()
     err = np.abs(gfilm - ofilm).max() / scale
-    assert err < 1e-5, "film max relative difference %.3e" % err
+    assert err < film_tol, "film max relative difference %.3e" % err
     return gfilm, ofilm
 
 
@@ -447,7 +447,11 @@ def test_groups_above_16_views(gpu_ready, amvpt_mod, oracle, scene, gx, gy, reus
     s = amvpt_mod.load_file(os.path.join(SCENES, scene), res=res, spp=16, gx=gx, gy=gy, reuse=reuse)
     sd, vd, p = s.describe(0, 0, 0)
     assert oracle.plan(p)["group"] == reuse
-    _check(amvpt_mod, oracle, s)
+    # film tolerance: the records are bit-identical; the film sums differ only in order.  At 512 views of
+    # 2 x 2 px every film cell sums ~8192 splats (512 x 4 x 16 lanes into 4 cells per view), whose f32 sum
+    # order alone moves a cell by up to 8192 x 2^-24 = 4.9e-4 relative; 1e-4 (measured 2.3e-5, r04a) keeps
+    # the check well inside that bound.  The smaller groups sum <= 4096 per cell and keep 1e-5.
+    _check(amvpt_mod, oracle, s, film_tol=1e-4 if reuse > 256 else 1e-5)
 
 
 def test_group_above_1024_views_refused(gpu_ready, amvpt_mod):
