@@ -1680,7 +1680,10 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #define AMVPT_EXTEND_WAVES 6
 #endif
 #ifndef AMVPT_TREELETS
-#define AMVPT_TREELETS 1   /* the any-hit walks (k_vis, k_shadow) of large BVHs start in an LDS treelet (0: A/B) */
+/* walks of large BVHs that start in an LDS treelet: bit 0 k_shadow (per-lane any hit), bit 1 k_extend (per-lane
+ * closest hit, octant treelets), bit 2 k_vis (wave-uniform any hit; its scalar node loads already hit the
+ * scalar cache) */
+#define AMVPT_TREELETS 3
 #endif
 #ifndef AMVPT_SHADOW_WAVES
 #define AMVPT_SHADOW_WAVES 1
@@ -1689,7 +1692,7 @@ template <int kWalk>
 __global__ void __launch_bounds__(256, AMVPT_EXTEND_WAVES) k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false, true, false, AMVPT_TREELETS != 0>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, false, (AMVPT_TREELETS & 2) != 0>(S, lds, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
@@ -1710,7 +1713,7 @@ template <int kWalk>
 __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false, true, AMVPT_TREELETS != 0>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 1) != 0>(S, lds, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_nee[part * kCntStride], pbase = part * B.qcap;
     for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
@@ -2336,7 +2339,7 @@ template <int G, bool kUni>
 __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>())) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false, true, AMVPT_TREELETS != 0>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 4) != 0>(S, lds, P.trav_mode);
     const int Gn = group_size<G>(P);
     if constexpr (vis_pairs<G, kUni>()) {
         const int k = (int) (threadIdx.x >> 6);
@@ -3068,9 +3071,9 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     uint32_t splats = 0, fallback = 0, nonfinite = 0, negative = 0;   /* per lane, <= G each */
 #pragma unroll 1
     for (int k = 0; k < Gn; ++k) {
-        /* a view no lane of the wave splats into: no reprojection, no put (all-diffuse records carry
-         * the valid bits in the lane record; records / debug mode write every view's entry) */
-        if (AMVPT_SPLAT_SKIP && (kRow ? kd : kDiff) && k > 0 && !P.record && !P.debug) {
+        /* a view no lane of the wave splats into: no reprojection, no put (the lane record carries the
+         * valid bits of every view, both record formats; records / debug mode write every view's entry) */
+        if (AMVPT_SPLAT_SKIP && k > 0 && !P.record && !P.debug) {
             /* wave windows skip per wave; the block window's put has block barriers, so its skip must be
              * block-uniform (a wave skipping alone would pair its next barriers with the wrong view's) */
             const bool any = kRow ? wave_any(ok && mget(vmask, k)) : __syncthreads_or(ok && mget(vmask, k));
@@ -3111,13 +3114,18 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
                     result = res0;
                 }
             } else {
-                const float4 r = vR[o], bv = vB[o];
-                const uint32_t vf = fbits(bv.w);
+                /* the lane masks are the records' VF_VALID / VF_INDIRECT bits (k_mv_primary writes both from
+                 * the same vmask / imask): a view's (result, weight) is read only when it splats (or is
+                 * recorded), its BSDF value only when it adds the indirect term -- 32 B per view otherwise */
+                valid = mget(vmask, k);
+                const bool ind = mis && mget(imask, k);
+                float4 r = make_float4(0.f, 0.f, 0.f, 0.f), bv = r;
+                if (valid || P.record) r = vR[o];
+                if (ind) bv = vB[o];
                 weight = r.w;
-                valid = (vf & VF_VALID) != 0;
                 if (mis) {
                     result = C3{r.x, r.y, r.z};
-                    if (vf & VF_INDIRECT) result = cfma(C3{bv.x, bv.y, bv.z} * pdfW, indirect, result);
+                    if (ind) result = cfma(C3{bv.x, bv.y, bv.z} * pdfW, indirect, result);
                 } else {
                     result = res0;
                 }
@@ -3935,8 +3943,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const uint32_t fused_blocks = K.fused_blocks;
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
-    const size_t lds_any = lds_ext + (AMVPT_TREELETS ? tree_lds_bytes(scene->dev, trav) : 0u);     /* + any-hit treelet */
-    const size_t lds_close = lds_ext + (AMVPT_TREELETS ? oct_tree_lds_bytes(scene->dev, trav) : 0u); /* + octant treelets */
+    const size_t lds_any = lds_ext + ((AMVPT_TREELETS & 1) ? tree_lds_bytes(scene->dev, trav) : 0u);     /* k_shadow: + any-hit treelet */
+    const size_t lds_vis = lds_ext + ((AMVPT_TREELETS & 4) ? tree_lds_bytes(scene->dev, trav) : 0u);     /* k_vis */
+    const size_t lds_close = lds_ext + ((AMVPT_TREELETS & 2) ? oct_tree_lds_bytes(scene->dev, trav) : 0u); /* k_extend: + octant treelets */
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
     KTimer T;
     T.init(counters != nullptr);
@@ -4041,7 +4050,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                     hipLaunchKernelGGL(k_raygen_single, grid, dim3(256), 0, st, P, dviews, B);
                     T.end(st);
                 } else {
-                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_any, st, P, dS, dviews, B, tab_p, uni_coh, diff, T);
+                    kPrimary[dispatch_g(G)](cn, lds_prim, lds_vis, st, P, dS, dviews, B, tab_p, uni_coh, diff, T);
                 }
             }
             HIPCHK(hipGetLastError());

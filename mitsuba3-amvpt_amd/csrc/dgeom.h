@@ -186,6 +186,28 @@ template <typename T> AD T load_uniform(const T *base, uint32_t idx) {
 }
 AD bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
 
+/* Per-lane reads of 16-byte records through an explicit address space.  A treelet walk reads a node from
+ * its LDS treelet or from the global array, lane by lane; through the generic SceneRef pointers the two
+ * became one flat load (every node read paying the flat path, and flat loads count against both the
+ * vector-memory and the LDS wait counters).  load_lds takes a generic pointer into the block's LDS (its
+ * low 32 bits are the LDS offset), load_global a pointer into device memory. */
+template <typename T, int AS> AD T load_as(const T *base, uint32_t idx) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(AS))) const v4u av4u;
+    static_assert(sizeof(T) % 16 == 0, "16-byte records");
+    constexpr int W = (int) (sizeof(T) / 16);
+    const av4u *p;
+    if constexpr (AS == 3) p = (const av4u *) (uint32_t) (uintptr_t) base + idx * (uint32_t) W;
+    else p = (const av4u *) (uintptr_t) base + (size_t) idx * W;
+    T out;
+    v4u *o = reinterpret_cast<v4u *>(&out);
+#pragma unroll
+    for (int k = 0; k < W; ++k) o[k] = p[k];
+    return out;
+}
+template <typename T> AD T load_lds(const T *base, uint32_t idx) { return load_as<T, 3>(base, idx); }
+template <typename T> AD T load_global(const T *base, uint32_t idx) { return load_as<T, 1>(base, idx); }
+
 /* Primitive test with a wave-uniform primitive type (no divergence between shapes). */
 AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
     if (type == PRIM_RECT) return rect_hit(p, r, t, u, v);
@@ -223,7 +245,7 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
     auto leaf_test = [&](uint32_t first, uint32_t count) {
         for (uint32_t i = 0; i < count; ++i) {
             const uint32_t pi = first + i;
-            const DPrim p = sc.prims[pi];
+            const DPrim p = load_global(sc.gprims, pi);
             float t, u, v;
             if (prim_hit(p, ray, t, u, v)) {
                 if (t < best.t || (t == best.t && p.pad < best_orig)) {
@@ -244,7 +266,9 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
             const bool open = glob || node < nt;
             if (!wave_any(open && lc == 0u)) break;
             if (open && !stop) {
-                const DNode n = glob ? gn[node] : tn[node];
+                DNode n;
+                if (glob) n = load_global(gn, node);
+                else n = load_lds(tn, node);
                 if (glob && gend == kNoEnd) gend = n.skip_count & kNodeSkipMask;   /* the portal's own node */
                 const bool hit = box_hit(n, br, tmax_box);
                 const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
@@ -379,7 +403,7 @@ AD bool trace_any_tl(const SceneRef &sc, const Ray &ray) {
     auto leaf_any = [&](uint32_t first, uint32_t count) {
         bool f = false;
         for (uint32_t i = 0; i < count && !f; ++i) {
-            const DPrim p = sc.prims[first + i];
+            const DPrim p = load_global(sc.gprims, first + i);
             float t, u, v;
             f = prim_hit(p, ray, t, u, v);
         }
@@ -397,7 +421,9 @@ AD bool trace_any_tl(const SceneRef &sc, const Ray &ray) {
             const bool open = !found && (glob || node < nt);
             if (!wave_any(open && lc == 0u)) break;
             if (open && !stop) {
-                const DNode n = glob ? sc.gnodes[node] : sc.tnodes[node];
+                DNode n;
+                if (glob) n = load_global(sc.gnodes, node);
+                else n = load_lds(sc.tnodes, node);
                 if (glob && gend == kNoEnd) gend = n.skip_count & kNodeSkipMask;   /* the portal's own node */
                 const bool hit = box_hit(n, br, ray.maxt);
                 const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
@@ -437,7 +463,7 @@ AD void trace_any_uni_tl(const SceneRef &sc, const Ray &r0, bool act0, const Ray
         DNode n;
         if (!glob) {
             if (t >= nt) break;
-            n = sc.tnodes[t];
+            n = load_lds(sc.tnodes, t);
         } else {
             n = load_uniform(sc.gnodes, g);
             if (gend == kNoEnd) gend = ufirst(n.skip_count) & kNodeSkipMask;
@@ -519,7 +545,7 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
     auto leaf_any = [&](uint32_t first, uint32_t count) {
         bool f = false;
         for (uint32_t i = 0; i < count && !f; ++i) {
-            const DPrim p = sc.prims[first + i];
+            const DPrim p = load_global(sc.gprims, first + i);
             float t, u, v;
             f = prim_hit(p, ray, t, u, v);
         }
