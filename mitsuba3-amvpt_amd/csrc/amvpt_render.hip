@@ -1681,9 +1681,11 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #endif
 #ifndef AMVPT_TREELETS
 /* walks of large BVHs that start in an LDS treelet: bit 0 k_shadow (per-lane any hit), bit 1 k_extend (per-lane
- * closest hit, octant treelets), bit 2 k_vis (wave-uniform any hit; its scalar node loads already hit the
- * scalar cache) */
-#define AMVPT_TREELETS 3
+ * closest hit, octant treelets), bit 2 k_vis (wave-uniform any hit).  Off: measured slower on the mesh bench
+ * (r04c, one-stream kernel ms: k_extend 266 -> 320, k_shadow 191 -> 254, k_vis 80 -> 110; 717 -> 634 / 607
+ * Msamples/s) -- the top levels they stage are the nodes every walk already finds in L1 / the scalar cache,
+ * and a wave whose lanes are split between treelet and global nodes waits for both loads per step. */
+#define AMVPT_TREELETS 0
 #endif
 #ifndef AMVPT_SHADOW_WAVES
 #define AMVPT_SHADOW_WAVES 1
