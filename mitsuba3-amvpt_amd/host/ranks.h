@@ -117,7 +117,9 @@ struct Ranks {
         bar.arrived = 0;
         ex.reset(n);
         std::vector<std::string> err((size_t) n);
-        std::vector<bool> echo((size_t) n, false);   /* the error only reports a peer's failure */
+        /* the error only reports a peer's failure; one byte per rank (vector<bool> packs the ranks' flags into
+         * shared words, and the threads' concurrent writes lost each other's updates) */
+        std::vector<uint8_t> echo((size_t) n, 0);
         std::vector<std::thread> threads;
         for (int r = 0; r < n; ++r)
             threads.emplace_back([&, r] {
@@ -150,7 +152,7 @@ struct Ranks {
         for (auto &t : threads) t.join();
         for (int pass = 0; pass < 2; ++pass)   /* own failures first, then echoes */
             for (int r = 0; r < n; ++r)
-                if (!err[(size_t) r].empty() && echo[(size_t) r] == (pass == 1))
+                if (!err[(size_t) r].empty() && (echo[(size_t) r] != 0) == (pass == 1))
                     return "rank " + std::to_string(r) + ": " + err[(size_t) r];
         return "";
     }
