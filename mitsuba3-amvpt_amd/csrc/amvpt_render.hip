@@ -1992,8 +1992,10 @@ template <int kMask> constexpr uint32_t park_lds_bytes() { return kMask ? park_f
 constexpr uint32_t kFusedParkBytes = park_lds_bytes<AMVPT_FUSED_PARK>();
 
 #ifndef AMVPT_FUSED_WAVES_GLOSSY
-/* the instance with microfacet BSDFs (kDiff = false): its own register budget (A/B 5 vs 6) */
-#define AMVPT_FUSED_WAVES_GLOSSY AMVPT_FUSED_WAVES
+/* the instance with microfacet BSDFs (kDiff = false): its own register budget.  5 waves/SIMD (96 VGPRs, no
+ * scratch) and 6 (80 VGPRs, 44 B of scratch) run the C3 suffix in the same time (305.1 vs 303.9 ms, r04b);
+ * at 6 its PMC bytes are 1.54x the algorithmic ones (r04d_traffic_C3.json), so 5 */
+#define AMVPT_FUSED_WAVES_GLOSSY 5
 #endif
 template <bool kTab, bool kDiff, int kW>
 __global__ void __launch_bounds__(kFusedBlock, kDiff ? AMVPT_FUSED_WAVES : AMVPT_FUSED_WAVES_GLOSSY)

@@ -71,6 +71,82 @@ AD bool tri_hit(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
     return active && t >= 0.f && t <= r.maxt;
 }
 
+/*
+ * Packed intersection tests: two (primitive, ray) tests of one primitive type with their arithmetic in
+ * v_pk_* pairs -- two primitives against one ray (AMVPT_PAIR_PRIMS) or one primitive against two rays
+ * (AMVPT_PAIR_RAYS, the two visibility rays per lane of k_vis).  Element e performs exactly rect_hit's /
+ * tri_hit's IEEE operations in the same order (packed FMA, multiply, add and subtract are per-element IEEE;
+ * the divisions stay per element), so the hits, t, u and v are the same bits.
+ */
+typedef float f2v __attribute__((ext_vector_type(2)));
+AD f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+struct Hit2 { bool h[2]; float t[2], u[2], v[2]; };
+struct PrimPair { f2v a[4], b[4], c[4]; };
+struct RayPair { f2v ox, oy, oz, dx, dy, dz; float maxt[2]; };
+AD PrimPair prim_pair(const DPrim &p, const DPrim &q) {
+    PrimPair o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { o.a[k] = f2v{p.a[k], q.a[k]}; o.b[k] = f2v{p.b[k], q.b[k]}; o.c[k] = f2v{p.c[k], q.c[k]}; }
+    return o;
+}
+AD PrimPair prim_pair(const DPrim &p) {
+    PrimPair o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { o.a[k] = (f2v) p.a[k]; o.b[k] = (f2v) p.b[k]; o.c[k] = (f2v) p.c[k]; }
+    return o;
+}
+AD RayPair ray_pair(const Ray &r) {
+    return RayPair{(f2v) r.o.x, (f2v) r.o.y, (f2v) r.o.z, (f2v) r.d.x, (f2v) r.d.y, (f2v) r.d.z, {r.maxt, r.maxt}};
+}
+AD RayPair ray_pair(const Ray &r0, const Ray &r1) {
+    return RayPair{f2v{r0.o.x, r1.o.x}, f2v{r0.o.y, r1.o.y}, f2v{r0.o.z, r1.o.z},
+                   f2v{r0.d.x, r1.d.x}, f2v{r0.d.y, r1.d.y}, f2v{r0.d.z, r1.d.z}, {r0.maxt, r1.maxt}};
+}
+AD Hit2 rect_hit2(const PrimPair &P, const RayPair &R) {
+    const f2v lox = fma2(P.a[2], R.oz, fma2(P.a[1], R.oy, fma2(P.a[0], R.ox, P.a[3])));
+    const f2v loy = fma2(P.b[2], R.oz, fma2(P.b[1], R.oy, fma2(P.b[0], R.ox, P.b[3])));
+    const f2v loz = fma2(P.c[2], R.oz, fma2(P.c[1], R.oy, fma2(P.c[0], R.ox, P.c[3])));
+    const f2v ldx = fma2(P.a[2], R.dz, fma2(P.a[1], R.dy, P.a[0] * R.dx));
+    const f2v ldy = fma2(P.b[2], R.dz, fma2(P.b[1], R.dy, P.b[0] * R.dx));
+    const f2v ldz = fma2(P.c[2], R.dz, fma2(P.c[1], R.dy, P.c[0] * R.dx));
+    Hit2 o;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) o.t[e] = -loz[e] / ldz[e];
+    /* the local hit point (lx = fma(dx, t, ox) per element) */
+    const f2v tt = {o.t[0], o.t[1]};
+    const f2v lx = fma2(ldx, tt, lox), ly = fma2(ldy, tt, loy);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        o.u[e] = lx[e];
+        o.v[e] = ly[e];
+        o.h[e] = o.t[e] >= 0.f && o.t[e] <= R.maxt[e] && fabs_(lx[e]) <= 1.f && fabs_(ly[e]) <= 1.f;
+    }
+    return o;
+}
+AD Hit2 tri_hit2(const PrimPair &P, const RayPair &R) {
+    /* p0 = a, e1 = b, e2 = c; pvec = cross(d, e2) with fmsub(a, b, c) = fma(a, b, -c) */
+    const f2v pvx = fma2(R.dy, P.c[2], -(R.dz * P.c[1])), pvy = fma2(R.dz, P.c[0], -(R.dx * P.c[2])),
+              pvz = fma2(R.dx, P.c[1], -(R.dy * P.c[0]));
+    const f2v det = fma2(P.b[2], pvz, fma2(P.b[1], pvy, P.b[0] * pvx));
+    f2v inv;
+    inv[0] = 1.0f / det[0];
+    inv[1] = 1.0f / det[1];
+    const f2v tvx = R.ox - P.a[0], tvy = R.oy - P.a[1], tvz = R.oz - P.a[2];
+    const f2v u = fma2(tvz, pvz, fma2(tvy, pvy, tvx * pvx)) * inv;
+    const f2v qx = fma2(tvy, P.b[2], -(tvz * P.b[1])), qy = fma2(tvz, P.b[0], -(tvx * P.b[2])),
+              qz = fma2(tvx, P.b[1], -(tvy * P.b[0]));
+    const f2v v = fma2(R.dz, qz, fma2(R.dy, qy, R.dx * qx)) * inv;
+    const f2v t = fma2(P.c[2], qz, fma2(P.c[1], qy, P.c[0] * qx)) * inv;
+    const f2v uv = u + v;
+    Hit2 o;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        o.t[e] = t[e]; o.u[e] = u[e]; o.v[e] = v[e];
+        o.h[e] = u[e] >= 0.f && u[e] <= 1.f && v[e] >= 0.f && uv[e] <= 1.f && t[e] >= 0.f && t[e] <= R.maxt[e];
+    }
+    return o;
+}
+
 /* float64 sphere test, as the llvm variants compute it (sphere.cpp:460-518) */
 AD bool sphere_hit(const DPrim &p, const Ray &ray, float &t_out) {
     double cx = p.a[0], cy = p.a[1], cz = p.a[2], r = p.a[3];
@@ -594,9 +670,13 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
  * once per two rays.  Lanes without a ray pass act = false (they count as found).  Exact for the
  * same reason as trace_any: a primitive tested for a ray whose box test failed cannot hit it.
  */
+#ifndef AMVPT_PAIR_RAYS
+#define AMVPT_PAIR_RAYS 1   /* trace_any2_uni tests a primitive against both rays as one packed test (0: A/B) */
+#endif
 AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
     if (sc.t_n) { trace_any_uni_tl(sc, r0, act0, r1, act1, true, f0, f1); return; }
     const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
+    const RayPair R2 = ray_pair(r0, r1);
     const uint32_t nn = ufirst(sc.n_nodes);
     f0 = !act0; f1 = !act1;
     uint32_t node = 0;
@@ -610,6 +690,13 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
             for (uint32_t i = 0; i < count; ++i) {
                 const DPrim p = load_uniform(sc.gprims, first + i);
                 const uint32_t type = ufirst(p.type);
+                if (AMVPT_PAIR_RAYS && type != PRIM_SPHERE) {
+                    /* both rays against the primitive as one packed test */
+                    const Hit2 h = type == PRIM_RECT ? rect_hit2(prim_pair(p), R2) : tri_hit2(prim_pair(p), R2);
+                    f0 = f0 || h.h[0];
+                    f1 = f1 || h.h[1];
+                    continue;
+                }
                 float t, u, v;
                 const bool h0 = prim_hit_u(p, type, r0, t, u, v);
                 const bool h1 = prim_hit_u(p, type, r1, t, u, v);
@@ -655,6 +742,44 @@ template <bool kSph> AD void brute_test(const DPrim &p, uint32_t pi, const Ray &
         }
     }
 }
+#ifndef AMVPT_PAIR_PRIMS
+/* 1: the brute-force walks test two same-type primitives as one packed pair -- off: at the fused suffix's
+ * 80-VGPR budget the pairs spill (240 B of scratch, k_suffix_fused<true, true, 3>) */
+#define AMVPT_PAIR_PRIMS 0
+#endif
+/* the pair (a, b) = primitives (pi, pi + 1): one packed test when both are rectangles or both triangles */
+template <bool kSph> AD void brute_pair(const DPrim &a, const DPrim &b, uint32_t pi, const Ray &ray, Hit &best,
+                                        uint32_t &best_orig) {
+    const uint32_t ta = ufirst(a.type), tb = ufirst(b.type);
+    if (AMVPT_PAIR_PRIMS && ta == tb && ta != PRIM_SPHERE) {
+        Hit2 h;
+        if (ta == PRIM_RECT) h = rect_hit2(prim_pair(a, b), ray_pair(ray));
+        else h = tri_hit2(prim_pair(a, b), ray_pair(ray));
+        const uint32_t orig[2] = {ufirst(a.pad), ufirst(b.pad)};
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (h.h[e] && (h.t[e] < best.t || (h.t[e] == best.t && orig[e] < best_orig))) {
+                best.t = h.t[e]; best.u = h.u[e]; best.v = h.v[e]; best.prim = (int32_t) (pi + e);
+                best_orig = orig[e];
+            }
+    } else {
+        brute_test<kSph>(a, pi, ray, best, best_orig);
+        brute_test<kSph>(b, pi + 1, ray, best, best_orig);
+    }
+}
+template <bool kSph> AD bool brute_pair_any(const DPrim &a, const DPrim &b, const Ray &ray) {
+    const uint32_t ta = ufirst(a.type), tb = ufirst(b.type);
+    if (AMVPT_PAIR_PRIMS && ta == tb && ta != PRIM_SPHERE) {
+        Hit2 h;
+        if (ta == PRIM_RECT) h = rect_hit2(prim_pair(a, b), ray_pair(ray));
+        else h = tri_hit2(prim_pair(a, b), ray_pair(ray));
+        return h.h[0] || h.h[1];
+    }
+    float t, u, v;
+    const bool ha = prim_hit_b<kSph>(a, ta, ray, t, u, v);
+    const bool hb = prim_hit_b<kSph>(b, tb, ray, t, u, v);
+    return ha || hb;
+}
 /* Two records in flight (a, b), each reloaded in place right after its own test: the next
  * record's scalar load overlaps the current test and no record is copied between registers
  * (a one-record prefetch made the compiler move all 16 SGPRs of the record every iteration). */
@@ -667,6 +792,12 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     for (uint32_t pi = 0; pi < np; pi += 2) {
         /* unconditional reloads (index clamped to the table): a conditional one would merge two
          * values of the record and cost a register copy per primitive */
+        if (AMVPT_PAIR_PRIMS && pi + 1 < np) {
+            brute_pair<kSph>(a, b, pi, ray, best, best_orig);
+            a = load_uniform(sc.gprims, min(pi + 2u, last));
+            b = load_uniform(sc.gprims, min(pi + 3u, last));
+            continue;
+        }
         brute_test<kSph>(a, pi, ray, best, best_orig);
         a = load_uniform(sc.gprims, min(pi + 2u, last));
         if (pi + 1 < np) brute_test<kSph>(b, pi + 1, ray, best, best_orig);
@@ -683,15 +814,22 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
     DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
     for (uint32_t pi = 0; pi < np; pi += 2) {
         /* branch-free: every lane tests (the wave runs the test anyway while any lane is open) */
-        float t, u, v;
-        const bool ha = prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
-        found = found || ha;
-        a = load_uniform(sc.gprims, min(pi + 2u, last));
-        if (pi + 1 < np) {
-            const bool hb = prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
-            found = found || hb;
+        if (AMVPT_PAIR_PRIMS && pi + 1 < np) {
+            const bool hab = brute_pair_any<kSph>(a, b, ray);
+            found = found || hab;
+            a = load_uniform(sc.gprims, min(pi + 2u, last));
+            b = load_uniform(sc.gprims, min(pi + 3u, last));
+        } else {
+            float t, u, v;
+            const bool ha = prim_hit_b<kSph>(a, ufirst(a.type), ray, t, u, v);
+            found = found || ha;
+            a = load_uniform(sc.gprims, min(pi + 2u, last));
+            if (pi + 1 < np) {
+                const bool hb = prim_hit_b<kSph>(b, ufirst(b.type), ray, t, u, v);
+                found = found || hb;
+            }
+            b = load_uniform(sc.gprims, min(pi + 3u, last));
         }
-        b = load_uniform(sc.gprims, min(pi + 3u, last));
         if (!wave_any(!found)) break;
     }
     return found;
