@@ -147,8 +147,36 @@ AD Hit2 tri_hit2(const PrimPair &P, const RayPair &R) {
     return o;
 }
 
+/*
+ * f32 screen in front of the float64 sphere test (AMVPT_SPHERE_SCREEN): false only when the ray's line
+ * passes the sphere by a clear margin, where the exact test cannot hit.  The exact test hits only if its
+ * discriminant B^2 - 4AC >= 0, i.e. (up to f64 rounding, ~1e-16 relative) only if the line through pp (the
+ * f32 point o + d * plane_t) along d passes within r of the center; pp lies within eps <= 4u (|o| + |l|)
+ * (u = 2^-24, l = o - c) of the ray's own line, so a hit needs dist(c, line) <= r + eps.  Here dist^2 =
+ * |l|^2 - (l.d)^2 / |d|^2 in f32 (absolute error <~ 16u |l|^2) and the screen keeps the ray unless
+ * dist^2 > r^2 (1 + 1e-4) + 1e-5 (|l|^2 + |o|^2) -- a margin over 10x the error and eps terms.  A ray the
+ * screen drops would have returned no hit (t = inf), so the results are the same bits; NaN keeps the ray.
+ */
+#ifndef AMVPT_SPHERE_SCREEN
+#define AMVPT_SPHERE_SCREEN 1
+#endif
+AD bool sphere_maybe(const DPrim &p, const Ray &ray) {
+    const float lx = ray.o.x - p.a[0], ly = ray.o.y - p.a[1], lz = ray.o.z - p.a[2], r = p.a[3];
+    const float dd = fmadd(ray.d.z, ray.d.z, fmadd(ray.d.y, ray.d.y, ray.d.x * ray.d.x));
+    const float ld = fmadd(lz, ray.d.z, fmadd(ly, ray.d.y, lx * ray.d.x));
+    const float ll = fmadd(lz, lz, fmadd(ly, ly, lx * lx));
+    const float oo = fmadd(ray.o.z, ray.o.z, fmadd(ray.o.y, ray.o.y, ray.o.x * ray.o.x));
+    const float thr = fmadd(r * r, 1.0001f, 1e-5f * (ll + oo));
+    /* dist^2 > thr  <=>  dd * ll - ld^2 > dd * thr  (dd > 0) */
+    return !(fmadd(dd, ll, -(ld * ld)) > dd * thr);
+}
+
 /* float64 sphere test, as the llvm variants compute it (sphere.cpp:460-518) */
 AD bool sphere_hit(const DPrim &p, const Ray &ray, float &t_out) {
+    if (AMVPT_SPHERE_SCREEN && !sphere_maybe(p, ray)) {
+        t_out = kInf;
+        return false;
+    }
     double cx = p.a[0], cy = p.a[1], cz = p.a[2], r = p.a[3];
     double ox = ray.o.x, oy = ray.o.y, oz = ray.o.z, dx = ray.d.x, dy = ray.d.y, dz = ray.d.z;
     double maxt = ray.maxt;
@@ -671,7 +699,9 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
  * same reason as trace_any: a primitive tested for a ray whose box test failed cannot hit it.
  */
 #ifndef AMVPT_PAIR_RAYS
-#define AMVPT_PAIR_RAYS 1   /* trace_any2_uni tests a primitive against both rays as one packed test (0: A/B) */
+/* 1: trace_any2_uni tests a primitive against both rays as one packed test -- off: config-M k_vis 63.2 ->
+ * 79.0 ms, C3 232 -> 284 ms (r04e; 48 B of scratch and the pair moves outweigh the packed arithmetic) */
+#define AMVPT_PAIR_RAYS 0
 #endif
 AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
     if (sc.t_n) { trace_any_uni_tl(sc, r0, act0, r1, act1, true, f0, f1); return; }
