@@ -242,6 +242,7 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.t_n = 0;
     sc.onodes = nullptr;
     sc.o_n = 0;
+    sc.lds_bvh = false;
     sc.n_nodes = S.n_nodes;
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
@@ -258,6 +259,7 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
         for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) d4[i] = sn[i];
         for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) d4[nn + i] = spr[i];
         sc.nodes = (const DNode *) lds;
+        sc.lds_bvh = true;
         sc.oct_stride = 0;   /* only the first ordering is staged */
         sc.prims = (const DPrim *) (lds + (size_t) nn * 16);
         dst = lds + scene_lds_bytes(S, mode);

@@ -15,6 +15,7 @@
  * interaction.h:140-169.
  */
 #pragma once
+#include <type_traits>
 #include "dmath.h"
 #include "dscene.h"
 
@@ -37,6 +38,7 @@ struct SceneRef {
     uint32_t t_n;
     const DNode *onodes;      /* LDS treelets of the 8 octant orderings (stage_scene kOct), o_n nodes each; 0: none */
     uint32_t o_n;
+    bool lds_bvh;             /* nodes / prims are the block's LDS copy (stage_scene), else device memory */
 };
 
 
@@ -148,27 +150,44 @@ AD Hit2 tri_hit2(const PrimPair &P, const RayPair &R) {
 }
 
 /*
- * f32 screen in front of the float64 sphere test (AMVPT_SPHERE_SCREEN): false only when the ray's line
- * passes the sphere by a clear margin, where the exact test cannot hit.  The exact test hits only if its
- * discriminant B^2 - 4AC >= 0, i.e. (up to f64 rounding, ~1e-16 relative) only if the line through pp (the
- * f32 point o + d * plane_t) along d passes within r of the center; pp lies within eps <= 4u (|o| + |l|)
- * (u = 2^-24, l = o - c) of the ray's own line, so a hit needs dist(c, line) <= r + eps.  Here dist^2 =
- * |l|^2 - (l.d)^2 / |d|^2 in f32 (absolute error <~ 16u |l|^2) and the screen keeps the ray unless
- * dist^2 > r^2 (1 + 1e-4) + 1e-5 (|l|^2 + |o|^2) -- a margin over 10x the error and eps terms.  A ray the
- * screen drops would have returned no hit (t = inf), so the results are the same bits; NaN keeps the ray.
+ * f32 screen in front of the float64 sphere test (AMVPT_SPHERE_SCREEN): false only when the exact test
+ * cannot hit, so a dropped ray returns what the exact test would (no hit, t = inf) and the results are the
+ * same bits; NaN keeps the ray.
+ * Line: the exact test hits only if its discriminant B^2 - 4AC >= 0, i.e. (up to f64 rounding, ~1e-16
+ * relative) only if the line through pp (the f32 point o + d * plane_t) along d passes within r of the
+ * center; pp lies within eps <= 8u (|o| + |l|) of the ray's own line (u = 2^-24, l = o - c).  Here
+ * h^2 |d|^2 = |l x d|^2 -- the cross-product form, whose f32 error near h = r is <~ 8u |l| r |d|^2 (no
+ * cancellation of |l|^2 terms) -- and the ray is dropped only if h^2 > R2 = r^2 (1 + 1e-5) +
+ * 2e-5 r s + 4e-12 s^2 (s = sqrt(2 (|o|^2 + |l|^2)) >= |o| + |l|): over 10x the error and eps terms.
+ * Segment (AMVPT_SPHERE_SCREEN 2): the sphere of radius^2 R2 meets the line over the parameters tc -+ th
+ * (tc = -l.d / |d|^2, th = sqrt(R2 - h^2) / |d|), which contain the exact test's entry and exit parameters
+ * (plane_t + x0 / x1) up to errors below m = 2e-5 (|tc| + |l| / |d|); the ray is dropped when that range
+ * lies beyond [0, maxt] by m.  A shadow ray toward a point on a sphere light stops ShadowEpsilon ~ 9e-4 of
+ * its length short of it (spawn_ray_to), so the target light's own exact test is dropped too.
  */
 #ifndef AMVPT_SPHERE_SCREEN
-#define AMVPT_SPHERE_SCREEN 1
+#define AMVPT_SPHERE_SCREEN 2   /* 1: the line test only, 0: off (A/B) */
 #endif
 AD bool sphere_maybe(const DPrim &p, const Ray &ray) {
     const float lx = ray.o.x - p.a[0], ly = ray.o.y - p.a[1], lz = ray.o.z - p.a[2], r = p.a[3];
-    const float dd = fmadd(ray.d.z, ray.d.z, fmadd(ray.d.y, ray.d.y, ray.d.x * ray.d.x));
-    const float ld = fmadd(lz, ray.d.z, fmadd(ly, ray.d.y, lx * ray.d.x));
+    const f3 d = ray.d;
+    const float dd = fmadd(d.z, d.z, fmadd(d.y, d.y, d.x * d.x));
     const float ll = fmadd(lz, lz, fmadd(ly, ly, lx * lx));
     const float oo = fmadd(ray.o.z, ray.o.z, fmadd(ray.o.y, ray.o.y, ray.o.x * ray.o.x));
-    const float thr = fmadd(r * r, 1.0001f, 1e-5f * (ll + oo));
-    /* dist^2 > thr  <=>  dd * ll - ld^2 > dd * thr  (dd > 0) */
-    return !(fmadd(dd, ll, -(ld * ld)) > dd * thr);
+    const float cx = fmsub(ly, d.z, lz * d.y), cy = fmsub(lz, d.x, lx * d.z), cz = fmsub(lx, d.y, ly * d.x);
+    const float E = fmadd(cz, cz, fmadd(cy, cy, cx * cx));   /* h^2 |d|^2 */
+    const float sc = __builtin_amdgcn_sqrtf(2.f * (oo + ll));
+    const float R2 = fmadd(r * r, 1.00001f, fmadd(2e-5f * r, sc, 4e-12f * (sc * sc)));
+    if (E > dd * R2) return false;
+    if (AMVPT_SPHERE_SCREEN >= 2) {
+        const float ld = fmadd(lz, d.z, fmadd(ly, d.y, lx * d.x));
+        const float idd = __builtin_amdgcn_rcpf(dd);
+        const float tc = -ld * idd;
+        const float th = __builtin_amdgcn_sqrtf(fmaxf(fmadd(dd, R2, -E), 0.f)) * idd * 1.0001f;
+        const float m = 2e-5f * (fabs_(tc) + __builtin_amdgcn_sqrtf(ll * idd));
+        if (tc - th > ray.maxt + m || tc + th < -m) return false;
+    }
+    return true;
 }
 
 /* float64 sphere test, as the llvm variants compute it (sphere.cpp:460-518) */
@@ -310,6 +329,9 @@ template <typename T, int AS> AD T load_as(const T *base, uint32_t idx) {
     return out;
 }
 template <typename T> AD T load_lds(const T *base, uint32_t idx) { return load_as<T, 3>(base, idx); }
+#ifndef AMVPT_WALK_AS
+#define AMVPT_WALK_AS 1   /* per-lane walks read nodes / primitives through explicit address spaces (0: generic, A/B) */
+#endif
 template <typename T> AD T load_global(const T *base, uint32_t idx) { return load_as<T, 1>(base, idx); }
 
 /* Primitive test with a wave-uniform primitive type (no divergence between shapes). */
@@ -439,59 +461,69 @@ template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const
         return best;
     }
     const DNode *const nodes = octant_nodes(sc, ray.d);
-    auto leaf_test = [&](uint32_t first, uint32_t count) {
-        for (uint32_t i = 0; i < count; ++i) {
-            const uint32_t pi = first + i;
-            const DPrim p = sc.prims[pi];
-            float t, u, v;
-            if (prim_hit(p, ray, t, u, v)) {
-                if (t < best.t || (t == best.t && p.pad < best_orig)) {
-                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
-                    best_orig = p.pad;
-                    tmax_box = t;
+    /* kL: the BVH is staged in LDS (stage_scene), else it is read from device memory; explicit address
+     * spaces (not the generic SceneRef pointers, which made every node and primitive read a flat load) */
+    auto walk = [&](auto lds_tag) -> Hit {
+        constexpr bool kL = decltype(lds_tag)::value;
+        auto ld_node = [&](uint32_t i) {
+            if (!AMVPT_WALK_AS) return nodes[i];
+            return kL ? load_lds(nodes, i) : load_global(nodes, i);
+        };
+        auto leaf_test = [&](uint32_t first, uint32_t count) {
+            for (uint32_t i = 0; i < count; ++i) {
+                const uint32_t pi = first + i;
+                const DPrim p = !AMVPT_WALK_AS ? sc.prims[pi] : kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
+                float t, u, v;
+                if (prim_hit(p, ray, t, u, v)) {
+                    if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                        best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                        best_orig = p.pad;
+                        tmax_box = t;
+                    }
                 }
             }
-        }
-    };
-    const uint32_t nn = sc.n_nodes;
-    uint32_t node = 0;
-    if constexpr (kWW != 0) {
-    /* while-while (per-lane walks of large BVHs): the node loop runs until every lane holds a hit
-     * leaf or has finished, then the wave tests its leaves together -- the primitive code runs
-     * once per round for all lanes instead of once per divergent leaf visit.  kWW = 2: a lane
-     * that holds a leaf keeps stepping speculatively until the others have one (it stops at a
-     * second leaf and keeps it for the next round).  Incoherent rays only (the suffix walks):
-     * coherent primary / visibility waves lose with it (mesh k_vis 122 -> 138 ms). */
-    for (;;) {
-        uint32_t lf = 0, lc = 0;
-        bool stop = false;
+        };
+        const uint32_t nn = sc.n_nodes;
+        uint32_t node = 0;
+        if constexpr (kWW != 0) {
+        /* while-while (per-lane walks of large BVHs): the node loop runs until every lane holds a hit
+         * leaf or has finished, then the wave tests its leaves together -- the primitive code runs
+         * once per round for all lanes instead of once per divergent leaf visit.  kWW = 2: a lane
+         * that holds a leaf keeps stepping speculatively until the others have one (it stops at a
+         * second leaf and keeps it for the next round).  Incoherent rays only (the suffix walks):
+         * coherent primary / visibility waves lose with it (mesh k_vis 122 -> 138 ms). */
         for (;;) {
-            if (!wave_any(lc == 0u && node < nn)) break;
-            if (node < nn && !stop && (kWW == 2 || lc == 0u)) {
-                const DNode n = nodes[node];
-                const bool hit = box_hit(n, br, tmax_box);
-                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-                if (hit && count) {
-                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
-                    else stop = true;   /* the second leaf: revisit it next round */
-                } else {
-                    node = hit ? node + 1 : skip;
+            uint32_t lf = 0, lc = 0;
+            bool stop = false;
+            for (;;) {
+                if (!wave_any(lc == 0u && node < nn)) break;
+                if (node < nn && !stop && (kWW == 2 || lc == 0u)) {
+                    const DNode n = ld_node(node);
+                    const bool hit = box_hit(n, br, tmax_box);
+                    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                    if (hit && count) {
+                        if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                        else stop = true;   /* the second leaf: revisit it next round */
+                    } else {
+                        node = hit ? node + 1 : skip;
+                    }
                 }
             }
+            if (!wave_any(lc != 0u)) break;
+            leaf_test(lf, lc);
         }
-        if (!wave_any(lc != 0u)) break;
-        leaf_test(lf, lc);
-    }
-    return best;
-    }
-    while (node < nn) {
-        const DNode n = nodes[node];
-        const bool hit = box_hit(n, br, tmax_box);
-        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-        if (hit && count) leaf_test(n.first, count);
-        node = (hit && !count) ? node + 1 : skip;
-    }
-    return best;
+        return best;
+        }
+        while (node < nn) {
+            const DNode n = ld_node(node);
+            const bool hit = box_hit(n, br, tmax_box);
+            const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+            if (hit && count) leaf_test(n.first, count);
+            node = (hit && !count) ? node + 1 : skip;
+        }
+        return best;
+    };
+    return sc.lds_bvh ? walk(std::true_type{}) : walk(std::false_type{});
 }
 
 /*
@@ -645,50 +677,60 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
     }
     /* the first ordering: an any-hit walk gains nothing from near-first order (an unoccluded
      * ray visits every box it crosses either way) and one copy keeps the cache footprint small
-     * (k_shadow on the 3.6 k-triangle mesh: 280 ms with it, 301 ms with the octant copies) */
-    auto leaf_any = [&](uint32_t first, uint32_t count) {
-        bool f = false;
-        for (uint32_t i = 0; i < count && !f; ++i) {
-            const DPrim p = load_global(sc.gprims, first + i);
-            float t, u, v;
-            f = prim_hit(p, ray, t, u, v);
-        }
-        return f;
-    };
-    const uint32_t nn = sc.n_nodes;
-    uint32_t node = 0;
-    if constexpr (kWW != 0) {
-    bool found = false;
-    for (;;) {
-        uint32_t lf = 0, lc = 0;
-        bool stop = false;
+     * (k_shadow on the 3.6 k-triangle mesh: 280 ms with it, 301 ms with the octant copies).
+     * kL: LDS-staged BVH, else device memory (explicit address spaces, see trace_closest) */
+    auto walk = [&](auto lds_tag) -> bool {
+        constexpr bool kL = decltype(lds_tag)::value;
+        auto ld_node = [&](uint32_t i) {
+            if (!AMVPT_WALK_AS) return sc.nodes[i];
+            return kL ? load_lds(sc.nodes, i) : load_global(sc.nodes, i);
+        };
+        auto leaf_any = [&](uint32_t first, uint32_t count) {
+            bool f = false;
+            for (uint32_t i = 0; i < count && !f; ++i) {
+                const DPrim p = !AMVPT_WALK_AS ? sc.prims[first + i]
+                                : kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
+                float t, u, v;
+                f = prim_hit(p, ray, t, u, v);
+            }
+            return f;
+        };
+        const uint32_t nn = sc.n_nodes;
+        uint32_t node = 0;
+        if constexpr (kWW != 0) {
+        bool found = false;
         for (;;) {
-            if (!wave_any(!found && lc == 0u && node < nn)) break;
-            if (!found && node < nn && !stop && (kWW == 2 || lc == 0u)) {
-                const DNode n = sc.nodes[node];
-                const bool hit = box_hit(n, br, ray.maxt);
-                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-                if (hit && count) {
-                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
-                    else stop = true;
-                } else {
-                    node = hit ? node + 1 : skip;
+            uint32_t lf = 0, lc = 0;
+            bool stop = false;
+            for (;;) {
+                if (!wave_any(!found && lc == 0u && node < nn)) break;
+                if (!found && node < nn && !stop && (kWW == 2 || lc == 0u)) {
+                    const DNode n = ld_node(node);
+                    const bool hit = box_hit(n, br, ray.maxt);
+                    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                    if (hit && count) {
+                        if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                        else stop = true;
+                    } else {
+                        node = hit ? node + 1 : skip;
+                    }
                 }
             }
+            if (!wave_any(lc != 0u)) break;
+            if (lc) found = found || leaf_any(lf, lc);
         }
-        if (!wave_any(lc != 0u)) break;
-        if (lc) found = found || leaf_any(lf, lc);
-    }
-    return found;
-    }
-    while (node < nn) {
-        const DNode n = sc.nodes[node];
-        const bool hit = box_hit(n, br, ray.maxt);
-        const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-        if (hit && count && leaf_any(n.first, count)) return true;
-        node = (hit && !count) ? node + 1 : skip;
-    }
-    return false;
+        return found;
+        }
+        while (node < nn) {
+            const DNode n = ld_node(node);
+            const bool hit = box_hit(n, br, ray.maxt);
+            const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+            if (hit && count && leaf_any(n.first, count)) return true;
+            node = (hit && !count) ? node + 1 : skip;
+        }
+        return false;
+    };
+    return sc.lds_bvh ? walk(std::true_type{}) : walk(std::false_type{});
 }
 
 /*
