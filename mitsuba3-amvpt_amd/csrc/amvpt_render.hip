@@ -67,14 +67,19 @@ void *g_exchange_ctx = nullptr;
  * (tiny scenes; measured on the Cornell box: k_extend 114 -> 100 ms, k_shadow 103 -> 81 ms
  * per config-M frame; brute force in the coherent primary / visibility walks was slower:
  * k_vis 90 -> 248 ms, k_prim_hit 12 -> 30 ms). */
-enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */ };
+/* WALK_LANE_NS: the per-lane walk of a scene without spheres (no float64 sphere code in the suffix walks:
+ * the sphere branch cost the mesh k_shadow 191 -> 207 ms once the sphere screen grew it, r04g) */
+enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */, WALK_LANE_NS = 4 };
+#ifndef AMVPT_LANE_NS
+#define AMVPT_LANE_NS 1   /* sphere-free scenes take the WALK_LANE_NS suffix walks (0: WALK_LANE, A/B) */
+#endif
 template <int kWalk> AD Hit walk_closest(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_closest<kWalk == WALK_BRUTE>(sc, r);
-    return trace_closest<kWalk == WALK_UNI, AMVPT_WALK_WW>(sc, r);
+    return trace_closest<kWalk == WALK_UNI, AMVPT_WALK_WW, kWalk != WALK_LANE_NS>(sc, r);
 }
 template <int kWalk> AD bool walk_any(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_any<kWalk == WALK_BRUTE>(sc, r);
-    return trace_any<kWalk == WALK_UNI, AMVPT_WALK_WW>(sc, r);
+    return trace_any<kWalk == WALK_UNI, AMVPT_WALK_WW, kWalk != WALK_LANE_NS>(sc, r);
 }
 
 struct KParams {
@@ -3185,6 +3190,7 @@ void launch_shadow(int walk, dim3 grid, size_t lds, hipStream_t st, const KParam
     if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_UNI>), grid, dim3(256), lds, st, P, dS, B);
+    else if (walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_NS>), grid, dim3(256), lds, st, P, dS, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE>), grid, dim3(256), lds, st, P, dS, B);
 }
 #else
@@ -3805,7 +3811,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * (AMVPT_COH_UNI, see launch_primary); the incoherent suffix rays keep the per-lane walk */
     const bool uni_coh = uni || (AMVPT_COH_UNI && trav == 0u);
     /* suffix walk: brute force for tiny scenes in auto mode */
-    int walk = uni ? WALK_UNI : WALK_LANE;
+    int walk = uni ? WALK_UNI : (scene->has_spheres || !AMVPT_LANE_NS) ? WALK_LANE : WALK_LANE_NS;
     if (uni && trav == 0u && K.brute && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
     const bool diff = diff_rec;                                                                           /* kDiff instances */
     /* NEE traced inside k_bounce (brute-force walks; AMVPT_OPT_SPLIT_NEE keeps k_shadow) */
@@ -3994,6 +4000,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else if (walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_NS>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             T.end(st);
             T.begin(AMVPT_K_BOUNCE, st);

@@ -420,7 +420,9 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
     return best;
 }
 
-template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
+template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v);
+/* kSph = false (per-lane walks): the scene has no sphere, the primitive tests carry no float64 code */
+template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     if (!kUni && sc.o_n) return trace_closest_tl(sc, ray);
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
@@ -474,7 +476,7 @@ template <bool kUni, int kWW = 0> AD Hit trace_closest(const SceneRef &sc, const
                 const uint32_t pi = first + i;
                 const DPrim p = !AMVPT_WALK_AS ? sc.prims[pi] : kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
                 float t, u, v;
-                if (prim_hit(p, ray, t, u, v)) {
+                if (prim_hit_b<kSph>(p, p.type, ray, t, u, v)) {
                     if (t < best.t || (t == best.t && p.pad < best_orig)) {
                         best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
                         best_orig = p.pad;
@@ -642,7 +644,7 @@ AD void trace_any_uni_tl(const SceneRef &sc, const Ray &r0, bool act0, const Ray
 }
 
 /* Any hit in [0, maxt] (Scene::ray_test); same two walks as trace_closest. */
-template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
+template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
     if (sc.t_n) {
         if (kUni) {
             bool f0, f1;
@@ -691,7 +693,7 @@ template <bool kUni, int kWW = 0> AD bool trace_any(const SceneRef &sc, const Ra
                 const DPrim p = !AMVPT_WALK_AS ? sc.prims[first + i]
                                 : kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
                 float t, u, v;
-                f = prim_hit(p, ray, t, u, v);
+                f = prim_hit_b<kSph>(p, p.type, ray, t, u, v);
             }
             return f;
         };
