@@ -93,6 +93,7 @@ struct KParams {
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
     uint32_t trav_mode;     /* amvpt_set_traversal */
+    uint32_t sph;           /* the scene has spheres (else the coherent walks run their sphere-free instances) */
     uint32_t win_rs;        /* splat window row stride residue mod 32 (0: stride = width) */
     uint32_t adapt_seed;    /* adaptive pass: seed of the forked sampler (base_seed + wavefront) */
     uint32_t pass_seed;     /* adaptive pass: seed_value of the pass whose lanes are refilled */
@@ -2314,7 +2315,7 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
  * is computed once and the hit goes straight into the request code (it is still stored for
  * k_mv_primary).  AMVPT_FUSE_PRIM=0 keeps the two launches (A/B).
  */
-template <int G, bool kTab, bool kDiff>
+template <int G, bool kTab, bool kDiff, bool kSph = true>
 __global__ void __launch_bounds__(256) k_prim_hit_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -2324,7 +2325,7 @@ __global__ void __launch_bounds__(256) k_prim_hit_req(KParams P, const DScene *S
     const PrimRay pr = primary_raygen(P, V, i);
     Hit h{kInf, 0.f, 0.f, -1};
     if (P.max_depth != 0) {
-        h = trace_closest<true>(sc, pr.ray);
+        h = trace_closest<true, 0, kSph>(sc, pr.ray);
         B.hit[i] = hit_rec(h);
     }
     prim_requests<G, kTab, kDiff>(P, sc, S, V, B, i, pr, h);
@@ -2346,7 +2347,7 @@ template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS 
 #define AMVPT_VIS_WAVES 6
 #endif
 template <int G, bool kUni> constexpr int vis_min_waves() { return vis_pairs<G, kUni>() ? AMVPT_VIS_WAVES : 0; }
-template <int G, bool kUni>
+template <int G, bool kUni, bool kSph = true>
 __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>())) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -2373,7 +2374,7 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
             }
         }
         bool occ0, occ1;
-        trace_any2_uni(sc, r[0], act[0], r[1], act[1], occ0, occ1);
+        trace_any2_uni<kSph>(sc, r[0], act[0], r[1], act[1], occ0, occ1);
         const unsigned long long m0 = __ballot(occ0), m1 = __ballot(occ1);
         if ((threadIdx.x & 63u) == 0u) {
             B.occ[(size_t) (2u * blockIdx.x) * Gn + (uint32_t) k] = m0;
@@ -2402,7 +2403,7 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>()
         if (i < P.chunk_n && mget(bits, k)) {
             nn = B.vreq[1][i]; d = B.vreq[2][i];
             const f3 target = k == 0 ? mk(d.x, d.y, d.z) : camera_point(V[group_view_n((uint32_t) Gn, p_idx, k)], nn.w, d.w);
-            occ = trace_any<kUni>(sc, spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target));
+            occ = trace_any<kUni, 0, kSph>(sc, spawn_ray_to(mk(a.x, a.y, a.z), mk(nn.x, nn.y, nn.z), target));
         }
         const unsigned long long m = __ballot(occ);
         if ((threadIdx.x & 63u) == 0u) B.occ[(size_t) blockIdx.x * Gn + (uint32_t) k] = m;
@@ -3309,7 +3310,10 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     const size_t lds_view = B.vstate ? 0u : (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
     if (uni && ab_knobs().fuse_prim) {
         T.begin(AMVPT_K_PRIM_HIT, st);
-        if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        /* sphere-free scenes: the instances without float64 sphere code (the Cornell and mesh benches) */
+        if (tab && diff && !P.sph) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab && !P.sph) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
@@ -3328,7 +3332,8 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     T.begin(AMVPT_K_VIS, st);
     constexpr bool kVisPairs = vis_pairs<G, true>();
     const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
-    if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    if (uni && !P.sph) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true, false>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    else if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     T.end(st);
     T.begin(AMVPT_K_MV_PRIMARY, st);
@@ -3727,6 +3732,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.nc_oy = (float) (-(int) P.off_y) - .5f;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = trav;
+    P.sph = scene->has_spheres ? 1u : 0u;
     P.win_rs = K.win_rs;
     P.range_begin = rect ? 0 : lane_begin;
     P.rect = rect ? 1u : 0u;

@@ -335,9 +335,10 @@ template <typename T> AD T load_lds(const T *base, uint32_t idx) { return load_a
 template <typename T> AD T load_global(const T *base, uint32_t idx) { return load_as<T, 1>(base, idx); }
 
 /* Primitive test with a wave-uniform primitive type (no divergence between shapes). */
-AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
+/* kSph = false: the scene has no sphere -- no float64 code in the walk (k_vis 80 -> 41 VGPRs) */
+template <bool kSph = true> AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
     if (type == PRIM_RECT) return rect_hit(p, r, t, u, v);
-    if (type == PRIM_TRI) return tri_hit(p, r, t, u, v);
+    if (!kSph || type == PRIM_TRI) return tri_hit(p, r, t, u, v);
     u = v = 0.f;
     return sphere_hit(p, r, t);
 }
@@ -447,7 +448,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const S
                     const uint32_t pi = first + i;
                     const DPrim p = load_uniform(sc.gprims, pi);
                     float t, u, v;
-                    const bool h = prim_hit_u(p, ufirst(p.type), ray, t, u, v);
+                    const bool h = prim_hit_u<kSph>(p, ufirst(p.type), ray, t, u, v);
                     const uint32_t orig = ufirst(p.pad);
                     const bool better = h && (t < best.t || (t == best.t && orig < best_orig));
                     best.t = better ? t : best.t;
@@ -668,7 +669,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const Scen
                 for (uint32_t i = 0; i < count; ++i) {
                     const DPrim p = load_uniform(sc.gprims, first + i);
                     float t, u, v;
-                    const bool h = prim_hit_u(p, ufirst(p.type), ray, t, u, v);
+                    const bool h = prim_hit_u<kSph>(p, ufirst(p.type), ray, t, u, v);
                     found = found || h;
                 }
                 if (!wave_any(!found)) break;
@@ -747,6 +748,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const Scen
  * 79.0 ms, C3 232 -> 284 ms (r04e; 48 B of scratch and the pair moves outweigh the packed arithmetic) */
 #define AMVPT_PAIR_RAYS 0
 #endif
+template <bool kSph = true>
 AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
     if (sc.t_n) { trace_any_uni_tl(sc, r0, act0, r1, act1, true, f0, f1); return; }
     const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
@@ -772,8 +774,8 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
                     continue;
                 }
                 float t, u, v;
-                const bool h0 = prim_hit_u(p, type, r0, t, u, v);
-                const bool h1 = prim_hit_u(p, type, r1, t, u, v);
+                const bool h0 = prim_hit_u<kSph>(p, type, r0, t, u, v);
+                const bool h1 = prim_hit_u<kSph>(p, type, r1, t, u, v);
                 f0 = f0 || h0;
                 f1 = f1 || h1;
             }
