@@ -660,7 +660,16 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", (int) e);
         return AMVPT_OK;
     };
-    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes;
+    /* sphere ordinals (DScene::sph_prims): the record's `face` field, unused by spheres otherwise */
+    std::vector<uint32_t> sph_prims;
+    for (uint32_t i = 0; i < (uint32_t) prims.size(); ++i)
+        if (prims[i].type == PRIM_SPHERE) {
+            prims[i].face = (uint32_t) sph_prims.size();
+            sph_prims.push_back(i);
+        }
+    const uint32_t n_sph = (uint32_t) sph_prims.size();
+    if (sph_prims.empty()) sph_prims.resize(1, 0u);
+    void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes, *p_sph;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
     if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
@@ -671,6 +680,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
     UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
+    UP(sph_prims, p_sph)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -689,6 +699,9 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.t_stride = t_stride;
     D.onodes = (const DNode *) p_onodes;
     D.o_stride = o_stride;
+    D.sph_prims = (const uint32_t *) p_sph;
+    D.n_sph = n_sph;
+    sc->n_sph = n_sph;
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;

@@ -70,6 +70,9 @@ void *g_exchange_ctx = nullptr;
 /* WALK_LANE_NS: the per-lane walk of a scene without spheres (no float64 sphere code in the suffix walks:
  * the sphere branch cost the mesh k_shadow 191 -> 207 ms once the sphere screen grew it, r04g) */
 enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */, WALK_LANE_NS = 4 };
+#ifndef AMVPT_SPHERE_DEFER
+#define AMVPT_SPHERE_DEFER 1   /* scenes of <= 64 spheres: the coherent walks defer their float64 tests (0: in place, A/B) */
+#endif
 #ifndef AMVPT_LANE_NS
 #define AMVPT_LANE_NS 1   /* sphere-free scenes take the WALK_LANE_NS suffix walks (0: WALK_LANE, A/B) */
 #endif
@@ -93,7 +96,7 @@ struct KParams {
     uint32_t box, coalesce_single, path_box_pos, is_mvpath;
     uint32_t seed_value;
     uint32_t trav_mode;     /* amvpt_set_traversal */
-    uint32_t sph;           /* the scene has spheres (else the coherent walks run their sphere-free instances) */
+    uint32_t sph;           /* spheres in the coherent walks: 0 none (sphere-free instances), 1 tested in place, 2 deferred (dgeom.h) */
     uint32_t win_rs;        /* splat window row stride residue mod 32 (0: stride = width) */
     uint32_t adapt_seed;    /* adaptive pass: seed of the forked sampler (base_seed + wavefront) */
     uint32_t pass_seed;     /* adaptive pass: seed_value of the pass whose lanes are refilled */
@@ -2315,8 +2318,11 @@ __global__ void __launch_bounds__(256) k_prim_req(KParams P, const DScene *Sp, c
  * is computed once and the hit goes straight into the request code (it is still stored for
  * k_mv_primary).  AMVPT_FUSE_PRIM=0 keeps the two launches (A/B).
  */
-template <int G, bool kTab, bool kDiff, bool kSph = true>
-__global__ void __launch_bounds__(256) k_prim_hit_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+#ifndef AMVPT_PRIM_HIT_WAVES_DEFER
+#define AMVPT_PRIM_HIT_WAVES_DEFER 8   /* as AMVPT_VIS_WAVES_DEFER, for the primary closest-hit walk */
+#endif
+template <int G, bool kTab, bool kDiff, int kSph = 1>
+__global__ void __launch_bounds__(256, kSph == 2 ? AMVPT_PRIM_HIT_WAVES_DEFER : 1) k_prim_hit_req(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, &V, P.n_views);
@@ -2347,8 +2353,13 @@ template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS 
 #define AMVPT_VIS_WAVES 6
 #endif
 template <int G, bool kUni> constexpr int vis_min_waves() { return vis_pairs<G, kUni>() ? AMVPT_VIS_WAVES : 0; }
-template <int G, bool kUni, bool kSph = true>
-__global__ void __launch_bounds__(64 * vis_waves<G>(), (vis_min_waves<G, kUni>())) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
+#ifndef AMVPT_VIS_WAVES_DEFER
+/* k_vis with deferred sphere tests: the walk needs what the sphere-free walk needs (41 VGPRs), so the register
+ * budget is that of 8 waves/SIMD; the float64 tests after the walk -- rare, after the screen -- may spill */
+#define AMVPT_VIS_WAVES_DEFER 8
+#endif
+template <int G, bool kUni, int kSph = 1>
+__global__ void __launch_bounds__(64 * vis_waves<G>(), (kSph == 2 && vis_pairs<G, kUni>() ? AMVPT_VIS_WAVES_DEFER : vis_min_waves<G, kUni>())) k_vis(KParams P, const DScene *Sp, const DView *V, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 4) != 0>(S, lds, P.trav_mode);
@@ -3313,9 +3324,12 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     const size_t lds_view = B.vstate ? 0u : (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
     if (uni && ab_knobs().fuse_prim) {
         T.begin(AMVPT_K_PRIM_HIT, st);
-        /* sphere-free scenes: the instances without float64 sphere code (the Cornell and mesh benches) */
-        if (tab && diff && !P.sph) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
-        else if (tab && !P.sph) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        /* sphere-free scenes: the instances without float64 sphere code (the Cornell and mesh benches); scenes of
+         * <= 64 spheres: the deferred sphere tests (P.sph, dgeom.h) */
+        if (tab && diff && P.sph == 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true, 0>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab && P.sph == 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false, 0>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab && diff && P.sph == 2) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true, 2>), g256, dim3(256), lds_tab, st, P, S, V, B);
+        else if (tab && P.sph == 2) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false, 2>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else if (tab && diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, true, false>), g256, dim3(256), lds_tab, st, P, S, V, B);
         else if (diff) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_prim_hit_req<G, false, true>), g256, dim3(256), lds_tab, st, P, S, V, B);
@@ -3335,7 +3349,8 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     T.begin(AMVPT_K_VIS, st);
     constexpr bool kVisPairs = vis_pairs<G, true>();
     const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
-    if (uni && !P.sph) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true, false>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    if (uni && P.sph == 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true, 0>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
+    else if (uni && P.sph == 2) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true, 2>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     else if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, false>), g64, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     T.end(st);
@@ -3737,7 +3752,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.nc_oy = (float) (-(int) P.off_y) - .5f;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = trav;
-    P.sph = scene->has_spheres ? 1u : 0u;
+    P.sph = !scene->has_spheres ? 0u : (AMVPT_SPHERE_DEFER && scene->n_sph <= 64u) ? 2u : 1u;
     P.win_rs = K.win_rs;
     P.range_begin = rect ? 0 : lane_begin;
     P.rect = rect ? 1u : 0u;

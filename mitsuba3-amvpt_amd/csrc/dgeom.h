@@ -335,12 +335,30 @@ template <typename T> AD T load_lds(const T *base, uint32_t idx) { return load_a
 template <typename T> AD T load_global(const T *base, uint32_t idx) { return load_as<T, 1>(base, idx); }
 
 /* Primitive test with a wave-uniform primitive type (no divergence between shapes). */
-/* kSph = false: the scene has no sphere -- no float64 code in the walk (k_vis 80 -> 41 VGPRs) */
-template <bool kSph = true> AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
+/*
+ * Spheres in the wave-uniform walks, kSph: 0 the scene has none (no float64 code in the walk: k_vis 80 -> 41
+ * VGPRs), 1 tested in place, 2 deferred (scenes of <= 64 spheres): the walk only screens a sphere
+ * (sphere_maybe) and, when a lane may hit it, sets the sphere's bit in a wave-uniform 64-bit mask (the
+ * record's `face` field holds its ordinal, DScene::sph_prims maps it back); the float64 tests run after the
+ * walk, where the walk's own registers are free -- the walk loop then allocates like a sphere-free one.
+ * Hits are order-independent (any hit; closest by the (t, scene-order index) rule), so the results are the
+ * same bits.
+ */
+template <int kSph = 1> AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
     if (type == PRIM_RECT) return rect_hit(p, r, t, u, v);
-    if (!kSph || type == PRIM_TRI) return tri_hit(p, r, t, u, v);
+    if (kSph != 1 || type == PRIM_TRI) return tri_hit(p, r, t, u, v);
     u = v = 0.f;
     return sphere_hit(p, r, t);
+}
+/* the k-th sphere's primitive record (a scalar load of DScene::sph_prims) */
+AD DPrim deferred_sphere(const SceneRef &sc, uint32_t k) {
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    return load_uniform(sc.gprims, ufirst(((cu32 *) (uintptr_t) sc.g->sph_prims)[k]));
+}
+AD uint32_t mask_pop(uint64_t &m) {
+    const uint32_t k = (uint32_t) __builtin_ctzll(m);
+    m &= m - 1ull;
+    return k;
 }
 
 /*
@@ -423,7 +441,7 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
 
 template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v);
 /* kSph = false (per-lane walks): the scene has no sphere, the primitive tests carry no float64 code */
-template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
+template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     if (!kUni && sc.o_n) return trace_closest_tl(sc, ray);
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
@@ -437,6 +455,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const S
                                     (fbits(ray.d.x) >> 31) | ((fbits(ray.d.y) >> 31) << 1) | ((fbits(ray.d.z) >> 31) << 2)) * sc.oct_stride
                                               : sc.gnodes;
         uint32_t node = 0;
+        uint64_t dm = 0;   /* kSph = 2: deferred spheres */
         while (node < nn) {
             const DNode n = load_uniform(gn, node);
             const bool enter = wave_any(box_hit(n, br, tmax_box));
@@ -447,8 +466,13 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const S
                 for (uint32_t i = 0; i < count; ++i) {
                     const uint32_t pi = first + i;
                     const DPrim p = load_uniform(sc.gprims, pi);
+                    const uint32_t type = ufirst(p.type);
+                    if (kSph == 2 && type == PRIM_SPHERE) {
+                        if (wave_any(sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+                        continue;
+                    }
                     float t, u, v;
-                    const bool h = prim_hit_u<kSph>(p, ufirst(p.type), ray, t, u, v);
+                    const bool h = prim_hit_u<kSph>(p, type, ray, t, u, v);
                     const uint32_t orig = ufirst(p.pad);
                     const bool better = h && (t < best.t || (t == best.t && orig < best_orig));
                     best.t = better ? t : best.t;
@@ -460,6 +484,21 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const S
                 }
             }
             node = (enter && !count) ? node + 1 : skip;
+        }
+        if constexpr (kSph == 2) {
+            while (dm) {
+                const uint32_t k = mask_pop(dm);
+                const DPrim p = deferred_sphere(sc, k);
+                float t;
+                const bool h = sphere_hit(p, ray, t);
+                const uint32_t orig = ufirst(p.pad);
+                const bool better = h && (t < best.t || (t == best.t && orig < best_orig));
+                best.t = better ? t : best.t;
+                best.u = better ? 0.f : best.u;
+                best.v = better ? 0.f : best.v;
+                best.prim = better ? (int32_t) ufirst(sc.g->sph_prims[k]) : best.prim;
+                best_orig = better ? orig : best_orig;
+            }
         }
         return best;
     }
@@ -477,7 +516,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD Hit trace_closest(const S
                 const uint32_t pi = first + i;
                 const DPrim p = !AMVPT_WALK_AS ? sc.prims[pi] : kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
                 float t, u, v;
-                if (prim_hit_b<kSph>(p, p.type, ray, t, u, v)) {
+                if (prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v)) {
                     if (t < best.t || (t == best.t && p.pad < best_orig)) {
                         best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
                         best_orig = p.pad;
@@ -645,7 +684,7 @@ AD void trace_any_uni_tl(const SceneRef &sc, const Ray &r0, bool act0, const Ray
 }
 
 /* Any hit in [0, maxt] (Scene::ray_test); same two walks as trace_closest. */
-template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
+template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef &sc, const Ray &ray) {
     if (sc.t_n) {
         if (kUni) {
             bool f0, f1;
@@ -659,6 +698,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const Scen
         const uint32_t nn = ufirst(sc.n_nodes);
         bool found = false;
         uint32_t node = 0;
+        uint64_t dm = 0;   /* kSph = 2: deferred spheres */
         while (node < nn) {
             const DNode n = load_uniform(sc.gnodes, node);
             const bool enter = wave_any(!found && box_hit(n, br, ray.maxt));
@@ -668,13 +708,26 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const Scen
                 const uint32_t first = ufirst(n.first);
                 for (uint32_t i = 0; i < count; ++i) {
                     const DPrim p = load_uniform(sc.gprims, first + i);
+                    const uint32_t type = ufirst(p.type);
+                    if (kSph == 2 && type == PRIM_SPHERE) {
+                        if (wave_any(!found && sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+                        continue;
+                    }
                     float t, u, v;
-                    const bool h = prim_hit_u<kSph>(p, ufirst(p.type), ray, t, u, v);
+                    const bool h = prim_hit_u<kSph>(p, type, ray, t, u, v);
                     found = found || h;
                 }
                 if (!wave_any(!found)) break;
             }
             node = (enter && !count) ? node + 1 : skip;
+        }
+        if constexpr (kSph == 2) {
+            while (dm && wave_any(!found)) {
+                const DPrim p = deferred_sphere(sc, mask_pop(dm));
+                float t;
+                const bool h = !found && sphere_hit(p, ray, t);
+                found = found || h;
+            }
         }
         return found;
     }
@@ -694,7 +747,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const Scen
                 const DPrim p = !AMVPT_WALK_AS ? sc.prims[first + i]
                                 : kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
                 float t, u, v;
-                f = prim_hit_b<kSph>(p, p.type, ray, t, u, v);
+                f = prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v);
             }
             return f;
         };
@@ -748,7 +801,7 @@ template <bool kUni, int kWW = 0, bool kSph = true> AD bool trace_any(const Scen
  * 79.0 ms, C3 232 -> 284 ms (r04e; 48 B of scratch and the pair moves outweigh the packed arithmetic) */
 #define AMVPT_PAIR_RAYS 0
 #endif
-template <bool kSph = true>
+template <int kSph = 1>
 AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
     if (sc.t_n) { trace_any_uni_tl(sc, r0, act0, r1, act1, true, f0, f1); return; }
     const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
@@ -756,6 +809,7 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
     const uint32_t nn = ufirst(sc.n_nodes);
     f0 = !act0; f1 = !act1;
     uint32_t node = 0;
+    uint64_t dm = 0;   /* kSph = 2: deferred spheres */
     while (node < nn) {
         const DNode n = load_uniform(sc.gnodes, node);
         const bool enter = wave_any((!f0 && box_hit(n, b0, r0.maxt)) || (!f1 && box_hit(n, b1, r1.maxt)));
@@ -766,6 +820,10 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
             for (uint32_t i = 0; i < count; ++i) {
                 const DPrim p = load_uniform(sc.gprims, first + i);
                 const uint32_t type = ufirst(p.type);
+                if (kSph == 2 && type == PRIM_SPHERE) {
+                    if (wave_any((!f0 && sphere_maybe(p, r0)) || (!f1 && sphere_maybe(p, r1)))) dm |= 1ull << ufirst(p.face);
+                    continue;
+                }
                 if (AMVPT_PAIR_RAYS && type != PRIM_SPHERE) {
                     /* both rays against the primitive as one packed test */
                     const Hit2 h = type == PRIM_RECT ? rect_hit2(prim_pair(p), R2) : tri_hit2(prim_pair(p), R2);
@@ -782,6 +840,16 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
             if (!wave_any(!f0 || !f1)) break;
         }
         node = (enter && !count) ? node + 1 : skip;
+    }
+    if constexpr (kSph == 2) {
+        while (dm && wave_any(!f0 || !f1)) {
+            const DPrim p = deferred_sphere(sc, mask_pop(dm));
+            float t;
+            const bool h0 = !f0 && sphere_hit(p, r0, t);
+            const bool h1 = !f1 && sphere_hit(p, r1, t);
+            f0 = f0 || h0;
+            f1 = f1 || h1;
+        }
     }
     f0 = f0 && act0;
     f1 = f1 && act1;

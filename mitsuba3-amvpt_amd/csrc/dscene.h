@@ -121,6 +121,10 @@ struct DScene {
      * each, a shallower cut (all 8 are staged together); 0: none */
     const DNode *onodes;
     uint32_t o_stride;
+    /* the spheres' primitive indices in scene order of their ordinals (a sphere record's `face` field holds its
+     * ordinal): the wave-uniform walks' deferred sphere tests (dgeom.h, kSph = 2) */
+    const uint32_t *sph_prims;
+    uint32_t n_sph;
 };
 constexpr uint32_t kPortal = 0x80000000u;
 
