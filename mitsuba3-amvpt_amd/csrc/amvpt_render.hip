@@ -70,9 +70,6 @@ void *g_exchange_ctx = nullptr;
 /* WALK_LANE_NS: the per-lane walk of a scene without spheres (no float64 sphere code in the suffix walks:
  * the sphere branch cost the mesh k_shadow 191 -> 207 ms once the sphere screen grew it, r04g) */
 enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */, WALK_LANE_NS = 4 };
-#ifndef AMVPT_SPHERE_DEFER
-#define AMVPT_SPHERE_DEFER 1   /* scenes of <= 64 spheres: the coherent walks defer their float64 tests (0: in place, A/B) */
-#endif
 #ifndef AMVPT_LANE_NS
 #define AMVPT_LANE_NS 1   /* sphere-free scenes take the WALK_LANE_NS suffix walks (0: WALK_LANE, A/B) */
 #endif

@@ -168,6 +168,11 @@ AD Hit2 tri_hit2(const PrimPair &P, const RayPair &R) {
 #ifndef AMVPT_SPHERE_SCREEN
 #define AMVPT_SPHERE_SCREEN 2   /* 1: the line test only, 0: off (A/B) */
 #endif
+#ifndef AMVPT_SPHERE_DEFER
+/* 1: the wave-uniform walks of scenes with <= 64 spheres and the brute-force walks defer the float64 tests
+ * past the walk (kSph = 2 below, brute_closest / brute_any); 0: in place (A/B) */
+#define AMVPT_SPHERE_DEFER 1
+#endif
 AD bool sphere_maybe(const DPrim &p, const Ray &ray) {
     const float lx = ray.o.x - p.a[0], ly = ray.o.y - p.a[1], lz = ray.o.z - p.a[2], r = p.a[3];
     const f3 d = ray.d;
@@ -927,9 +932,20 @@ template <bool kSph> AD bool brute_pair_any(const DPrim &a, const DPrim &b, cons
 /* Two records in flight (a, b), each reloaded in place right after its own test: the next
  * record's scalar load overlaps the current test and no record is copied between registers
  * (a one-record prefetch made the compiler move all 16 SGPRs of the record every iteration). */
+/* kSph with AMVPT_SPHERE_DEFER: the float64 sphere tests run after the loop over the primitives (a brute-force
+ * scene has <= kBrutePrims < 64 spheres), so the loop allocates like a sphere-free one (see prim_hit_u) */
 template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
+    constexpr bool kDefer = kSph && AMVPT_SPHERE_DEFER && !AMVPT_PAIR_PRIMS;
+    uint64_t dm = 0;
+    auto test = [&](const DPrim &p, uint32_t pi) {
+        if (ufirst(p.type) == PRIM_SPHERE) {
+            if (wave_any(sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+            return;
+        }
+        brute_test<false>(p, pi, ray, best, best_orig);
+    };
     const uint32_t np = ufirst(sc.g->n_prims);
     const uint32_t last = np - 1u;
     DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
@@ -942,10 +958,31 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
             b = load_uniform(sc.gprims, min(pi + 3u, last));
             continue;
         }
+        if constexpr (kDefer) {
+            test(a, pi);
+            a = load_uniform(sc.gprims, min(pi + 2u, last));
+            if (pi + 1 < np) test(b, pi + 1);
+            b = load_uniform(sc.gprims, min(pi + 3u, last));
+            continue;
+        }
         brute_test<kSph>(a, pi, ray, best, best_orig);
         a = load_uniform(sc.gprims, min(pi + 2u, last));
         if (pi + 1 < np) brute_test<kSph>(b, pi + 1, ray, best, best_orig);
         b = load_uniform(sc.gprims, min(pi + 3u, last));
+    }
+    if constexpr (kDefer) {
+        while (dm) {
+            const uint32_t k = mask_pop(dm);
+            const DPrim p = deferred_sphere(sc, k);
+            float t;
+            if (sphere_hit(p, ray, t)) {
+                const uint32_t orig = ufirst(p.pad);
+                if (t < best.t || (t == best.t && orig < best_orig)) {
+                    best.t = t; best.u = 0.f; best.v = 0.f; best.prim = (int32_t) ufirst(sc.g->sph_prims[k]);
+                    best_orig = orig;
+                }
+            }
+        }
     }
     return best;
 }
@@ -954,6 +991,18 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
 template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool skip = false) {
     const uint32_t np = ufirst(sc.g->n_prims);
     bool found = skip;
+    constexpr bool kDefer = kSph && AMVPT_SPHERE_DEFER && !AMVPT_PAIR_PRIMS;
+    uint64_t dm = 0;
+    auto test = [&](const DPrim &p) {
+        const uint32_t type = ufirst(p.type);
+        if (type == PRIM_SPHERE) {
+            if (wave_any(!found && sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+            return;
+        }
+        float t, u, v;
+        const bool h = prim_hit_b<false>(p, type, ray, t, u, v);
+        found = found || h;
+    };
     const uint32_t last = np - 1u;
     DPrim a = load_uniform(sc.gprims, 0), b = load_uniform(sc.gprims, min(1u, last));
     for (uint32_t pi = 0; pi < np; pi += 2) {
@@ -962,6 +1011,11 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
             const bool hab = brute_pair_any<kSph>(a, b, ray);
             found = found || hab;
             a = load_uniform(sc.gprims, min(pi + 2u, last));
+            b = load_uniform(sc.gprims, min(pi + 3u, last));
+        } else if constexpr (kDefer) {
+            test(a);
+            a = load_uniform(sc.gprims, min(pi + 2u, last));
+            if (pi + 1 < np) test(b);
             b = load_uniform(sc.gprims, min(pi + 3u, last));
         } else {
             float t, u, v;
@@ -975,6 +1029,14 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
             b = load_uniform(sc.gprims, min(pi + 3u, last));
         }
         if (!wave_any(!found)) break;
+    }
+    if constexpr (kDefer) {
+        while (dm && wave_any(!found)) {
+            const DPrim p = deferred_sphere(sc, mask_pop(dm));
+            float t;
+            const bool h = !found && sphere_hit(p, ray, t);
+            found = found || h;
+        }
     }
     return found;
 }
