@@ -2343,6 +2343,9 @@ __global__ void __launch_bounds__(256, kSph == 2 ? AMVPT_PRIM_HIT_WAVES_DEFER : 
 #endif
 template <int G> constexpr int vis_waves() { return G > 0 ? G : 16; }
 template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS && kUni && G > 0; }
+#ifndef AMVPT_VIS_RAYS
+#define AMVPT_VIS_RAYS 2   /* rays per lane of the pair walk (trace_any2_uni; > 2: trace_anyN_uni, A/B) */
+#endif
 /* waves per SIMD the paired walk's register allocation must allow (0: no bound).  Measured at
  * config M (r02ac): unbounded 96 VGPRs / 5 waves 69.3 ms, 6 waves (80 VGPRs, 12 B scratch)
  * 63.5 ms, 8 waves (64 VGPRs, 52 B scratch) 74.1 ms; one ray per lane, 8 waves: 72.3 ms */
@@ -2362,12 +2365,14 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (kSph == 2 && vis_pairs<G
     SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 4) != 0>(S, lds, P.trav_mode);
     const int Gn = group_size<G>(P);
     if constexpr (vis_pairs<G, kUni>()) {
+        /* kVR = AMVPT_VIS_RAYS rays per lane: 64-lane groups h of the block's 64 x kVR lanes, one view slot k per wave */
+        constexpr int kVR = AMVPT_VIS_RAYS;
         const int k = (int) (threadIdx.x >> 6);
-        Ray r[2];
-        bool act[2];
+        Ray r[kVR];
+        bool act[kVR];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t i = blockIdx.x * 128u + 64u * (uint32_t) h + (threadIdx.x & 63u);
+        for (int h = 0; h < kVR; ++h) {
+            const uint32_t i = blockIdx.x * (64u * kVR) + 64u * (uint32_t) h + (threadIdx.x & 63u);
             act[h] = false;
             r[h] = Ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), 0.f};
             if (i < P.chunk_n) {
@@ -2381,12 +2386,14 @@ __global__ void __launch_bounds__(64 * vis_waves<G>(), (kSph == 2 && vis_pairs<G
                 }
             }
         }
-        bool occ0, occ1;
-        trace_any2_uni<kSph>(sc, r[0], act[0], r[1], act[1], occ0, occ1);
-        const unsigned long long m0 = __ballot(occ0), m1 = __ballot(occ1);
-        if ((threadIdx.x & 63u) == 0u) {
-            B.occ[(size_t) (2u * blockIdx.x) * Gn + (uint32_t) k] = m0;
-            if ((2u * blockIdx.x + 1u) * 64u < P.chunk_n) B.occ[(size_t) (2u * blockIdx.x + 1u) * Gn + (uint32_t) k] = m1;
+        bool occ[kVR];
+        if constexpr (kVR == 2) trace_any2_uni<kSph>(sc, r[0], act[0], r[1], act[1], occ[0], occ[1]);
+        else trace_anyN_uni<kSph, kVR>(sc, r, act, occ);
+#pragma unroll
+        for (int h = 0; h < kVR; ++h) {
+            const unsigned long long m = __ballot(occ[h]);
+            const uint32_t grp = kVR * blockIdx.x + (uint32_t) h;
+            if ((threadIdx.x & 63u) == 0u && (h == 0 || grp * 64u < P.chunk_n)) B.occ[(size_t) grp * Gn + (uint32_t) k] = m;
         }
         return;
     }
@@ -3345,7 +3352,7 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     }
     T.begin(AMVPT_K_VIS, st);
     constexpr bool kVisPairs = vis_pairs<G, true>();
-    const dim3 gvis = kVisPairs ? dim3((cn + 127) / 128) : g64;
+    const dim3 gvis = kVisPairs ? dim3((cn + 64 * AMVPT_VIS_RAYS - 1) / (64 * AMVPT_VIS_RAYS)) : g64;
     if (uni && P.sph == 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true, 0>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     else if (uni && P.sph == 2) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true, 2>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);
     else if (uni) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_vis<G, true>), gvis, dim3(64 * kVW), lds_bvh, st, P, S, V, B);

@@ -860,6 +860,68 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
     f1 = f1 && act1;
 }
 
+/* trace_any2_uni for N rays per lane (AMVPT_VIS_RAYS = N > 2 in k_vis): the wave enters a node when any lane's
+ * ray of any of its N hits its box -- N times the rays in flight per wave on the latency-bound walk */
+template <int kSph, int N>
+AD void trace_anyN_uni(const SceneRef &sc, const Ray *r, const bool *act, bool *f) {
+    BoxRay b[N];
+#pragma unroll
+    for (int h = 0; h < N; ++h) { b[h] = box_ray(r[h]); f[h] = !act[h]; }
+    const uint32_t nn = ufirst(sc.n_nodes);
+    uint32_t node = 0;
+    uint64_t dm = 0;   /* kSph = 2: deferred spheres */
+    auto open = [&]() {
+        bool o = false;
+#pragma unroll
+        for (int h = 0; h < N; ++h) o = o || !f[h];
+        return o;
+    };
+    while (node < nn) {
+        const DNode n = load_uniform(sc.gnodes, node);
+        bool hit = false;
+#pragma unroll
+        for (int h = 0; h < N; ++h) hit = hit || (!f[h] && box_hit(n, b[h], r[h].maxt));
+        const bool enter = wave_any(hit);
+        const uint32_t skc = ufirst(n.skip_count);
+        const uint32_t count = skc >> kNodeCountShift, skip = skc & kNodeSkipMask;
+        if (enter && count) {
+            const uint32_t first = ufirst(n.first);
+            for (uint32_t i = 0; i < count; ++i) {
+                const DPrim p = load_uniform(sc.gprims, first + i);
+                const uint32_t type = ufirst(p.type);
+                if (kSph == 2 && type == PRIM_SPHERE) {
+                    bool m = false;
+#pragma unroll
+                    for (int h = 0; h < N; ++h) m = m || (!f[h] && sphere_maybe(p, r[h]));
+                    if (wave_any(m)) dm |= 1ull << ufirst(p.face);
+                    continue;
+                }
+#pragma unroll
+                for (int h = 0; h < N; ++h) {
+                    float t, u, v;
+                    const bool hh = prim_hit_u<kSph>(p, type, r[h], t, u, v);
+                    f[h] = f[h] || hh;
+                }
+            }
+            if (!wave_any(open())) break;
+        }
+        node = (enter && !count) ? node + 1 : skip;
+    }
+    if constexpr (kSph == 2) {
+        while (dm && wave_any(open())) {
+            const DPrim p = deferred_sphere(sc, mask_pop(dm));
+#pragma unroll
+            for (int h = 0; h < N; ++h) {
+                float t;
+                const bool hh = !f[h] && sphere_hit(p, r[h], t);
+                f[h] = f[h] || hh;
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < N; ++h) f[h] = f[h] && act[h];
+}
+
 /*
  * Brute-force walks for tiny scenes (n_prims <= kBrutePrims, wave-uniform kernels only):
  * every primitive is tested in BVH order with the next record's scalar load issued
