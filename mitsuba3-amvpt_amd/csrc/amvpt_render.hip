@@ -1695,11 +1695,22 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
  * and a wave whose lanes are split between treelet and global nodes waits for both loads per step. */
 #define AMVPT_TREELETS 0
 #endif
+#ifndef AMVPT_EXTEND_RAYS
+#define AMVPT_EXTEND_RAYS 2   /* per-lane k_extend walks: paths per thread (trace_closest_lane2; 1: one, A/B) */
+#endif
+#ifndef AMVPT_EXTEND2_WAVES
+#define AMVPT_EXTEND2_WAVES 5   /* the two-path walk: 89 VGPRs, no scratch (at 6: 80 VGPRs and spills inside the walk) */
+#endif
+#ifndef AMVPT_SHADOW_RAYS
+#define AMVPT_SHADOW_RAYS 2   /* per-lane k_shadow walks: records per thread (trace_any_lane2; 1: one, A/B) */
+#endif
 #ifndef AMVPT_SHADOW_WAVES
 #define AMVPT_SHADOW_WAVES 1
 #endif
 template <int kWalk>
-__global__ void __launch_bounds__(256, AMVPT_EXTEND_WAVES) k_extend(KParams P, const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(256, (AMVPT_EXTEND_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) ? AMVPT_EXTEND2_WAVES
+                                                                                                                  : AMVPT_EXTEND_WAVES)
+k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false, true, false, (AMVPT_TREELETS & 2) != 0>(S, lds, P.trav_mode);
@@ -1708,6 +1719,21 @@ __global__ void __launch_bounds__(256, AMVPT_EXTEND_WAVES) k_extend(KParams P, c
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
     if (blockIdx.x == 0) {
         for (uint32_t q = threadIdx.x; q < kQParts; q += blockDim.x) { B.cnt_out[q * kCntStride] = 0u; B.cnt_nee[q * kCntStride] = 0u; }
+    }
+    if constexpr (AMVPT_EXTEND_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) {
+        /* two paths per thread (trace_closest_lane2): entries e0 + t and e0 + t + blockDim.x */
+        for (uint32_t e0 = blockIdx.x / kQParts * 2u * blockDim.x; e0 < count; e0 += 2u * pstride) {
+            const uint32_t e_0 = e0 + threadIdx.x, e_1 = e_0 + blockDim.x;
+            const bool act0 = e_0 < count, act1 = e_1 < count;
+            Ray r0{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f), kLargest}, r1 = r0;
+            if (act0) { const float4 a = B.q_in[0][pbase + e_0], b = B.q_in[1][pbase + e_0]; r0 = Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest}; }
+            if (act1) { const float4 a = B.q_in[0][pbase + e_1], b = B.q_in[1][pbase + e_1]; r1 = Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest}; }
+            Hit h0, h1;
+            trace_closest_lane2<kWalk == WALK_LANE_NS ? 0 : 1>(sc, r0, act0, r1, act1, h0, h1);
+            if (act0) B.hit[pbase + e_0] = hit_rec(h0);
+            if (act1) B.hit[pbase + e_1] = hit_rec(h1);
+        }
+        return;
     }
     for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
         const uint32_t i = pbase + e0 + threadIdx.x;
@@ -1726,6 +1752,39 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
     SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 1) != 0>(S, lds, P.trav_mode);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_nee[part * kCntStride], pbase = part * B.qcap;
+    /* the visible-light write of a record (the path's result becomes fma(throughput, contribution, result),
+     * formed by k_bounce; its .w -- valid_ray / rng hi -- stays) */
+    auto visible = [&](uint32_t i, const float4 &a, const float4 &b) {
+        const float2 gb = B.nee_gb[i];
+        const uint32_t dest = fbits(a.w);
+        float *const dp = (float *) ((dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest]);
+        dp[0] = b.w;
+        dp[1] = gb.x;
+        dp[2] = gb.y;
+    };
+    auto nee_ray = [&](const float4 &a, const float4 &b) {
+        /* spawn_ray_to's direction and extent from its origin and target (same operations) */
+        const f3 o = mk(a.x, a.y, a.z);
+        f3 d = mk(b.x, b.y, b.z) - o;
+        const float dist = norm(d);
+        d = d / dist;
+        return Ray{o, d, dist * (1.f - kShadowEps)};
+    };
+    if constexpr (AMVPT_SHADOW_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) {
+        /* two records per thread (trace_any_lane2): entries e0 + t and e0 + t + blockDim.x */
+        for (uint32_t e0 = blockIdx.x / kQParts * 2u * blockDim.x; e0 < count; e0 += 2u * pstride) {
+            const uint32_t e_0 = e0 + threadIdx.x, e_1 = e_0 + blockDim.x;
+            const bool act0 = e_0 < count, act1 = e_1 < count;
+            float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), b0 = make_float4(0.f, 0.f, 1.f, 0.f), a1 = a0, b1 = b0;
+            if (act0) { a0 = B.nee[0][pbase + e_0]; b0 = B.nee[1][pbase + e_0]; }
+            if (act1) { a1 = B.nee[0][pbase + e_1]; b1 = B.nee[1][pbase + e_1]; }
+            bool occ0, occ1;
+            trace_any_lane2<kWalk == WALK_LANE_NS ? 0 : 1>(sc, nee_ray(a0, b0), act0, nee_ray(a1, b1), act1, occ0, occ1);
+            if (act0 && !occ0) visible(pbase + e_0, a0, b0);
+            if (act1 && !occ1) visible(pbase + e_1, a1, b1);
+        }
+        return;
+    }
     for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
         const uint32_t i = pbase + e0 + threadIdx.x;
         if (e0 + threadIdx.x < count) {
@@ -1736,16 +1795,7 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
             const float dist = norm(d);
             d = d / dist;
             const Ray r{o, d, dist * (1.f - kShadowEps)};
-            if (!walk_any<kWalk>(sc, r)) {
-                /* the light is visible: the path's result becomes the record's fma(throughput,
-                 * contribution, result), formed by k_bounce (its .w -- valid_ray / rng hi -- stays) */
-                const float2 gb = B.nee_gb[i];
-                const uint32_t dest = fbits(a.w);
-                float *const dp = (float *) ((dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest]);
-                dp[0] = b.w;
-                dp[1] = gb.x;
-                dp[2] = gb.y;
-            }
+            if (!walk_any<kWalk>(sc, r)) visible(i, a, b);   /* the light is visible */
         }
     }
 }

@@ -860,6 +860,115 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
     f1 = f1 && act1;
 }
 
+/*
+ * Per-lane walks of two rays per thread (AMVPT_SHADOW_RAYS / AMVPT_EXTEND_RAYS = 2, the suffix walks of large
+ * BVHs): the speculative while-while walk of trace_any / trace_closest for each ray, stepped together -- the
+ * two node loads of a step are issued back to back, so a thread keeps two dependent-load chains in flight.
+ * Each ray visits exactly the nodes and primitives its single walk visits, so the results are the same.
+ */
+struct LaneWalk { uint32_t node, lf, lc; bool stop; };
+AD void lane_step(const DNode &n, const BoxRay &b, float tmax, LaneWalk &w) {
+    const bool hit = box_hit(n, b, tmax);
+    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+    if (hit && count) {
+        if (w.lc == 0u) { w.lf = n.first; w.lc = count; w.node = skip; }
+        else w.stop = true;   /* the second leaf: revisit it next round */
+    } else {
+        w.node = hit ? w.node + 1 : skip;
+    }
+}
+template <int kSph = 1>
+AD void trace_any_lane2(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, bool &f0, bool &f1) {
+    const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
+    auto walk = [&](auto lds_tag) {
+        constexpr bool kL = decltype(lds_tag)::value;
+        auto ld_node = [&](uint32_t i) { return kL ? load_lds(sc.nodes, i) : load_global(sc.nodes, i); };
+        auto leaf_any = [&](const Ray &ray, uint32_t first, uint32_t count) {
+            bool f = false;
+            for (uint32_t i = 0; i < count && !f; ++i) {
+                const DPrim p = kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
+                float t, u, v;
+                f = prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v);
+            }
+            return f;
+        };
+        const uint32_t nn = sc.n_nodes;
+        LaneWalk w0{act0 ? 0u : nn, 0u, 0u, false}, w1{act1 ? 0u : nn, 0u, 0u, false};
+        bool h0 = false, h1 = false;
+        for (;;) {
+            w0.lf = w0.lc = w1.lf = w1.lc = 0u;
+            w0.stop = w1.stop = false;
+            for (;;) {
+                const bool need = (!h0 && w0.lc == 0u && w0.node < nn) || (!h1 && w1.lc == 0u && w1.node < nn);
+                if (!wave_any(need)) break;
+                const bool s0 = !h0 && w0.node < nn && !w0.stop, s1 = !h1 && w1.node < nn && !w1.stop;
+                DNode n0, n1;
+                if (s0) n0 = ld_node(w0.node);
+                if (s1) n1 = ld_node(w1.node);
+                if (s0) lane_step(n0, b0, r0.maxt, w0);
+                if (s1) lane_step(n1, b1, r1.maxt, w1);
+            }
+            if (!wave_any(w0.lc != 0u || w1.lc != 0u)) break;
+            if (w0.lc) h0 = h0 || leaf_any(r0, w0.lf, w0.lc);
+            if (w1.lc) h1 = h1 || leaf_any(r1, w1.lf, w1.lc);
+        }
+        f0 = h0 && act0;
+        f1 = h1 && act1;
+    };
+    if (sc.lds_bvh) walk(std::true_type{});
+    else walk(std::false_type{});
+}
+
+template <int kSph = 1>
+AD void trace_closest_lane2(const SceneRef &sc, const Ray &r0, bool act0, const Ray &r1, bool act1, Hit &o0, Hit &o1) {
+    const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
+    const DNode *const nodes0 = octant_nodes(sc, r0.d), *const nodes1 = octant_nodes(sc, r1.d);
+    Hit best0{kInf, 0.f, 0.f, -1}, best1{kInf, 0.f, 0.f, -1};
+    uint32_t orig0 = 0xffffffffu, orig1 = 0xffffffffu;
+    float tmax0 = r0.maxt, tmax1 = r1.maxt;
+    auto walk = [&](auto lds_tag) {
+        constexpr bool kL = decltype(lds_tag)::value;
+        auto ld_node = [&](const DNode *nodes, uint32_t i) { return kL ? load_lds(nodes, i) : load_global(nodes, i); };
+        auto leaf_test = [&](const Ray &ray, uint32_t first, uint32_t count, Hit &best, uint32_t &best_orig, float &tmax) {
+            for (uint32_t i = 0; i < count; ++i) {
+                const uint32_t pi = first + i;
+                const DPrim p = kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
+                float t, u, v;
+                if (prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v)) {
+                    if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                        best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                        best_orig = p.pad;
+                        tmax = t;
+                    }
+                }
+            }
+        };
+        const uint32_t nn = sc.n_nodes;
+        LaneWalk w0{act0 ? 0u : nn, 0u, 0u, false}, w1{act1 ? 0u : nn, 0u, 0u, false};
+        for (;;) {
+            w0.lf = w0.lc = w1.lf = w1.lc = 0u;
+            w0.stop = w1.stop = false;
+            for (;;) {
+                const bool need = (w0.lc == 0u && w0.node < nn) || (w1.lc == 0u && w1.node < nn);
+                if (!wave_any(need)) break;
+                const bool s0 = w0.node < nn && !w0.stop, s1 = w1.node < nn && !w1.stop;
+                DNode n0, n1;
+                if (s0) n0 = ld_node(nodes0, w0.node);
+                if (s1) n1 = ld_node(nodes1, w1.node);
+                if (s0) lane_step(n0, b0, tmax0, w0);
+                if (s1) lane_step(n1, b1, tmax1, w1);
+            }
+            if (!wave_any(w0.lc != 0u || w1.lc != 0u)) break;
+            if (w0.lc) leaf_test(r0, w0.lf, w0.lc, best0, orig0, tmax0);
+            if (w1.lc) leaf_test(r1, w1.lf, w1.lc, best1, orig1, tmax1);
+        }
+    };
+    if (sc.lds_bvh) walk(std::true_type{});
+    else walk(std::false_type{});
+    o0 = best0;
+    o1 = best1;
+}
+
 /* trace_any2_uni for N rays per lane (AMVPT_VIS_RAYS = N > 2 in k_vis): the wave enters a node when any lane's
  * ray of any of its N hits its box -- N times the rays in flight per wave on the latency-bound walk */
 template <int kSph, int N>
