@@ -200,6 +200,35 @@ def test_veach_mis_g8(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
+def _cbox_spheres(amvpt_mod, **defines):
+    """The Cornell box with its two cubes replaced by two large diffuse spheres and a small sphere light: the
+    camera, visibility and suffix rays graze the silhouettes constantly, and the NEE rays toward the light
+    end a ShadowEpsilon short of it -- the cases the f32 sphere screen and the deferred float64 tests decide."""
+    import re
+    xml = open(os.path.join(SCENES, "cbox_grid.xml")).read()
+    xml = re.sub(r'<shape type="cube" id="small-box">.*?</shape>\s*<shape type="cube" id="large-box">.*?</shape>',
+                 '<shape type="sphere"><point name="center" x="0.33" y="-0.6" z="0.3"/><float name="radius" value="0.4"/>'
+                 '<ref id="white"/></shape>'
+                 '<shape type="sphere"><point name="center" x="-0.35" y="-0.45" z="-0.3"/><float name="radius" value="0.55"/>'
+                 '<ref id="white"/></shape>'
+                 '<shape type="sphere"><point name="center" x="0.0" y="0.55" z="0.2"/><float name="radius" value="0.08"/>'
+                 '<emitter type="area"><rgb name="radiance" value="20, 20, 20"/></emitter></shape>', xml, flags=re.S)
+    assert xml.count('type="sphere"') == 3
+    return amvpt_mod.load_string(xml, **defines)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["auto_deferred", "wave_uniform_bvh", "per_lane_bvh"])
+def test_sphere_grazing_rays(gpu_ready, amvpt_mod, oracle, mode):
+    """Spheres under every walk: auto mode (brute-force suffix and wave-uniform coherent walks with the
+    float64 tests deferred past the walk), the wave-uniform and the per-lane BVH walks (tested in place),
+    all behind the f32 sphere screen (dgeom.h sphere_maybe) -- records bit-identical to the oracle."""
+    amvpt_mod.set_traversal(mode)
+    try:
+        _check(amvpt_mod, oracle, _cbox_spheres(amvpt_mod, res=24, spp=16, gx=4, gy=2, reuse=8))
+    finally:
+        amvpt_mod.set_traversal(0)
+
+
 @pytest.mark.parametrize("defines", [
     dict(distr="beckmann"),                                            # the reference's default model
     dict(distr="beckmann", vis="false"),
