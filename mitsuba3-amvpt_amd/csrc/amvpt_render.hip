@@ -1696,13 +1696,17 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #define AMVPT_TREELETS 0
 #endif
 #ifndef AMVPT_EXTEND_RAYS
-#define AMVPT_EXTEND_RAYS 2   /* per-lane k_extend walks: paths per thread (trace_closest_lane2; 1: one, A/B) */
+/* per-lane k_extend walks: paths per thread (2: trace_closest_lane2, A/B).  1: the two-path walk measured slower
+ * on the mesh bench (k_extend 229.4 -> 254.9 ms at 5 waves/SIMD, r04z_ab_mesh.log) */
+#define AMVPT_EXTEND_RAYS 1
 #endif
 #ifndef AMVPT_EXTEND2_WAVES
 #define AMVPT_EXTEND2_WAVES 5   /* the two-path walk: 89 VGPRs, no scratch (at 6: 80 VGPRs and spills inside the walk) */
 #endif
 #ifndef AMVPT_SHADOW_RAYS
-#define AMVPT_SHADOW_RAYS 2   /* per-lane k_shadow walks: records per thread (trace_any_lane2; 1: one, A/B) */
+/* per-lane k_shadow walks: records per thread (2: trace_any_lane2, A/B).  1: k_shadow 172.8 -> 182.7 ms with two
+ * (r04z_ab_mesh.log) */
+#define AMVPT_SHADOW_RAYS 1
 #endif
 #ifndef AMVPT_SHADOW_WAVES
 #define AMVPT_SHADOW_WAVES 1
@@ -2394,7 +2398,9 @@ __global__ void __launch_bounds__(256, kSph == 2 ? AMVPT_PRIM_HIT_WAVES_DEFER : 
 template <int G> constexpr int vis_waves() { return G > 0 ? G : 16; }
 template <int G, bool kUni> constexpr bool vis_pairs() { return AMVPT_VIS_PAIRS && kUni && G > 0; }
 #ifndef AMVPT_VIS_RAYS
-#define AMVPT_VIS_RAYS 2   /* rays per lane of the pair walk (trace_any2_uni; > 2: trace_anyN_uni, A/B) */
+/* rays per lane of the pair walk (trace_any2_uni; > 2: trace_anyN_uni, A/B -- 4 rays: config-M k_vis 43.5 ->
+ * 50.5 ms, C3 165 -> 238 ms, r04z_ab_*.log) */
+#define AMVPT_VIS_RAYS 2
 #endif
 /* waves per SIMD the paired walk's register allocation must allow (0: no bound).  Measured at
  * config M (r02ac): unbounded 96 VGPRs / 5 waves 69.3 ms, 6 waves (80 VGPRs, 12 B scratch)

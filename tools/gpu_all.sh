@@ -7,9 +7,12 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 $S 900 tests -- python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread
 $S 300 smoke -- python -u -c "import __graft_entry__ as g; g.smoke()"
-AB_CONFIG=mesh $S 300 abmesh -- python -u tools/ab_value.py --kernels lib_r1 lib lib_v4 lib_r1 lib lib_v4
-AB_CONFIG=C3 $S 300 abC3 -- python -u tools/ab_value.py --kernels lib_d0 lib_u lib_r1 lib_v4 lib_d0 lib_u lib_r1 lib_v4
-$S 300 abM -- python -u tools/ab_value.py --kernels lib_r1 lib_v4 lib lib_r1 lib_v4 lib
+# the A/B set of the call (AB=0 skips it): variant library dirs next to lib/, see profiles/<tag>_ab_*.log
+if [ "${AB:-1}" = 1 ]; then
+  AB_CONFIG=mesh $S 300 abmesh -- python -u tools/ab_value.py --kernels lib_r1 lib lib_v4 lib_r1 lib lib_v4
+  AB_CONFIG=C3 $S 300 abC3 -- python -u tools/ab_value.py --kernels lib_d0 lib_u lib_r1 lib_v4 lib_d0 lib_u lib_r1 lib_v4
+  $S 300 abM -- python -u tools/ab_value.py --kernels lib_r1 lib_v4 lib lib_r1 lib_v4 lib
+fi
 one() {   # config
   c=$1
   if [ $c = M ]; then B="--steps 10 --warmup 2"; P=""; else B="--steps 3 --warmup 1 --no-cpu-baseline --config $c"; P="--config $c"; fi
