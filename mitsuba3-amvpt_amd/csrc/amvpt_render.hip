@@ -1156,33 +1156,6 @@ AD FilterCoeffs default_filter() {
 #ifndef AMVPT_SPLAT_PK
 #define AMVPT_SPLAT_PK 1   /* row splat: packed-f32 products of the two row halves: config-M splat 101.8 -> 97.7 ms (r03y; 0: A/B) */
 #endif
-#ifndef AMVPT_SPLAT_PKW
-#define AMVPT_SPLAT_PKW 1   /* row splat: the union weights evaluated two at a time in v_pk_* pairs (0: one by one, A/B) */
-#endif
-typedef float f2w __attribute__((ext_vector_type(2)));
-/* gaussian_eval of two arguments at once: per element exactly gaussian_eval's IEEE operations (packed FMA and
- * multiply are per-element IEEE), so the same bits */
-AD f2w gaussian_eval2(const FilterCoeffs &f, f2w x) {
-    auto fm = [](f2w a, f2w b, f2w c) { return __builtin_elementwise_fma(a, b, c); };
-    const float *c = f.c;
-    const f2w x2 = x * x;
-    const f2w r0 = fm(x2, (f2w) c[1], (f2w) c[0]), r1 = fm(x2, (f2w) c[3], (f2w) c[2]), r2 = fm(x2, (f2w) c[5], (f2w) c[4]),
-              r3 = fm(x2, (f2w) c[7], (f2w) c[6]), r4 = fm(x2, (f2w) c[9], (f2w) c[8]);
-    const f2w x4 = x2 * x2;
-    const f2w q0 = fm(x4, r1, r0), q1 = fm(x4, r3, r2), q2 = r4;
-    const f2w x8 = x4 * x4;
-    const f2w w0 = fm(x8, q1, q0), w1 = q2;
-    const f2w x16 = x8 * x8;
-    const f2w g = fm(x16, w1, w0);
-    return f2w{vmax(g.x, 0.f), vmax(g.y, 0.f)};
-}
-/* union_weight of cells (cell, cell + 1) of a footprint starting at x0 with argument r, zero outside [lo, hi):
- * the arguments r + (cell - x0) as union_weight forms them */
-AD f2w union_weight2(const FilterCoeffs &F, float r, int x0, int cell, int lo, int hi) {
-    const f2w w = gaussian_eval2(F, f2w{r + (float) (cell - x0), r + (float) (cell + 1 - x0)});
-    return f2w{(cell >= lo && cell < hi) ? w.x : 0.f, (cell + 1 >= lo && cell + 1 < hi) ? w.y : 0.f};
-}
-
 /* union box of the active footprints of the lane's 16-lane row (every lane of the wave active) */
 struct RowBox { int x0, y0, x1, y1; };
 AD RowBox row_box(const Foot &f, bool act) {
@@ -1215,33 +1188,16 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
          * straight-line code, not a branch per evaluation */
         const FilterCoeffs F = default_filter();
         float wx[6];
-        if (AMVPT_SPLAT_PKW) {
 #pragma unroll
-            for (int c = 0; c < 6; c += 2) {
-                const f2w w = union_weight2(F, f.rx, f.x0, ux0 + c, x0c, x1);
-                wx[c] = w.x;
-                wx[c + 1] = w.y;
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < 6; ++c) wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
-        }
+        for (int c = 0; c < 6; ++c) wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
         WinT *const wch = wbase + ch * wn.plane;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
             /* row position r + 3 h holds union row r + 3 (h ^ b2); the quad shares b2 */
             float Ky[2], B1y[2], B2y[2], B3y[2];
-            float wyh[2];
-            if (AMVPT_SPLAT_PKW) {
-                /* rows uy0 + r + 3 (h ^ b2), h = 0, 1: a pair of arguments 3 rows apart */
-                const int ra = uy0 + r + 3 * b2, rb = uy0 + r + 3 * (1 ^ b2);
-                const f2w w = gaussian_eval2(F, f2w{f.ry + (float) (ra - f.y0), f.ry + (float) (rb - f.y0)});
-                wyh[0] = (ra >= y0c && ra < y1) ? w.x : 0.f;
-                wyh[1] = (rb >= y0c && rb < y1) ? w.y : 0.f;
-            }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const float wy = AMVPT_SPLAT_PKW ? wyh[h] : union_weight(F, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1);
+                const float wy = union_weight(F, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1);
                 Ky[h] = K * wy;
                 B1y[h] = B1 * dpp_f<DPP_XOR1>(wy);
                 B2y[h] = B2 * dpp_f<DPP_XOR2>(wy);
