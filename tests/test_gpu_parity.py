@@ -229,6 +229,22 @@ def test_sphere_grazing_rays(gpu_ready, amvpt_mod, oracle, mode):
         amvpt_mod.set_traversal(0)
 
 
+@pytest.mark.parametrize("n_spheres", [64, 70], ids=["deferred_64", "in_place_70"])
+def test_many_spheres(gpu_ready, amvpt_mod, oracle, n_spheres):
+    """A field of small spheres in the Cornell box (with the two cubes): 64 spheres take the deferred float64
+    tests of the wave-uniform walks (one 64-bit mask), 70 the in-place tests; the suffix walks the per-lane
+    BVH with spheres -- records bit-identical to the oracle either way."""
+    xml = open(os.path.join(SCENES, "cbox_grid.xml")).read()
+    balls = []
+    for i in range(n_spheres):
+        x, y, z = -0.8 + 0.2 * (i % 9), -0.9 + 0.22 * ((i // 9) % 9), -0.6 + 0.45 * (i // 81)
+        balls.append('<shape type="sphere"><point name="center" x="%.3f" y="%.3f" z="%.3f"/>'
+                     '<float name="radius" value="0.07"/><ref id="white"/></shape>' % (x, y, z))
+    xml = xml.replace("</scene>", "\n".join(balls) + "\n</scene>")
+    s = amvpt_mod.load_string(xml, res=16, spp=16, gx=4, gy=2, reuse=8)
+    _check(amvpt_mod, oracle, s)
+
+
 @pytest.mark.parametrize("defines", [
     dict(distr="beckmann"),                                            # the reference's default model
     dict(distr="beckmann", vis="false"),
