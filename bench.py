@@ -240,7 +240,7 @@ def main():
     hbar = c["reuse_lanes"] / max(1, lanes)
     stage_ms = {"primary": c["kernel_ms_primary"], "bounce": c["kernel_ms_bounce"], "splat": c["kernel_ms_splat"]}
     kms, kl = c["kernel_ms"], c["kernel_launches"]
-    bytes_kernel = kernel_bytes(c, G, C)
+    bytes_kernel = kernel_bytes(c, G, C, min(p.adaptive, G - 1) if G > 1 else 0)
     # the dominant single kernel (HIP events around each launch on the render stream)
     dom = max((k for k in kms if kl[k]), key=lambda k: kms[k])
     launches = kl[dom]
@@ -270,6 +270,13 @@ def main():
     rmse = None
     if rank == 0 and args.rmse_lanes > 0 and not p.adaptive:
         rmse = rmse_window(dev, sd, vd, p, plan, args.rmse_lanes, stream)
+    elif rank == 0 and args.rmse_lanes > 0:
+        # the adaptive fill compacts and re-traces over the WHOLE pass, so no lane window of the full-size
+        # frame can include it: the same workload at reduced view size, whole frame, fill included (and, on
+        # one GPU, the oracle's time for it is the CPU baseline's sample)
+        rmse, cpu_small = rmse_reduced_frame(scene_file, cfg, stream)
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_small
 
     if rank == 0:
         out = {
@@ -342,7 +349,7 @@ def main():
             "cpu_baseline": cpu,
             "counters": {k: c[k] for k in ("lanes", "vertices", "reuse_lanes", "visibility_rays", "view_splats",
                                              "nonfinite_samples", "negative_samples", "record_bytes",
-                                             "splat_fallback", "pushed_paths", "film_overflow")},
+                                             "splat_fallback", "pushed_paths", "film_overflow", "film_range_drops")},
         }
         print(json.dumps(out))
     if world > 1:
@@ -381,7 +388,46 @@ def rmse_window(dev, sd, vd, p, plan, n, stream):
             "oracle_seconds": round(st["seconds"], 2)}
 
 
-def kernel_bytes(c, G, C):
+def rmse_reduced_frame(scene_file, cfg, stream, res=64):
+    """Adaptive configs: per-pixel RMSE (developed) of the whole frame of the same workload with `res`^2
+    views (grid, spp, groups and adaptive kept), HIP pipeline vs the CPU oracle -- the adaptive fill
+    (mvpath_multi.h:52-59,79-115) included; and the oracle's time for that frame as a CPU baseline."""
+    import torch
+    import amvpt
+    from amvpt import compare
+    from oracle import oracle as O
+    small = dict(cfg, res=res)
+    s = amvpt.load_file(os.path.join(REPO, "scenes", scene_file), **small)
+    sd, vd, p = s.describe(0, 0, 0)
+    spp, spp_pp, n_passes, lanes_per_pass = amvpt.plan(p)
+    C = 5 if p.film_alpha else 4
+    dev = amvpt.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, C), dtype=torch.float32, device="cuda")
+    cnt = amvpt.Counters()
+    dev.render_ex(vd, p, film.data_ptr(), stream=stream, counters=cnt)
+    torch.cuda.synchronize()
+    g = film.cpu().numpy()
+    del film
+    threads, machine = host_cores()
+    O.build()
+    o, _, st = O.render(sd, vd, p, threads=threads)
+    touched = (g[..., -1] != 0) | (o[..., -1] != 0)
+    m = compare.metrics(O.develop(g)[touched], O.develop(o)[touched])
+    lanes = lanes_per_pass * n_passes
+    rmse = {"rmse": m["rmse"], "max_abs": m["max_abs"], "pixels": int(touched.sum()),
+            "window": "the whole frame of the workload at %dx%d per view (quilt %dx%d, %d lanes + %d adaptive "
+                      "re-traces on the GPU, %d in the oracle)" % (res, res, p.film_width, p.film_height, lanes,
+                                                                   cnt.adaptive_lanes, st["adaptive_lanes"]),
+            "reference": "CPU oracle (restatement of mvpath, not Dr.Jit llvm_rgb)",
+            "oracle_seconds": round(st["seconds"], 2)}
+    cpu = {"value": round(lanes / st["seconds"] / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+           "host_cpus": machine, "kind": "port",
+           "sample": "the whole %dx%d-per-view frame above, adaptive fill included (%.1f s); CPU restatement of "
+                     "mvpath (oracle/, brute-force intersection), not Dr.Jit llvm_rgb" % (res, res, st["seconds"])}
+    return rmse, cpu
+
+
+def kernel_bytes(c, G, C, n_adapt=0):
     """Algorithmic HBM bytes per frame of each kernel: every SoA
     stream element is written once by its producer and read once by its consumer."""
     lanes, verts, shadow = c["lanes"], c["vertices"], c["shadow_rays"]
@@ -407,6 +453,8 @@ def kernel_bytes(c, G, C):
         # fused suffix (brute-force scenes): each path's state in once, its result out once; the
         # vertices in between stay in registers
         "k_suffix": (state + 16) * pushed,
+        # the adaptive fill's compaction: 1 B of mask per lane in, 4 B per selected lane out
+        "k_select": lanes + 4 * adapt / max(1, n_adapt),
     }
 
 

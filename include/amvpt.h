@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 8
+#define AMVPT_ABI_VERSION 9
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -211,6 +211,9 @@ typedef struct amvpt_counters {
     /* ABI 8 */
     uint64_t pushed_paths;      /* paths that left the primary vertex into the shared suffix (byte model of the suffix) */
     uint64_t film_overflow;     /* film floats added to the overflow list (cells outside an amvpt_film_window) */
+    /* ABI 9 */
+    uint64_t film_range_drops;  /* AMVPT_OPT_DETERMINISTIC: finite footprint-cell adds of |v| >= 2^31 the fixed-point
+                                 * film cannot hold, dropped (ImageBlock::put would add them; 0 otherwise) */
 } amvpt_counters;
 
 /* kernels of the pipeline, for amvpt_counters.kernel_ms */
@@ -225,7 +228,8 @@ typedef enum amvpt_kernel_id {
     AMVPT_K_SHADOW = 7,        /* suffix NEE any-hit                      */
     AMVPT_K_SPLAT = 8,         /* ImageBlock::put                         */
     AMVPT_K_SUFFIX = 9,        /* ABI 7: the whole suffix in one launch (closest hit + shading + NEE, brute-force scenes) */
-    AMVPT_K_COUNT = 10
+    AMVPT_K_SELECT = 10,       /* ABI 9: the adaptive fill's compaction of the adapt_mask lanes (k_select_flagged) */
+    AMVPT_K_COUNT = 11
 } amvpt_kernel_id;
 
 typedef struct amvpt_scene amvpt_scene; /* opaque device-resident scene */
@@ -372,8 +376,8 @@ enum {
                                        * integer atomics (order-independent), added to the film once at the
                                        * end; each footprint-cell add is rounded to a multiple of 2^-32 and
                                        * must stay below 2^31 in magnitude: non-finite values (counted by
-                                       * nonfinite_samples) and finite ones of |v| >= 2^31 (not counted) are
-                                       * dropped; needs a whole-quilt film window */
+                                       * nonfinite_samples) and finite ones of |v| >= 2^31 (counted per cell
+                                       * add by film_range_drops) are dropped; needs a whole-quilt film window */
 };
 typedef struct amvpt_render_opts {
     uint64_t chunk_lanes;             /* 0: automatic (see amvpt_set_chunk_lanes) */

@@ -77,7 +77,7 @@ class Counters(ctypes.Structure):
                 ("total_ms", f64), ("splat_fallback", u64),
                 ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12),
                 ("record_bytes", u64), ("nonfinite_samples", u64), ("negative_samples", u64),
-                ("pushed_paths", u64), ("film_overflow", u64)]
+                ("pushed_paths", u64), ("film_overflow", u64), ("film_range_drops", u64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -133,7 +133,7 @@ def wrap_run_exchange(fn):
 
 # amvpt_kernel_id (include/amvpt.h): index -> name of Counters.kernel_ms / kernel_launches
 KERNELS = ("k_prim_hit", "k_prim_req", "k_vis", "k_mv_primary", "k_raygen", "k_extend", "k_bounce", "k_shadow",
-           "k_splat", "k_suffix")
+           "k_splat", "k_suffix", "k_select")
 
 
 INTEGRATOR_MVPATH, INTEGRATOR_PATH = 0, 1

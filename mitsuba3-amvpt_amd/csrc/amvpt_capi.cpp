@@ -78,11 +78,19 @@ static uint32_t g_bvh_max_leaf = 4;
 static float g_bvh_trav_cost = 0.f;
 /* depth of the LDS treelets (dscene.h DScene::tnodes), 0: none (A/B builds: EXTRA=-DAMVPT_TREELET_DEPTH=n);
  * 2^depth - 1 nodes at most, 32 B each */
+#ifndef AMVPT_TREELETS
+#define AMVPT_TREELETS 0   /* the walks that stage treelets (amvpt_render.hip); 0: none, so none are built */
+#endif
 #ifndef AMVPT_TREELET_DEPTH
-#define AMVPT_TREELET_DEPTH 8
+#define AMVPT_TREELET_DEPTH ((AMVPT_TREELETS & 5) ? 8 : 0)   /* any-hit walks (k_shadow, k_vis): 255 nodes, 8 KB */
 #endif
 #ifndef AMVPT_OCT_TREELET_DEPTH
-#define AMVPT_OCT_TREELET_DEPTH 6   /* the 8 octant treelets of the closest-hit walks: 8 x 63 nodes, 16 KB */
+#define AMVPT_OCT_TREELET_DEPTH ((AMVPT_TREELETS & 2) ? 6 : 0)   /* closest hit: 8 octant treelets, 8 x 63 nodes, 16 KB */
+#endif
+/* direction-octant node orderings for the per-lane closest-hit walks of large BVHs (A/B builds:
+ * EXTRA=-DAMVPT_OCT_BVH=0 keeps one copy); a build-time choice, never a process-global knob */
+#ifndef AMVPT_OCT_BVH
+#define AMVPT_OCT_BVH 1
 #endif
 static const uint32_t g_treelet_depth = AMVPT_TREELET_DEPTH, g_oct_treelet_depth = AMVPT_OCT_TREELET_DEPTH;
 
@@ -569,21 +577,23 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         b.nodes.resize(1);
         b.build(0, 0, (uint32_t) bprims.size(), 0);
         nodes.reserve(b.nodes.size());
-        std::vector<std::vector<uint32_t>> gpos(8, std::vector<uint32_t>(b.nodes.size(), 0u));
-        b.flatten(0, nodes, 0, 0, &gpos[0]);
+        /* per-ordering positions of the build nodes: only the treelet builds read them */
+        const bool want_pos = g_treelet_depth > 0 || g_oct_treelet_depth > 0;
+        std::vector<std::vector<uint32_t>> gpos(want_pos ? 8 : 1);
+        if (want_pos) for (auto &g : gpos) g.assign(b.nodes.size(), 0u);
+        b.flatten(0, nodes, 0, 0, want_pos ? &gpos[0] : nullptr);
         if (nodes.size() > kNodeSkipMask) {
             set_error("BVH too large (more than 2^28 nodes)");
             return AMVPT_ERR_INVALID;
         }
         /* per-lane walks of BVHs that are neither wave-uniform nor LDS-staged read the copy of
          * their ray's direction octant: nearest child first, so the closest hit shrinks the
-         * box-test range early (AMVPT_OCT_BVH=0: one copy, A/B) */
-        const char *e = std::getenv("AMVPT_OCT_BVH");
+         * box-test range early */
         const uint32_t n0 = (uint32_t) nodes.size();
         const uint64_t lds_b = (uint64_t) n0 * sizeof(DNode) + bprims.size() * sizeof(DPrim);
-        if (!(e && e[0] == '0') && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes && (uint64_t) n0 * 8 <= kNodeSkipMask) {
+        if (AMVPT_OCT_BVH && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes && (uint64_t) n0 * 8 <= kNodeSkipMask) {
             nodes.reserve((size_t) n0 * 8);
-            for (uint32_t o = 1; o < 8; ++o) b.flatten(0, nodes, o, o * n0, &gpos[o]);
+            for (uint32_t o = 1; o < 8; ++o) b.flatten(0, nodes, o, o * n0, want_pos ? &gpos[o] : nullptr);
             oct_stride = n0;
         }
         /* LDS treelets for BVHs the walks read from global memory (neither wave-uniform-small nor staged

@@ -21,7 +21,6 @@
  * stream: one dwordx4 load/store per lane, 1 KiB per wave instruction).
  */
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
@@ -125,6 +124,7 @@ struct KParams {
     uint32_t vs_stride;   /* Bufs::vstate: floats between a field's consecutive view slots (the chunk) */
     unsigned long long *film_fx;   /* deterministic mode: 32.32 fixed-point shadow of the film (else null) */
     float *film_base;              /* the film the shadow mirrors (film_fx index = film float index) */
+    unsigned long long *fx_drops;  /* deterministic mode: sharded count of finite cell adds out of the 32.32 range */
     /* stock `path` over several passes (integrator.cpp:279-330): the sampler is seeded once and every
      * pass continues each lane's PCG32 stream -- rng_in (passes > 0) holds the state each lane starts the
      * pass with, rng_out (all but the last pass) receives the state its path ends with; both indexed by
@@ -694,7 +694,10 @@ constexpr double kFixScale = 4294967296.0, kFixLimit = 2147483647.0;
 template <bool kDet = true> AD void film_add(const KParams &P, float *p, float v) {
     if (kDet && P.film_fx) {
         const double d = (double) v * kFixScale;
-        if (!(fabs(d) < kFixLimit * kFixScale)) return;   /* NaN / Inf / out of range */
+        if (!(fabs(d) < kFixLimit * kFixScale)) {   /* NaN / Inf (counted per sample by check_sample) / out of range */
+            if (P.fx_drops && __builtin_isfinite(v)) atomicAdd(P.fx_drops + blockIdx.x % 256u, 1ull);   /* kStatShards */
+            return;
+        }
         atomicAdd(P.film_fx + (p - P.film_base), (unsigned long long) (long long) __builtin_rint(d));
         return;
     }
@@ -1450,7 +1453,8 @@ AD unsigned long long wave_sum(unsigned long long v) {
 }
 /* lane counters: stats[s * kStatShards + shard], one shard per block residue (summed on
  * the host), so the per-wave adds never pile onto one word */
-constexpr uint32_t kStatShards = 256, kStats = 9;   /* [8]: paths pushed into the suffix */
+constexpr uint32_t kStatShards = 256, kStats = 10;   /* [8]: paths pushed into the suffix, [9]: deterministic-film range drops */
+static_assert(kStatShards == 256, "film_add shards its range-drop count by blockIdx % 256");
 AD void stat_add(unsigned long long *stats, uint32_t which, unsigned long long v) {
     v = wave_sum(v);
     if (__lane_id() == 0 && v) atomicAdd(stats + which * kStatShards + blockIdx.x % kStatShards, v);
@@ -3647,7 +3651,94 @@ static const splat_fn kSplat[] = {launch_splat<0>, launch_splat<-1>, launch_spla
                                   launch_splat<13>, launch_splat<14>, launch_splat<15>, launch_splat<16>};
 constexpr uint32_t kMaxG = 16;
 static uint32_t dispatch_g(uint32_t G) { return G > kMaxGWide ? 1u : G > kMaxG ? 0u : G; }
-constexpr uint64_t kSelectChunk = 1ull << 30;
+/*
+ * The adaptive fill's compaction (dr::compress, mvpath_multi.h:79-88): the virtual indices of the pass's
+ * adapt_mask lanes, in lane order, in ONE pass over the mask with decoupled look-back.
+ *  - A block takes the next tile of kSelTile lanes by ticket (one returning atomic per block), so every earlier
+ *    tile belongs to a block that is already running and will publish: the look-back always ends.
+ *  - Each thread reads 16 mask bytes (one 16-B load) into a 16-bit flag word; a wave inclusive scan of the
+ *    per-thread counts and a 4-wave sum in LDS give the block's count and every thread's offset in it.
+ *  - The block publishes its count (kSelAgg), then wave 0 reads the predecessors' status words 64 tiles per
+ *    step (a ballot finds the nearest published inclusive prefix, kSelInc; an unpublished word in front of it
+ *    is read again) and sums them; the tile publishes its inclusive prefix.
+ *  - Every thread writes its flagged lanes' indices at tile prefix + wave prefix + thread prefix: ascending
+ *    lane order, as dr::compress keeps it.  The last tile writes the total.
+ * Status words are 64-bit (2 flag bits, 62 value bits), zeroed with the ticket before the launch.
+ */
+constexpr uint32_t kSelTile = 256 * 16;
+constexpr unsigned long long kSelAgg = 1ull << 62, kSelInc = 2ull << 62, kSelVal = kSelAgg - 1;
+AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_select_flagged(const uint8_t *amask, uint64_t n, uint32_t *out,
+                                                                      uint32_t *count, unsigned long long *status,
+                                                                      uint32_t *ticket, uint32_t n_tiles) {
+    __shared__ uint32_t s_tile, s_wave[4];
+    __shared__ unsigned long long s_prefix;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t base = (uint64_t) tile * kSelTile + (uint64_t) threadIdx.x * 16u;
+    uint32_t bits = 0;   /* bit i: lane base + i is flagged */
+    if (base + 16 <= n) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(amask + base);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bits |= (((w[k] >> (8 * b)) & 0xffu) != 0u ? 1u : 0u) << (4 * k + b);
+    } else {
+        for (int i = 0; i < 16; ++i)
+            if (base + i < n && amask[base + i]) bits |= 1u << i;
+    }
+    const uint32_t c = (uint32_t) __builtin_popcount(bits);
+    const int lane = (int) __lane_id(), wave = (int) (threadIdx.x >> 6);
+    uint32_t inc = c;   /* wave inclusive scan */
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    uint32_t wpre = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t t = s_wave[k];
+        wpre += k < wave ? t : 0u;
+        total += t;
+    }
+    if (wave == 0) {
+        unsigned long long excl = 0;
+        if (tile == 0) {
+            if (lane == 0) __hip_atomic_store(status, kSelInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(status + tile, kSelAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t) tile - 1;   /* the nearest predecessor not summed yet */
+            for (;;) {
+                const int64_t t = j - lane;
+                const unsigned long long v =
+                    t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kSelInc;
+                const unsigned long long inc_m = __ballot((v >> 62) == 2ull), zero_m = __ballot((v >> 62) == 0ull);
+                /* lanes up to and including the nearest inclusive prefix (all 64 when there is none) */
+                const unsigned long long upto = inc_m ? ((inc_m & (~inc_m + 1ull)) << 1) - 1ull : ~0ull;
+                if (zero_m & upto) continue;   /* a predecessor has not published yet: read again */
+                excl += wave_sum(((upto >> lane) & 1ull) ? (v & kSelVal) : 0ull);
+                if (inc_m) break;
+                j -= 64;
+            }
+            if (lane == 0) __hip_atomic_store(status + tile, kSelInc | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_prefix = excl;
+            if (tile == n_tiles - 1) *count = (uint32_t) (excl + total);
+        }
+    }
+    __syncthreads();
+    uint32_t o = (uint32_t) s_prefix + wpre + (inc - c);
+    while (bits) {
+        const int i = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        out[o++] = (uint32_t) (base + (uint64_t) i);
+    }
+}
 
 /* adaptive fill: flagged lanes of each run of a rectangular lane set (one block per run) */
 AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_run_counts(const uint8_t *amask, uint32_t run_len, uint32_t *counts) {
@@ -3965,6 +4056,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         HIPCHK(hipMemsetAsync(A.fx, 0, film_floats * 8, st));
         P.film_fx = (unsigned long long *) A.fx;
         P.film_base = film;
+        P.fx_drops = dstats + 9 * kStatShards;
     }
 
     /* multi-pass stock path: the per-lane sampler states between passes, two planes used in turn */
@@ -3978,17 +4070,20 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* adaptive fill buffers: per-lane mask + compacted lane list for a whole pass */
     uint8_t *d_amask = nullptr;
     uint32_t *d_asel = nullptr, *d_anum = nullptr, *d_runs = nullptr, *d_delta = nullptr;
-    void *d_cub = nullptr;
-    size_t cub_bytes = 0;
+    unsigned long long *d_sel_status = nullptr;
+    uint32_t *d_sel_ticket = nullptr;
     const uint64_t span_all = span;
     const size_t runs_bytes = 4 * (((size_t) n_runs + 63) & ~(size_t) 63);
-    const uint64_t sel_max = std::min<uint64_t>(span_all, kSelectChunk);
+    /* k_select_flagged: one status word per tile + the ticket */
+    const uint32_t sel_tiles = (uint32_t) ((span_all + kSelTile - 1) / kSelTile);
+    const size_t sel_bytes = 8 * (((size_t) sel_tiles + 31) & ~(size_t) 31) + 256;
+    if (do_fill && span_all > 0xffffffffull) {
+        set_error("amvpt_render: adaptive fill over a lane set of 2^32 or more lanes (32-bit lane indices)");
+        return AMVPT_ERR_UNSUPPORTED;
+    }
     if (do_fill) {
-        HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, cub_bytes, hipcub::CountingInputIterator<uint32_t>(0),
-                                             (const uint8_t *) nullptr, (uint32_t *) nullptr, (uint32_t *) nullptr,
-                                             (int) sel_max, st));
         const size_t abytes = ((span_all + 255) & ~(uint64_t) 255) + 4 * ((span_all + 63) & ~(uint64_t) 63) + 256 +
-                              2 * runs_bytes + cub_bytes + 256;
+                              2 * runs_bytes + sel_bytes;
         { const amvpt_status as_ = arena_reserve(A, A.adapt, A.abytes, abytes, "adaptive buffers"); if (as_ != AMVPT_OK) return as_; }
         char *ap = (char *) A.adapt;
         d_amask = (uint8_t *) ap; ap += (span_all + 255) & ~(uint64_t) 255;
@@ -3996,7 +4091,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         d_anum = (uint32_t *) ap; ap += 256;
         d_runs = (uint32_t *) ap; ap += runs_bytes;     /* flagged lanes per run (rect lane sets) */
         d_delta = (uint32_t *) ap; ap += runs_bytes;    /* run_delta */
-        d_cub = ap;
+        d_sel_status = (unsigned long long *) ap;
+        d_sel_ticket = (uint32_t *) (ap + sel_bytes - 256);
     }
 
     /* one buffer set per chunk stream: queues A / B and their counters, the chunk's lane arena */
@@ -4178,22 +4274,28 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             if (n_sets < 2) T.flush();
             HIPCHK(T.err);
         }
+        /* the stock path's next pass reads the sampler states this pass writes (and writes the plane this
+         * pass read): with two chunk streams, chunk c of the next pass may run on the other stream than chunk
+         * c of this one, so both streams meet at every pass boundary (the next side chunk forks again) */
+        if (rng_carry) arena_release.join();
         if (do_fill) {
             /* the fill reads the whole pass's adapt_mask: both chunk streams first */
             arena_release.join();
             RoctxScope range_fill("amvpt adaptive fill");
             /* compact the pass's adapt_mask lanes in lane order (virtual indices of the lane set,
              * ascending = lane order), then n_adapt re-traces each */
-            /* (hipcub counts in int: select in pieces of <= 2^30 lanes, appending) */
             uint64_t n_sel = 0;
-            for (uint64_t s0 = 0; s0 < span_all; s0 += kSelectChunk) {
-                const uint64_t sn = std::min<uint64_t>(kSelectChunk, span_all - s0);
-                HIPCHK(hipcub::DeviceSelect::Flagged(d_cub, cub_bytes, hipcub::CountingInputIterator<uint32_t>((uint32_t) s0),
-                                                     d_amask + s0, d_asel + n_sel, d_anum, (int) sn, st));
+            {
+                HIPCHK(hipMemsetAsync(d_sel_status, 0, sel_bytes, st));   /* status words + ticket */
+                T.begin(AMVPT_K_SELECT, st);
+                hipLaunchKernelGGL(k_select_flagged, dim3(sel_tiles), dim3(256), 0, st, (const uint8_t *) d_amask, span_all,
+                                   d_asel, d_anum, d_sel_status, d_sel_ticket, sel_tiles);
+                T.end(st);
+                HIPCHK(hipGetLastError());
                 uint32_t got = 0;
                 HIPCHK(hipMemcpyAsync(&got, d_anum, 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
-                n_sel += got;
+                n_sel = got;
             }
             /* this render's place in the pass's compressed array: per run, the flagged lanes of the
              * whole pass below it (one exchange per pass), as run_delta = global - local prefix */
@@ -4312,6 +4414,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.negative_samples = hs[7];
         c.pushed_paths = hs[8];
         c.film_overflow = overflow_added;   /* this render's cells (renders append to the list) */
+        c.film_range_drops = hs[9];
         T.flush();
         HIPCHK(T.err);
         for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }

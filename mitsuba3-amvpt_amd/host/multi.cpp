@@ -388,6 +388,7 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
                 c.shadow_rays += o.shadow_rays; c.nonfinite_samples += o.nonfinite_samples;
                 c.negative_samples += o.negative_samples; c.pushed_paths += o.pushed_paths;
                 c.film_overflow += o.film_overflow;
+                c.film_range_drops += o.film_range_drops;
                 c.total_ms = std::max(c.total_ms, o.total_ms);
                 c.kernel_ms_primary = std::max(c.kernel_ms_primary, o.kernel_ms_primary);
                 c.kernel_ms_bounce = std::max(c.kernel_ms_bounce, o.kernel_ms_bounce);

@@ -171,6 +171,8 @@ static void sensor_parts(const Properties &p, FilmInfo &film, SamplerInfo &samp)
             std::string c = wrap_class(o);
             if (c == "film") { if (hf) Throw("Only one film can be specified per sensor."); film = make_film(unwrap(o)); hf = true; }
             else if (c == "sampler") { if (hs) Throw("Only one sampler can be specified per sensor."); samp = make_sampler(unwrap(o)); hs = true; }
+            else continue;
+            p.mark_queried(e.first);   /* the sensor read its film / sampler, wrapped or not */
         }
     }
     if (!hf) film = FilmInfo();
@@ -715,6 +717,15 @@ static void build(amvpt_host_scene &S) {
             }
             S.shapes.push_back(d);
         }
+    }
+    /* the reference's loader instantiates every child of the scene, so a top-level BSDF no shape uses (or only
+     * a removed <ref> did) still has its constructor read its keys: build such BSDFs into a scratch scene (their
+     * keys marked read, their errors raised) without adding them to the device tables */
+    {
+        amvpt_host_scene scratch;
+        std::map<const Object *, int> scratch_seen;
+        for (auto &e : rp.objects())
+            if (e.second->tag == "bsdf" && !seen.count(e.second)) (void) add_bsdf(scratch, scratch_seen, *e.second);
     }
     if (!have_integrator) {
         /* Scene default: path integrator */

@@ -422,7 +422,9 @@ static void check_object(const Object &o, std::vector<const Object *> &seen) {
     /* children first: the loader instantiates (and checks) them before their parent */
     for (auto &e : o.props.entries)
         if (e.second.kind == Properties::Obj) check_object(*e.second.o, seen);
-    if (o.wrapped || o.tag == "wrap") return;   /* Wrap marks its properties queried (wrap.cpp:12-14) */
+    /* Wrap marks its own properties queried (wrap.cpp:12-14); the plugin it creates reads a copy of them
+     * (unwrap), and its XML children were instantiated, and are checked, as any other */
+    if (o.tag == "wrap") return;
     const std::string near = "\"" + o.src + "\" (near line " + std::to_string(o.line) + ")";
     const std::string type = o.tag == "scene" ? "scene" : o.props.plugin;
     std::vector<std::string> names;

@@ -116,9 +116,6 @@ struct Object {
     std::string base_dir;  /* root only: directory of the scene file (FileResolver for `filename`) */
     std::string src;       /* the scene file (or "<string>") and the line of the object's tag, for error messages */
     int line = 0;
-    /* instantiated through a Wrap (Wrap::create_instance -> PluginManager, not the XML loader): no
-     * unreferenced-property check, as in the reference */
-    mutable bool wrapped = false;
     virtual ~Object() = default;
 };
 

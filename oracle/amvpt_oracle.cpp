@@ -1037,6 +1037,21 @@ struct Film {
     Gaussian g;
     float *data;
     int ox = 0, oy = 0;   /* ImageBlock offset (the hdrfilm crop offset, mvpath.cpp:168) */
+    /* fixed-point film (oracle_set_fixed_film; the device's AMVPT_OPT_DETERMINISTIC film, include/amvpt.h):
+     * each cell add is rounded to a multiple of 2^-32 and summed as an integer, so the sum does not depend
+     * on the order of the adds; finite adds of |v| >= 2^31 are dropped and counted, non-finite ones dropped */
+    int64_t *fx = nullptr;
+    uint64_t *drops = nullptr;
+    void add(float *ptr, float v) const {
+        if (!fx) { *ptr += v; return; }
+        const double d = (double) v * 4294967296.0;
+        if (!(std::fabs(d) < 2147483647.0 * 4294967296.0)) {
+            if (std::isfinite(v)) ++*drops;
+            return;
+        }
+        int64_t &c = fx[ptr - data];
+        c = (int64_t) ((uint64_t) c + (uint64_t) (int64_t) std::rint(d));   /* two's-complement wrap, as the device's u64 atomics */
+    }
     void put(V2 pos, const float *values, bool active, bool coalesce) const {
         if (!active) return;
         if (box) {
@@ -1045,7 +1060,7 @@ struct Film {
             uint32_t ux = (uint32_t) px, uy = (uint32_t) py;
             if (!(ux < W && uy < H)) return;
             float *ptr = data + ((size_t) uy * W + ux) * C;
-            for (uint32_t k = 0; k < C; ++k) ptr[k] += values[k];
+            for (uint32_t k = 0; k < C; ++k) add(ptr + k, values[k]);
             return;
         }
         float radius = g.radius;
@@ -1068,7 +1083,7 @@ struct Film {
                     bool a2 = a1 && (u0x + xs <= u1x);
                     if (!a2) continue;
                     float *ptr = data + ((size_t) (u0y + ys) * W + (u0x + xs)) * C;
-                    for (uint32_t k = 0; k < C; ++k) ptr[k] += values[k] * w;
+                    for (uint32_t k = 0; k < C; ++k) add(ptr + k, values[k] * w);
                 }
             }
             return;
@@ -1087,7 +1102,7 @@ struct Film {
                 bool a2 = a1 && (x + xs < W);
                 if (!a2) continue;
                 float *ptr = data + ((size_t) (y + ys) * W + (x + xs)) * C;
-                for (uint32_t k = 0; k < C; ++k) ptr[k] += values[k] * w;
+                for (uint32_t k = 0; k < C; ++k) add(ptr + k, values[k] * w);
             }
         }
     }
@@ -1666,7 +1681,11 @@ static oracle_run_exchange_fn g_run_exchange = nullptr;
 static void *g_run_exchange_ctx = nullptr;
 void oracle_set_run_exchange(oracle_run_exchange_fn fn, void *ctx) { g_run_exchange = fn; g_run_exchange_ctx = ctx; }
 
-struct oracle_stats { uint64_t lanes, vertices, reuse_lanes, visibility_rays, adaptive_lanes; double seconds; };
+struct oracle_stats { uint64_t lanes, vertices, reuse_lanes, visibility_rays, adaptive_lanes; double seconds; uint64_t range_drops; };
+/* the device's deterministic film (AMVPT_OPT_DETERMINISTIC) restated: 32.32 fixed-point cell sums, resolved
+ * into the f32 film once at the end (k_fixed_resolve); 0: the f32 film of ImageBlock::put */
+static bool g_fixed_film = false;
+void oracle_set_fixed_film(int on) { g_fixed_film = on != 0; }
 
 /*
  * Render [lane_begin, lane_end) of every pass into `film` (host memory, H*W*C
@@ -1754,6 +1773,9 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
 
     std::atomic<uint64_t> a_vert{0}, a_reuse{0}, a_vis{0}, a_adapt{0};
     std::vector<std::vector<float>> films(n_threads);
+    const bool fixed = g_fixed_film;
+    std::vector<std::vector<int64_t>> fxs(fixed ? n_threads : 0);
+    std::vector<uint64_t> drops(n_threads, 0);
 
     for (uint32_t pass = 0; pass < n_passes; ++pass) {
         uint32_t seed_value = P.base_seed + (is_mv ? (spp_pp * pass + P.seed) : P.seed);
@@ -1765,6 +1787,11 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
             if (tf.empty()) tf.assign((size_t) W * H * C, 0.f);
             Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, tf.data(), ox, oy};
             film.g.init(P.rfilter_stddev);
+            if (fixed) {
+                if (fxs[tid].empty()) fxs[tid].assign((size_t) W * H * C, 0);
+                film.fx = fxs[tid].data();
+                film.drops = &drops[tid];
+            }
             Renderer R(sc, views, P);
             R.G = G;
             uint64_t verts = 0;
@@ -1890,6 +1917,7 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
                 auto aworker = [&](int tid) {
                     Film film{W, H, C, P.rfilter == AMVPT_RFILTER_BOX, {}, films[tid].data(), ox, oy};
                     film.g.init(P.rfilter_stddev);
+                    if (fixed) { film.fx = fxs[tid].data(); film.drops = &drops[tid]; }
                     Renderer R(sc, views, P);
                     R.G = G;
                     uint64_t verts = 0;
@@ -1919,9 +1947,18 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
         }
     }
     size_t n = (size_t) W * H * C;
-    for (int t = 0; t < n_threads; ++t)
-        if (!films[t].empty())
-            for (size_t i = 0; i < n; ++i) film[i] += films[t][i];
+    if (fixed) {
+        /* integer sums (order-free), then the device's k_fixed_resolve conversion */
+        std::vector<uint64_t> tot(n, 0);
+        for (int t = 0; t < n_threads; ++t)
+            if (!fxs[t].empty())
+                for (size_t i = 0; i < n; ++i) tot[i] += (uint64_t) fxs[t][i];
+        for (size_t i = 0; i < n; ++i) film[i] += (float) ((double) (int64_t) tot[i] * (1.0 / 4294967296.0));
+    } else {
+        for (int t = 0; t < n_threads; ++t)
+            if (!films[t].empty())
+                for (size_t i = 0; i < n; ++i) film[i] += films[t][i];
+    }
     if (stats) {
         stats->lanes = (lane_end - lane_begin) * (uint64_t) n_passes;
         stats->vertices = a_vert;
@@ -1929,6 +1966,8 @@ static int render_core(const amvpt_scene_desc *sd, const amvpt_view_desc *views,
         stats->visibility_rays = a_vis;
         stats->adaptive_lanes = a_adapt;
         stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        stats->range_drops = 0;
+        for (uint64_t d : drops) stats->range_drops += d;
     }
     return 0;
 }

@@ -19,7 +19,7 @@ _lib = None
 class OracleStats(ctypes.Structure):
     _fields_ = [("lanes", ctypes.c_uint64), ("vertices", ctypes.c_uint64), ("reuse_lanes", ctypes.c_uint64),
                 ("visibility_rays", ctypes.c_uint64), ("adaptive_lanes", ctypes.c_uint64),
-                ("seconds", ctypes.c_double)]
+                ("seconds", ctypes.c_double), ("range_drops", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -42,6 +42,7 @@ def lib():
         L.oracle_plan.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
         L.oracle_set_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.oracle_set_run_exchange.argtypes = [RunExchangeFn, ctypes.c_void_p]
+        L.oracle_set_fixed_film.argtypes = [ctypes.c_int]
         L.oracle_primary_hits.restype = ctypes.c_int
         L.oracle_primary_hits.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_render_rect.restype = ctypes.c_int
@@ -157,9 +158,19 @@ def render_rect(scene_desc_ptr, views_ptr, params, rect, threads=0, film=None):
 
 
 def render(scene_desc_ptr, views_ptr, params, lane_begin=0, lane_end=2 ** 64 - 1, threads=0,
-           record_pass=None, film=None):
-    """Render into a (H, W, C) float32 film; optionally return per-lane records of one pass."""
+           record_pass=None, film=None, fixed_film=False):
+    """Render into a (H, W, C) float32 film; optionally return per-lane records of one pass.
+    fixed_film: accumulate as the device's AMVPT_OPT_DETERMINISTIC film does (32.32 fixed-point integer
+    sums, converted once), which makes the film independent of summation order: bit-comparable."""
     L = lib()
+    L.oracle_set_fixed_film(1 if fixed_film else 0)
+    try:
+        return _render(L, scene_desc_ptr, views_ptr, params, lane_begin, lane_end, threads, record_pass, film)
+    finally:
+        L.oracle_set_fixed_film(0)
+
+
+def _render(L, scene_desc_ptr, views_ptr, params, lane_begin, lane_end, threads, record_pass, film):
     C = 5 if params.film_alpha else 4
     if film is None:
         film = np.zeros((params.film_height, params.film_width, C), dtype=np.float32)

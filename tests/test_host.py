@@ -305,6 +305,28 @@ def test_xml_unreferenced_properties_are_errors(amvpt_mod):
             _strict(amvpt_mod, **kw)
 
 
+def test_xml_unused_bsdf_and_wrapped_film_load(amvpt_mod):
+    """the reference's loader instantiates every child of the scene, so a scene-level BSDF no shape
+    uses reads its keys and loads (a typo in it still fails); a film given through <wrap> (wrap.cpp) is read by
+    the perspective sensor like a plain <film> child."""
+    unused = '<bsdf type="roughconductor" id="spare"><float name="alpha" value="0.2"/></bsdf>'
+    s = _strict(amvpt_mod, extra=unused)
+    assert s.describe(0, 0, 0)[0].contents.bsdf_count == _strict(amvpt_mod).describe(0, 0, 0)[0].contents.bsdf_count
+    with pytest.raises(RuntimeError, match=r'"\["alhpa"\]" in bsdf plugin of type "roughconductor"'):
+        _strict(amvpt_mod, extra=unused.replace("alpha", "alhpa"))
+    wrapped = _STRICT_BASE.replace(
+        '<film type="hdrfilm"><integer name="width" value="8"/><integer name="height" value="8"/>{fprops}</film>',
+        '<wrap type="wrap"><string name="wrap_class" value="film"/><string name="wrap_type" value="hdrfilm"/>'
+        '<integer name="width" value="12"/><integer name="height" value="8"/>{fprops}</wrap>')
+    fill = dict(itype="path", iprops="", sprops="", fprops="", shprops="", bprops="", eprops="", extra="")
+    w = amvpt_mod.load_string(wrapped.format(**fill))
+    assert w.film_info()[:2] == (12, 8)
+    # the wrapped film's own children are still checked
+    with pytest.raises(RuntimeError, match=r"in reconstructionfilter plugin of type \"gaussian\""):
+        amvpt_mod.load_string(wrapped.format(**dict(fill, fprops='<rfilter type="gaussian">'
+                                                                    '<float name="stdev" value="1"/></rfilter>')))
+
+
 def test_xml_accepts_every_key_the_reference_plugins_read(amvpt_mod):
     """Keys the reference's plugins query (so its loader accepts them) load here too, with the reference's
     meaning or its documented no-op on the JIT render path."""

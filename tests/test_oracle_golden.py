@@ -299,3 +299,19 @@ def test_microfacet_sampling_matches_its_pdf(oracle, kind, au, av, visible, thet
     for f in (lambda v: v[:, 0], lambda v: v[:, 2], lambda v: v[:, 0] ** 2, lambda v: v[:, 1] ** 2):
         q, s = (f(M.astype(np.float64)) * w).sum() / w.sum(), f(ms).mean()
         assert abs(q - s) < 4 * f(ms).std() / math.sqrt(n) + 2e-3, (q, s)
+
+
+def test_fixed_point_film_matches_float_film(oracle, amvpt_mod):
+    """The oracle's fixed-point film (the device's AMVPT_OPT_DETERMINISTIC accumulation restated: each cell add
+    rounded to 2^-32, summed as integers, converted once) equals the f32 ImageBlock film to summation order,
+    does not depend on the thread split, and drops nothing at normal radiance."""
+    from conftest import SCENES as _S
+    s = amvpt_mod.load_file(os.path.join(_S, "cbox_grid.xml"), res=8, spp=16, gx=2, gy=2, reuse=4)
+    sd, vd, p = s.describe(0, 0, 0)
+    f, _, _ = oracle.render(sd, vd, p, threads=4)
+    x1, _, st = oracle.render(sd, vd, p, threads=4, fixed_film=True)
+    x2, _, _ = oracle.render(sd, vd, p, threads=3, fixed_film=True)
+    assert np.array_equal(x1, x2) and st["range_drops"] == 0
+    assert np.abs(x1 - f).max() <= 1e-5 * np.abs(f).max()
+    g, _, _ = oracle.render(sd, vd, p, threads=4)   # the mode does not stick
+    assert np.abs(g - f).max() <= 1e-5 * np.abs(f).max()
