@@ -455,6 +455,8 @@ def kernel_bytes(c, G, C, n_adapt=0):
         "k_suffix": (state + 16) * pushed,
         # the adaptive fill's compaction: 1 B of mask per lane in, 4 B per selected lane out
         "k_select": lanes + 4 * adapt / max(1, n_adapt),
+        # ray binning: each binned ray read twice (histogram, scatter) and written once in bin order
+        "k_bin": 96 * (suffix + (shadow if not fused else 0)),
     }
 
 

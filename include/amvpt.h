@@ -229,7 +229,8 @@ typedef enum amvpt_kernel_id {
     AMVPT_K_SPLAT = 8,         /* ImageBlock::put                         */
     AMVPT_K_SUFFIX = 9,        /* ABI 7: the whole suffix in one launch (closest hit + shading + NEE, brute-force scenes) */
     AMVPT_K_SELECT = 10,       /* ABI 9: the adaptive fill's compaction of the adapt_mask lanes (k_select_flagged) */
-    AMVPT_K_COUNT = 11
+    AMVPT_K_BIN = 11,          /* ABI 9: ray binning of the per-lane suffix walks (k_bin_sort) */
+    AMVPT_K_COUNT = 12
 } amvpt_kernel_id;
 
 typedef struct amvpt_scene amvpt_scene; /* opaque device-resident scene */
@@ -372,6 +373,8 @@ enum {
     AMVPT_OPT_WAVEFRONT_SUFFIX = 2u,  /* per-depth k_extend / k_bounce instead of k_suffix_fused */
     AMVPT_OPT_SPLIT_NEE = 4u,         /* suffix NEE rays in k_shadow instead of inside k_bounce */
     AMVPT_OPT_ONE_STREAM = 8u,        /* every chunk on the render stream (no second chunk stream) */
+    AMVPT_OPT_NO_BINNING = 32u,       /* ABI 9: the per-lane suffix walks of large BVHs take the rays in queue order
+                                       * (no k_bin_sort); results are identical */
     AMVPT_OPT_DETERMINISTIC = 16u     /* bitwise-reproducible film: splats summed as 32.32 fixed point with
                                        * integer atomics (order-independent), added to the film once at the
                                        * end; each footprint-cell add is rounded to a multiple of 2^-32 and

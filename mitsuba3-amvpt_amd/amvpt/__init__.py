@@ -114,6 +114,7 @@ class RenderOpts(ctypes.Structure):
 
 # amvpt_render_opts.flags (results are identical; kernel-path selection for tests / A/B)
 OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE, OPT_ONE_STREAM, OPT_DETERMINISTIC = 1, 2, 4, 8, 16
+OPT_NO_BINNING = 32
 
 
 def wrap_run_exchange(fn):
@@ -133,7 +134,7 @@ def wrap_run_exchange(fn):
 
 # amvpt_kernel_id (include/amvpt.h): index -> name of Counters.kernel_ms / kernel_launches
 KERNELS = ("k_prim_hit", "k_prim_req", "k_vis", "k_mv_primary", "k_raygen", "k_extend", "k_bounce", "k_shadow",
-           "k_splat", "k_suffix", "k_select")
+           "k_splat", "k_suffix", "k_select", "k_bin")
 
 
 INTEGRATOR_MVPATH, INTEGRATOR_PATH = 0, 1

@@ -177,6 +177,7 @@ struct Bufs {
     uint4 *vreq_w[8];     /* groups > 16 views (G <= 0 instances): the lane's visibility-request mask (mstore) */
     uint4 *lmask_w[24];   /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (mask_planes<G>() each) */
     float *vstate;        /* runtime groups whose per-view state exceeds LDS: VS_FIELDS x G x vs_stride floats */
+    float4 *sray[2];      /* ray binning (k_bin_sort): a partition's rays in bin order, (o, d.x | dest), (d.yz | target, entry) */
 };
 
 /* ------------------------------------------------------------------ */
@@ -1715,7 +1716,89 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #ifndef AMVPT_SHADOW_WAVES
 #define AMVPT_SHADOW_WAVES 1
 #endif
-template <int kWalk>
+/*
+ * Ray binning for the per-lane suffix walks of large BVHs (coherence, not more per-lane tricks).
+ * The suffix rays of a queue partition arrive in whatever order the producer blocks pushed them: neighbouring
+ * lanes of a wave start anywhere and point anywhere, so a wave's walk runs as long as its longest lane and
+ * its node loads spread over the whole tree.  Embree restores coherence with ray packets (rtcIntersect16,
+ * scene_embree.inl:287-318); here k_bin_sort orders each partition by a key of direction octant (major) and
+ * the Morton code of the origin's cell in an 8 x 8 x 8 grid over the scene box -- a counting sort in LDS,
+ * one 1024-thread block per partition: an LDS histogram of the 4096 keys, a block scan, and a scatter whose
+ * returning LDS atomics hand out the positions -- and writes the rays in that order (32 B each, with the
+ * entry they came from).  k_extend / k_shadow then walk the binned rays: consecutive lanes share an octant
+ * (the same node ordering) and start nearby, and write their hit / verdict back to the entry.  The result of
+ * each ray does not depend on which lane walks it, so records stay bit-identical.  NEE rays are keyed the
+ * same way (direction to the light sample).
+ */
+#ifndef AMVPT_BIN
+#define AMVPT_BIN 3   /* bit 0: bin the extension rays (k_extend), bit 1: the NEE rays (k_shadow); 0: off (A/B) */
+#endif
+#ifndef AMVPT_BIN_UNI
+#define AMVPT_BIN_UNI 0   /* 1: binned waves take the wave-uniform walk (scalar node loads) instead of the per-lane one */
+#endif
+constexpr uint32_t kBinCellBits = 3, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
+AD uint32_t bin_cell(float v, float lo, float hi) {
+    const float f = (v - lo) / fmaxf(hi - lo, 1e-30f) * (float) (1u << kBinCellBits);
+    return (uint32_t) min(max((int) f, 0), (int) (1u << kBinCellBits) - 1);
+}
+AD uint32_t bin_key(const DNode &root, f3 o, f3 d) {
+    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+    const uint32_t cx = bin_cell(o.x, root.lo[0], root.hi[0]), cy = bin_cell(o.y, root.lo[1], root.hi[1]),
+                   cz = bin_cell(o.z, root.lo[2], root.hi[2]);
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < kBinCellBits; ++b)
+        m |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
+    return (oct << (3 * kBinCellBits)) | m;
+}
+template <bool kNee>
+__global__ void __launch_bounds__(kBinBlock) k_bin_sort(const DScene *Sp, Bufs B) {
+    __shared__ uint32_t h[kBins];
+    __shared__ uint32_t wsum[kBinBlock / 64];
+    const uint32_t part = blockIdx.x;
+    const uint32_t count = (kNee ? B.cnt_nee : B.cnt_in)[part * kCntStride], pbase = part * B.qcap;
+    const DNode root = load_uniform(Sp->nodes, 0u);   /* every node ordering starts at the root */
+    float4 *const *src = kNee ? B.nee : B.q_in;
+    auto key_of = [&](const float4 &a, const float4 &b) {
+        const f3 o = mk(a.x, a.y, a.z);
+        return bin_key(root, o, kNee ? mk(b.x, b.y, b.z) - o : mk(a.w, b.x, b.y));
+    };
+    for (uint32_t k = threadIdx.x; k < kBins; k += kBinBlock) h[k] = 0u;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) {
+        const uint32_t i = pbase + e;
+        (void) atomicAdd(&h[key_of(src[0][i], src[1][i])], 1u);
+    }
+    __syncthreads();
+    /* exclusive scan of the histogram: thread t owns bins [t * per, t * per + per) */
+    constexpr uint32_t per = kBins / kBinBlock;
+    uint32_t v[per], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < per; ++k) { v[k] = h[threadIdx.x * per + k]; sum += v[k]; }
+    const int lane = (int) __lane_id(), wave = (int) (threadIdx.x >> 6);
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (uint32_t k = 0; k < per; ++k) { h[threadIdx.x * per + k] = run; run += v[k]; }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) {
+        const uint32_t i = pbase + e;
+        const float4 a = src[0][i], b = src[1][i];
+        const uint32_t j = pbase + atomicAdd(&h[key_of(a, b)], 1u);
+        B.sray[0][j] = a;
+        B.sray[1][j] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
+    }
+}
+
+template <int kWalk, bool kBin = false>
 __global__ void __launch_bounds__(256, (AMVPT_EXTEND_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) ? AMVPT_EXTEND2_WAVES
                                                                                                                   : AMVPT_EXTEND_WAVES)
 k_extend(KParams P, const DScene *Sp, Bufs B) {
@@ -1727,6 +1810,19 @@ k_extend(KParams P, const DScene *Sp, Bufs B) {
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
     if (blockIdx.x == 0) {
         for (uint32_t q = threadIdx.x; q < kQParts; q += blockDim.x) { B.cnt_out[q * kCntStride] = 0u; B.cnt_nee[q * kCntStride] = 0u; }
+    }
+    if constexpr (kBin) {
+        /* the partition's rays in bin order (k_bin_sort); the hit goes back to the ray's entry */
+        for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
+            const uint32_t j = pbase + e0 + threadIdx.x;
+            if (e0 + threadIdx.x < count) {
+                const float4 a = B.sray[0][j], b = B.sray[1][j];
+                const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest};
+                const Hit h = AMVPT_BIN_UNI ? trace_closest<true, 0, kWalk != WALK_LANE_NS>(sc, r) : walk_closest<kWalk>(sc, r);
+                B.hit[fbits(b.z)] = hit_rec(h);
+            }
+        }
+        return;
     }
     if constexpr (AMVPT_EXTEND_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) {
         /* two paths per thread (trace_closest_lane2): entries e0 + t and e0 + t + blockDim.x */
@@ -1753,7 +1849,7 @@ k_extend(KParams P, const DScene *Sp, Bufs B) {
     }
 }
 
-template <int kWalk>
+template <int kWalk, bool kBin = false>
 __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
@@ -1778,6 +1874,23 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
         d = d / dist;
         return Ray{o, d, dist * (1.f - kShadowEps)};
     };
+    if constexpr (kBin) {
+        /* the partition's NEE rays in bin order (k_bin_sort): (origin, destination), (target, entry); a visible
+         * light's result is read from the entry's record */
+        for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
+            const uint32_t j = pbase + e0 + threadIdx.x;
+            if (e0 + threadIdx.x < count) {
+                const float4 a = B.sray[0][j], b = B.sray[1][j];
+                const Ray r = nee_ray(a, b);
+                const bool occ = AMVPT_BIN_UNI ? trace_any<true, 0, kWalk != WALK_LANE_NS>(sc, r) : walk_any<kWalk>(sc, r);
+                if (!occ) {
+                    const uint32_t i = fbits(b.w);
+                    visible(i, a, make_float4(0.f, 0.f, 0.f, B.nee[1][i].w));
+                }
+            }
+        }
+        return;
+    }
     if constexpr (AMVPT_SHADOW_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) {
         /* two records per thread (trace_any_lane2): entries e0 + t and e0 + t + blockDim.x */
         for (uint32_t e0 = blockIdx.x / kQParts * 2u * blockDim.x; e0 < count; e0 += 2u * pstride) {
@@ -3263,10 +3376,12 @@ AMVPT_TU_LOCAL __global__ void k_develop(const float *film, float *out, uint32_t
  * k_shadow is the one kernel that is faster with it (71 vs 80 ms per config-M frame),
  * while the rest of this file is built with -fno-slp-vectorize (see Makefile).
  */
-void launch_shadow(int walk, dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *dS, const Bufs &B)
+void launch_shadow(int walk, bool bin, dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *dS, const Bufs &B)
 #ifdef AMVPT_SHADOW_TU
 {
-    if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, dS, B);
+    if (bin && walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_NS, true>), grid, dim3(256), lds, st, P, dS, B);
+    else if (bin && walk == WALK_LANE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE, true>), grid, dim3(256), lds, st, P, dS, B);
+    else if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_UNI>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_NS>), grid, dim3(256), lds, st, P, dS, B);
@@ -3967,7 +4082,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds_tab_views = (AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views))
                                      ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;
     const bool vs_global = wide && lds_tab_views + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 65536;
-    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + (size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G + (G + 7) / 8 +
+    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + 32 /* binned rays */ +
+                            (size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G + (G + 7) / 8 +
                             (wide ? (size_t) 4 * 16 * mplanes : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
     if (chunk_max == 0) {
@@ -4002,6 +4118,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * and tails leave CUs idle that the other chunk's kernels fill (mesh 550 -> 599 Msamples/s).  The
      * fused-suffix scenes gain 0.0-0.5 % (r03i) and keep one stream, so their per-kernel HIP-event
      * times are not overlapped (AMVPT_OPT_ONE_STREAM forces one stream everywhere) */
+    /* ray binning (k_bin_sort) for the per-lane suffix walks of BVHs read from device memory */
+    const bool lane_walk = (walk == WALK_LANE || walk == WALK_LANE_NS) && !fuse_suffix && scene_lds_bytes(scene->dev, trav) == 0u;
+    const bool bin_ext = lane_walk && (AMVPT_BIN & 1) && !(opts.flags & AMVPT_OPT_NO_BINNING);
+    const bool bin_nee = lane_walk && (AMVPT_BIN & 2) && !fuse_nee && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
                         !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? 2 : 1;
     const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
@@ -4120,6 +4240,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.cnt_nee = cs.cntN;
         B.qcap = qcap;
         B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G * chunk);
+        if (bin_ext || bin_nee)
+            for (int k = 0; k < 2; ++k) B.sray[k] = (float4 *) carve(16 * qlen);
         if (wide) {
             for (int k = 0; k < mplanes; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
             for (int k = 0; k < 3 * mplanes; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
@@ -4178,8 +4300,15 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.cnt_in = a_is_in ? cntA : cntB;
             B.cnt_out = a_is_in ? cntB : cntA;
             /* k_extend zeroes cnt_out and cnt_nee */
+            if (bin_ext) {
+                T.begin(AMVPT_K_BIN, st);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false>), dim3(kQParts), dim3(kBinBlock), 0, st, dS, B);
+                T.end(st);
+            }
             T.begin(AMVPT_K_EXTEND, st);
-            if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            if (bin_ext && walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_NS, true>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
+            else if (bin_ext) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE, true>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
+            else if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_NS>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
@@ -4189,8 +4318,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             launch_bounce(tab_b, diff, fuse_nee ? walk : -1, dim3(bgrid), lds, st, P, dS, B);
             T.end(st);
             if (!fuse_nee) {
+                if (bin_nee) {
+                    T.begin(AMVPT_K_BIN, st);
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<true>), dim3(kQParts), dim3(kBinBlock), 0, st, dS, B);
+                    T.end(st);
+                }
                 T.begin(AMVPT_K_SHADOW, st);
-                launch_shadow(walk, dim3(bgrid), lds_any, st, P, dS, B);
+                launch_shadow(walk, bin_nee, dim3(bgrid), lds_any, st, P, dS, B);
                 T.end(st);
             }
             HIPCHK(hipGetLastError());

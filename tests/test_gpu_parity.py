@@ -425,6 +425,26 @@ def test_file_meshes_per_lane_bvh(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
+@pytest.mark.parametrize("kw", [dict(res=16, spp=16), dict(res=16, spp=16, gx=4, gy=2, reuse=8)], ids=["path_g1", "g8"])
+def test_ray_binning_keeps_records(gpu_ready, amvpt_mod, oracle, kw):
+    """Ray binning (k_bin_sort): the per-lane suffix walks of the 3.6 k-triangle mesh take each partition's
+    extension and NEE rays in (direction octant, origin cell) order and write hits / verdicts back to the
+    rays' entries.  Records are bit-identical to the oracle with binning (the default) and without it
+    (AMVPT_OPT_NO_BINNING), and the binning kernel ran."""
+    s = amvpt_mod.load_file(MESH, **kw)
+    _check(amvpt_mod, oracle, s)
+    _check(amvpt_mod, oracle, s, flags=amvpt_mod.OPT_NO_BINNING)
+    torch = _torch()
+    sd, vd, p = s.describe(0, 0, 0)
+    dev = amvpt_mod.DeviceScene(sd)
+    for flags, launched in [(0, True), (amvpt_mod.OPT_NO_BINNING, False)]:
+        film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+        cnt = amvpt_mod.Counters()
+        dev.render_ex(vd, p, film.data_ptr(), counters=cnt, flags=flags)
+        torch.cuda.synchronize()
+        assert (cnt.as_dict()["kernel_launches"]["k_bin"] > 0) == launched
+
+
 @pytest.mark.parametrize("chunk", [8192, 5000])
 def test_many_chunks_per_pass(gpu_ready, amvpt_mod, oracle, chunk):
     """Many lane chunks per pass (the arena bound at full size): records stay bit-identical, the film
