@@ -45,6 +45,7 @@ CBOX = os.path.join(SCENES, "cbox_grid.xml")
 VEACH = os.path.join(SCENES, "veach_grid.xml")
 MESHLIGHT = os.path.join(SCENES, "cbox_meshlight.xml")
 RECTLIGHTS = os.path.join(SCENES, "cbox_cubelight_rects.xml")
+MESH = os.path.join(SCENES, "cbox_mesh.xml")
 K = 24   # independent seeds per side
 
 
@@ -155,6 +156,15 @@ CASES = [
     ("cbox_g8", CBOX, dict(res=RES, spp=64, gx=4, gy=2, reuse=8), 8, 2),
     ("veach_g8", VEACH, dict(res=RES, spp=64, gx=4, gy=2, reuse=8), 8, 2),
     ("cbox_g8_box", CBOX, dict(res=RES, spp=64, gx=4, gy=2, reuse=8, rfilter="box"), 8, 1),
+    # the parts the restatement alone pins.  The adaptive fill (mvpath_multi.h:52-59,79-115) on the
+    # C5 shape (8 x 4 grid, groups of 4, adaptive 3, one 16-spp pass) -- its reference side is the same views
+    # with reuse off, where the fill does not apply; the 3.6 k-triangle OBJ/PLY box (per-lane BVH walks with ray
+    # binning, a rough-conductor object); thin-lens views (thinlens.cpp:358-418), whose defocus spreads a
+    # discontinuity over a circle of confusion of up to ~3 px here (aperture 0.05, focus 3.9, objects 3..4.9
+    # away), so their mask is dilated by 5 px instead of the filter's 2
+    ("c5_adaptive", CBOX, dict(res=64, spp=16, gx=8, gy=4, reuse=4, adaptive=3), 4, 2),
+    ("mesh_g8", MESH, dict(res=RES, spp=64, gx=4, gy=2, reuse=8), 8, 2),
+    ("cbox_g8_thinlens", CBOX, dict(res=RES, spp=64, gx=4, gy=2, reuse=8, cam="thinlens", aperture="0.05"), 8, 5),
 ]
 
 

@@ -7,7 +7,7 @@ P=profiles
 for c in M C3 mesh C5; do
   [ -f $G/${T}_bench_$c.log ] && grep '^{' $G/${T}_bench_$c.log | tail -1 > $P/${T}_bench_$c.json
 done
-for c in M C3 mesh; do
+for c in M C3 mesh C5; do
   [ -f $G/${T}_trace_$c/run_kernel_stats.csv ] && cp $G/${T}_trace_$c/run_kernel_stats.csv $P/${T}_kernel_stats_$c.csv
   sfx=$([ $c = M ] && echo "" || echo "_$c")
   if [ -f $G/${T}_fetch_$c/pmc_counter_collection.csv ] && [ -f $G/${T}_write_$c/pmc_counter_collection.csv ]; then
@@ -18,7 +18,8 @@ for c in M C3 mesh; do
     python3 tools/pmc_summary.py $G/${T}_sqA_$c > $P/${T}_sq_counters$sfx.txt
   fi
 done
-for c in M C3 mesh; do
+for c in M C3 mesh C5; do
+  [ -f $G/${T}_quick_$c.log ] && grep '^{' $G/${T}_quick_$c.log | tail -1 > $P/${T}_quick_$c.json
   [ -f $G/${T}_ab$c.log ] && grep '^{' $G/${T}_ab$c.log > $P/${T}_ab_$c.log || true
 done
 [ -f $G/${T}_tests.log ] && cp $G/${T}_tests.log $P/${T}_gpu_tests.txt
