@@ -375,6 +375,8 @@ enum {
     AMVPT_OPT_ONE_STREAM = 8u,        /* every chunk on the render stream (no second chunk stream) */
     AMVPT_OPT_NO_BINNING = 32u,       /* ABI 9: the per-lane suffix walks of large BVHs take the rays in queue order
                                        * (no k_bin_sort); results are identical */
+    AMVPT_OPT_NO_BOX_SCREEN = 64u,    /* ABI 9: the brute-force walks of small scenes test every triangle of a box
+                                       * mesh (no per-lane face screening); results are identical */
     AMVPT_OPT_DETERMINISTIC = 16u     /* bitwise-reproducible film: splats summed as 32.32 fixed point with
                                        * integer atomics (order-independent), added to the film once at the
                                        * end; each footprint-cell add is rounded to a multiple of 2^-32 and

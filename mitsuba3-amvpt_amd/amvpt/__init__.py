@@ -115,6 +115,7 @@ class RenderOpts(ctypes.Structure):
 # amvpt_render_opts.flags (results are identical; kernel-path selection for tests / A/B)
 OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE, OPT_ONE_STREAM, OPT_DETERMINISTIC = 1, 2, 4, 8, 16
 OPT_NO_BINNING = 32
+OPT_NO_BOX_SCREEN = 64
 
 
 def wrap_run_exchange(fn):

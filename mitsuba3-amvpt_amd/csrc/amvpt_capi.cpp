@@ -439,6 +439,77 @@ static void scene_bsphere(const amvpt_scene_desc *d, float center[3], float &rad
     radius = std::max(ray_eps, radius * (1.f + ray_eps));
 }
 
+#ifndef AMVPT_BOX_SCREEN
+#define AMVPT_BOX_SCREEN 1   /* box meshes of brute-force scenes get DBox records (0: none, A/B) */
+#endif
+/*
+ * Box meshes (dscene.h DBox): a mesh shape of 12 triangles whose vertices map, through the shape's
+ * to_object (in double), to corners of [-1, 1]^3 within 1e-5, every triangle lying in one face plane, two
+ * triangles per face covering its four corners -- the `cube` plugin's mesh (cube.cpp:105-160) under any
+ * affine to_world.  Boxes whose box-space coordinates would magnify the walks' rounding (a very thin box, or
+ * one far from the origin relative to its size: conditioning >= 100) are left to the plain scan.  prims[] is
+ * in BVH order; box_prims / loose_prims hold copies with the BVH index in `type`'s upper bits.
+ */
+static void find_boxes(const amvpt_scene_desc *d, const std::vector<DPrim> &prims, std::vector<DBox> &boxes,
+                       std::vector<DPrim> &box_prims, std::vector<DPrim> &loose) {
+    std::vector<int> in_box(prims.size(), 0);
+    for (uint32_t i = 0; i < d->shape_count; ++i) {
+        const amvpt_shape_desc &s = d->shapes[i];
+        if (s.type != AMVPT_SHAPE_MESH || s.face_count != 12 || !s.positions || !s.faces) continue;
+        std::vector<uint32_t> tris;
+        for (uint32_t pi = 0; pi < (uint32_t) prims.size(); ++pi)
+            if (prims[pi].type == PRIM_TRI && prims[pi].shape == i) tris.push_back(pi);
+        if (tris.size() != 12) continue;
+        double M[12], cond = 0.0, wmax = 0.0;
+        for (int k = 0; k < 12; ++k) M[k] = (double) s.to_object[k];
+        for (int r = 0; r < 3; ++r)
+            cond = std::max(cond, std::sqrt(M[4 * r] * M[4 * r] + M[4 * r + 1] * M[4 * r + 1] + M[4 * r + 2] * M[4 * r + 2]));
+        bool ok = true;
+        int n_on[6] = {0, 0, 0, 0, 0, 0};
+        uint32_t ftri[12];
+        uint32_t corners[6] = {0, 0, 0, 0, 0, 0};   /* per face: the (b, c) corners its triangles touch, 4 bits */
+        for (uint32_t pi : tris) {
+            const uint32_t f = prims[pi].face;
+            double b[3][3];
+            for (int v = 0; v < 3; ++v) {
+                const float *w = s.positions + 3 * (size_t) s.faces[3 * f + v];
+                for (int r = 0; r < 3; ++r) {
+                    b[v][r] = M[4 * r] * w[0] + M[4 * r + 1] * w[1] + M[4 * r + 2] * w[2] + M[4 * r + 3];
+                    wmax = std::max(wmax, (double) std::fabs(w[r]));
+                    if (std::fabs(std::fabs(b[v][r]) - 1.0) > 1e-5) ok = false;
+                }
+            }
+            int axis = -1;
+            for (int a = 0; a < 3; ++a)
+                if ((b[0][a] > 0) == (b[1][a] > 0) && (b[0][a] > 0) == (b[2][a] > 0)) { axis = a; break; }
+            if (!ok || axis < 0) { ok = false; break; }
+            const int face = 2 * axis + (b[0][axis] > 0 ? 1 : 0);
+            if (n_on[face] >= 2) { ok = false; break; }
+            ftri[2 * face + n_on[face]++] = pi;
+            const int bx = (axis + 1) % 3, cx = (axis + 2) % 3;
+            for (int v = 0; v < 3; ++v) corners[face] |= 1u << ((b[v][bx] > 0 ? 1 : 0) + (b[v][cx] > 0 ? 2 : 0));
+        }
+        for (int f = 0; ok && f < 6; ++f) ok = n_on[f] == 2 && corners[f] == 15u;
+        if (!ok || cond * (1.0 + wmax) >= 100.0) continue;
+        DBox B{};
+        for (int k = 0; k < 12; ++k) B.m[k] = (float) M[k];
+        for (int k = 0; k < 12; ++k) {
+            DPrim q = prims[ftri[k]];
+            q.type = PRIM_TRI | (ftri[k] << 8);
+            box_prims.push_back(q);
+            in_box[ftri[k]] = 1;
+        }
+        boxes.push_back(B);
+    }
+    if (boxes.empty()) return;
+    for (uint32_t pi = 0; pi < (uint32_t) prims.size(); ++pi)
+        if (!in_box[pi]) {
+            DPrim q = prims[pi];
+            q.type |= pi << 8;
+            loose.push_back(q);
+        }
+}
+
 amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (!d || !out) { set_error("amvpt_scene_create: null argument"); return AMVPT_ERR_INVALID; }
     *out = nullptr;
@@ -679,7 +750,16 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         }
     const uint32_t n_sph = (uint32_t) sph_prims.size();
     if (sph_prims.empty()) sph_prims.resize(1, 0u);
+    /* box meshes of brute-force scenes (dscene.h DBox; dgeom.h box_walk) */
+    std::vector<DBox> boxes;
+    std::vector<DPrim> box_prims, loose_prims;
+    if (AMVPT_BOX_SCREEN && prims.size() <= 48) find_boxes(d, prims, boxes, box_prims, loose_prims);
+    const uint32_t n_boxes = (uint32_t) boxes.size(), n_loose = (uint32_t) loose_prims.size();
+    if (boxes.empty()) boxes.resize(1);
+    if (box_prims.empty()) box_prims.resize(1);
+    if (loose_prims.empty()) loose_prims.resize(1);
     void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes, *p_sph;
+    void *p_boxes, *p_box_prims, *p_loose;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
     if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
@@ -690,7 +770,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
     UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
-    UP(sph_prims, p_sph)
+    UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -712,6 +792,12 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.sph_prims = (const uint32_t *) p_sph;
     D.n_sph = n_sph;
     sc->n_sph = n_sph;
+    D.boxes = (const DBox *) p_boxes;
+    D.box_prims = (const DPrim *) p_box_prims;
+    D.loose_prims = (const DPrim *) p_loose;
+    D.n_boxes = n_boxes;
+    D.n_loose = n_loose;
+    sc->n_boxes = n_boxes;
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;

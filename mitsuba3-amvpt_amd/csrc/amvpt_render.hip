@@ -130,6 +130,7 @@ struct KParams {
      * pass with, rng_out (all but the last pass) receives the state its path ends with; both indexed by
      * the lane's virtual index in the render's lane set */
     unsigned long long *rng_in, *rng_out;
+    uint32_t box_screen;  /* the brute-force suffix walks screen box meshes (box_walk); 0: AMVPT_OPT_NO_BOX_SCREEN */
 };
 
 /* the PCG32 a stock-path lane starts the pass with: TEA-seeded, or the previous pass's state (same
@@ -242,9 +243,16 @@ template <typename T> AD T *copy_to_lds(const T *src, uint32_t bytes, char *&dst
  * copy of the scene header; its table pointers are redirected.
  */
 template <bool kTab, bool kBvh = true, bool kTree = false, bool kOct = false>
-AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0) {
+AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0,
+                        bool boxes = false) {
     SceneRef sc;
     sc.g = &S;
+    /* the brute-force walks' box screening (box_walk) where the kernel asks for it */
+    sc.boxes = S.boxes;
+    sc.box_prims = S.box_prims;
+    sc.loose_prims = S.loose_prims;
+    sc.n_boxes = boxes ? S.n_boxes : 0u;
+    sc.n_loose = S.n_loose;
     sc.tnodes = nullptr;
     sc.t_n = 0;
     sc.onodes = nullptr;
@@ -1736,7 +1744,10 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #ifndef AMVPT_BIN_UNI
 #define AMVPT_BIN_UNI 0   /* 1: binned waves take the wave-uniform walk (scalar node loads) instead of the per-lane one */
 #endif
-constexpr uint32_t kBinCellBits = 3, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
+#ifndef AMVPT_BIN_CELL_BITS
+#define AMVPT_BIN_CELL_BITS 3   /* origin cells per axis of the bin key: 2^bits (A/B) */
+#endif
+constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
 AD uint32_t bin_cell(float v, float lo, float hi) {
     const float f = (v - lo) / fmaxf(hi - lo, 1e-30f) * (float) (1u << kBinCellBits);
     return (uint32_t) min(max((int) f, 0), (int) (1u << kBinCellBits) - 1);
@@ -1771,10 +1782,13 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(const DScene *Sp, Bufs B
     }
     __syncthreads();
     /* exclusive scan of the histogram: thread t owns bins [t * per, t * per + per) */
-    constexpr uint32_t per = kBins / kBinBlock;
+    constexpr uint32_t per = kBins >= kBinBlock ? kBins / kBinBlock : 1u;
     uint32_t v[per], sum = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < per; ++k) { v[k] = h[threadIdx.x * per + k]; sum += v[k]; }
+    for (uint32_t k = 0; k < per; ++k) {
+        v[k] = threadIdx.x * per + k < kBins ? h[threadIdx.x * per + k] : 0u;
+        sum += v[k];
+    }
     const int lane = (int) __lane_id(), wave = (int) (threadIdx.x >> 6);
     uint32_t inc = sum;
 #pragma unroll
@@ -1787,7 +1801,10 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(const DScene *Sp, Bufs B
     uint32_t run = inc - sum;
     for (int w = 0; w < wave; ++w) run += wsum[w];
 #pragma unroll
-    for (uint32_t k = 0; k < per; ++k) { h[threadIdx.x * per + k] = run; run += v[k]; }
+    for (uint32_t k = 0; k < per; ++k) {
+        if (threadIdx.x * per + k < kBins) h[threadIdx.x * per + k] = run;
+        run += v[k];
+    }
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) {
         const uint32_t i = pbase + e;
@@ -1804,7 +1821,7 @@ __global__ void __launch_bounds__(256, (AMVPT_EXTEND_RAYS == 2 && (kWalk == WALK
 k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false, true, false, (AMVPT_TREELETS & 2) != 0>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, false, (AMVPT_TREELETS & 2) != 0>(S, lds, P.trav_mode, nullptr, 0, P.box_screen != 0);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
@@ -1853,7 +1870,7 @@ template <int kWalk, bool kBin = false>
 __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 1) != 0>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 1) != 0>(S, lds, P.trav_mode, nullptr, 0, P.box_screen != 0);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_nee[part * kCntStride], pbase = part * B.qcap;
     /* the visible-light write of a record (the path's result becomes fma(throughput, contribution, result),
@@ -2027,7 +2044,7 @@ template <bool kTab, bool kDiff, int kNee>
 __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
-    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode);
+    SceneRef sc = stage_scene<kTab, false>(S, lds, P.trav_mode, nullptr, 0, P.box_screen != 0);
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     unsigned long long verts = 0, shadows = 0;
@@ -2184,7 +2201,7 @@ __global__ void __launch_bounds__(kFusedBlock, kDiff ? AMVPT_FUSED_WAVES : AMVPT
     /* the parked state sits in front of the staged tables (dynamic LDS: [park][tables]) */
     const LdsPark<kPk> pk{(lds_float *) (uint32_t) (uintptr_t) lds + threadIdx.x};
     DScene S = *Sp;
-    SceneRef sc = stage_scene<kTab, false>(S, lds + kFusedParkBytes, P.trav_mode);
+    SceneRef sc = stage_scene<kTab, false>(S, lds + kFusedParkBytes, P.trav_mode, nullptr, 0, P.box_screen != 0);
     const uint32_t part = blockIdx.x % kQParts;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     uint32_t *const work = B.cnt_out + part * kCntStride;
@@ -4018,6 +4035,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.nc_oy = (float) (-(int) P.off_y) - .5f;
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = trav;
+    P.box_screen = (opts.flags & AMVPT_OPT_NO_BOX_SCREEN) ? 0u : 1u;
     P.sph = !scene->has_spheres ? 0u : (AMVPT_SPHERE_DEFER && scene->n_sph <= 64u) ? 2u : 1u;
     P.win_rs = K.win_rs;
     P.range_begin = rect ? 0 : lane_begin;

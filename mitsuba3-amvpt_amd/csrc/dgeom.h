@@ -39,6 +39,12 @@ struct SceneRef {
     const DNode *onodes;      /* LDS treelets of the 8 octant orderings (stage_scene kOct), o_n nodes each; 0: none */
     uint32_t o_n;
     bool lds_bvh;             /* nodes / prims are the block's LDS copy (stage_scene), else device memory */
+    /* brute-force walks: box meshes screened per lane (DScene::boxes, box_walk) and the other primitives;
+     * n_boxes = 0: scan gprims[] (no boxes, or AMVPT_OPT_NO_BOX_SCREEN) */
+    const DBox *boxes;
+    const DPrim *box_prims;
+    const DPrim *loose_prims;
+    uint32_t n_boxes, n_loose;
 };
 
 
@@ -1100,6 +1106,101 @@ template <bool kSph> AD bool brute_pair_any(const DPrim &a, const DPrim &b, cons
     const bool hb = prim_hit_b<kSph>(b, tb, ray, t, u, v);
     return ha || hb;
 }
+/*
+ * Box meshes in the brute-force walks (the fused suffix's instruction count).  A `cube` is 12
+ * triangles, 24 of the Cornell box's 30 primitives, and a wave-uniform scan tests all of them for every ray.
+ * box_walk screens each box per lane in box space ([-1, 1]^3, DBox::m): for each of the six faces the ray's
+ * crossing of the face plane (an approximate reciprocal is enough) decides whether the face's two triangles
+ * can report a hit at all; only those are tested -- with the exact tri_hit and the same (t, scene-order index)
+ * rule as the scan, so the walk's hit is the scan's hit, bit for bit.  A face is skipped only when that is
+ * certain:
+ *   - the crossing point lies more than kBoxEps (box units) outside the face square, or its t lies outside
+ *     [0, maxt] by more than kBoxEpsT (1 + |t|), AND the ray is not grazing the face plane
+ *     (|d_axis| >= kBoxGraze |d|_max): then tri_hit's own rounding (relative ~1e-7 / sin of the angle to the
+ *     plane, below 1e-4 here) cannot move its barycentrics or t across the boundary;
+ *   - in the closest-hit walk, its crossing t exceeds the best hit so far by more than kBoxEpsT (1 + |t|): any
+ *     hit on it is farther.
+ * A grazing face whose crossing is anywhere near the square is always tested (first).  Lanes take their
+ * candidate faces in ascending crossing order, one face (two per-lane triangle loads) per round, so a lane
+ * that hits its entry face is done after one round; the wave runs until its last lane is.
+ */
+constexpr float kBoxEps = 1e-3f, kBoxEpsT = 1e-3f, kBoxGraze = 1e-3f;
+AD void box_candidates(const DBox &B, const Ray &r, float maxt, float *key, uint32_t &cand) {
+    const f3 o = mk(fmaf(B.m[2], r.o.z, fmaf(B.m[1], r.o.y, fmaf(B.m[0], r.o.x, B.m[3]))),
+                    fmaf(B.m[6], r.o.z, fmaf(B.m[5], r.o.y, fmaf(B.m[4], r.o.x, B.m[7]))),
+                    fmaf(B.m[10], r.o.z, fmaf(B.m[9], r.o.y, fmaf(B.m[8], r.o.x, B.m[11]))));
+    const f3 d = mk(fmaf(B.m[2], r.d.z, fmaf(B.m[1], r.d.y, B.m[0] * r.d.x)),
+                    fmaf(B.m[6], r.d.z, fmaf(B.m[5], r.d.y, B.m[4] * r.d.x)),
+                    fmaf(B.m[10], r.d.z, fmaf(B.m[9], r.d.y, B.m[8] * r.d.x)));
+    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+    const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    cand = 0u;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const int b = (a + 1) % 3, c = (a + 2) % 3;
+        const bool graze = !(fabsf(da[a]) >= kBoxGraze * dmax);
+        const float inv = __builtin_amdgcn_rcpf(da[a]);
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const float t = ((side ? 1.f : -1.f) - oa[a]) * inv;
+            const float qb = fabsf(fmaf(da[b], t, oa[b])), qc = fabsf(fmaf(da[c], t, oa[c]));
+            const float et = kBoxEpsT * (1.f + fabsf(t));
+            /* near the square; a grazing face: its crossing anywhere within 0.1 of the square (its t is
+             * unreliable), or the ray running within 0.1 of the face plane (tri_hit's determinant is then
+             * rounding noise), NaN included */
+            const bool in_sq = qb <= 1.f + kBoxEps && qc <= 1.f + kBoxEps && t >= -et && t <= maxt + et;
+            const bool near_g = !(qb > 1.1f) || !(qc > 1.1f) || !(fabsf((side ? 1.f : -1.f) - oa[a]) > .1f);
+            const bool c_ = graze ? near_g : in_sq;
+            key[2 * a + side] = graze ? -kInf : t;
+            cand |= c_ ? 1u << (2 * a + side) : 0u;
+        }
+    }
+}
+/* kAny: any hit in [0, ray.maxt] (found); else the closest hit (best, best_orig) */
+template <bool kAny>
+AD void box_walk(const SceneRef &sc, const Ray &ray, Hit &best, uint32_t &best_orig, bool &found) {
+    const uint32_t nb = ufirst(sc.n_boxes);
+    for (uint32_t bi = 0; bi < nb; ++bi) {
+        const DBox B = load_uniform(sc.boxes, bi);
+        float key[6];
+        uint32_t cand;
+        box_candidates(B, ray, ray.maxt, key, cand);
+        if (kAny && found) cand = 0u;
+        const DPrim *const bt = sc.box_prims + 12u * bi;
+        for (;;) {
+            /* the lane's next face: the candidate with the smallest crossing */
+            uint32_t k = 0u;
+            float kmin = kInf;
+#pragma unroll
+            for (uint32_t f = 0; f < 6; ++f) {
+                const bool take = ((cand >> f) & 1u) && !(key[f] >= kmin);
+                kmin = take ? key[f] : kmin;
+                k = take ? f : k;
+            }
+            bool act = cand != 0u;
+            if (!kAny) act = act && !(kmin > best.t + kBoxEpsT * (1.f + fabsf(best.t)));
+            if (!wave_any(act)) break;
+            if (act) {
+                cand &= ~(1u << k);
+#pragma unroll
+                for (uint32_t j = 0; j < 2; ++j) {
+                    const DPrim p = load_global(bt, 2u * k + j);
+                    float t, u, v;
+                    if (tri_hit(p, ray, t, u, v)) {
+                        if (kAny) {
+                            found = true;
+                        } else if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                            best.t = t; best.u = u; best.v = v; best.prim = (int32_t) (p.type >> 8);
+                            best_orig = p.pad;
+                        }
+                    }
+                }
+                if (kAny && found) cand = 0u;
+            }
+        }
+    }
+}
+
 /* Two records in flight (a, b), each reloaded in place right after its own test: the next
  * record's scalar load overlaps the current test and no record is copied between registers
  * (a one-record prefetch made the compiler move all 16 SGPRs of the record every iteration). */
@@ -1108,6 +1209,44 @@ template <bool kSph> AD bool brute_pair_any(const DPrim &a, const DPrim &b, cons
 template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
+    if (sc.n_boxes) {
+        /* the loose primitives (their BVH index in `type`'s upper bits), then the boxes */
+        const uint32_t nl = ufirst(sc.n_loose);
+        uint64_t dm = 0;
+        for (uint32_t j = 0; j < nl; ++j) {
+            const DPrim p = load_uniform(sc.loose_prims, j);
+            const uint32_t tw = ufirst(p.type), type = tw & 0xffu;
+            if (kSph && type == PRIM_SPHERE) {
+                if (wave_any(sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+                continue;
+            }
+            float t, u, v;
+            if (prim_hit_b<false>(p, type, ray, t, u, v)) {
+                const uint32_t orig = ufirst(p.pad);
+                if (t < best.t || (t == best.t && orig < best_orig)) {
+                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) (tw >> 8);
+                    best_orig = orig;
+                }
+            }
+        }
+        bool found = false;
+        box_walk<false>(sc, ray, best, best_orig, found);
+        if constexpr (kSph) {
+            while (dm) {
+                const uint32_t k = mask_pop(dm);
+                const DPrim p = deferred_sphere(sc, k);
+                float t;
+                if (sphere_hit(p, ray, t)) {
+                    const uint32_t orig = ufirst(p.pad);
+                    if (t < best.t || (t == best.t && orig < best_orig)) {
+                        best.t = t; best.u = 0.f; best.v = 0.f; best.prim = (int32_t) ufirst(sc.g->sph_prims[k]);
+                        best_orig = orig;
+                    }
+                }
+            }
+        }
+        return best;
+    }
     constexpr bool kDefer = kSph && AMVPT_SPHERE_DEFER && !AMVPT_PAIR_PRIMS;
     uint64_t dm = 0;
     auto test = [&](const DPrim &p, uint32_t pi) {
@@ -1162,6 +1301,34 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
 template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool skip = false) {
     const uint32_t np = ufirst(sc.g->n_prims);
     bool found = skip;
+    if (sc.n_boxes) {
+        const uint32_t nl = ufirst(sc.n_loose);
+        uint64_t dm = 0;
+        for (uint32_t j = 0; j < nl; ++j) {
+            const DPrim p = load_uniform(sc.loose_prims, j);
+            const uint32_t type = ufirst(p.type) & 0xffu;
+            if (kSph && type == PRIM_SPHERE) {
+                if (wave_any(!found && sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+                continue;
+            }
+            float t, u, v;
+            const bool h = prim_hit_b<false>(p, type, ray, t, u, v);
+            found = found || h;
+            if (!wave_any(!found)) return found;
+        }
+        Hit best_unused{kInf, 0.f, 0.f, -1};
+        uint32_t orig_unused = 0u;
+        box_walk<true>(sc, ray, best_unused, orig_unused, found);
+        if constexpr (kSph) {
+            while (dm && wave_any(!found)) {
+                const DPrim p = deferred_sphere(sc, mask_pop(dm));
+                float t;
+                const bool h = !found && sphere_hit(p, ray, t);
+                found = found || h;
+            }
+        }
+        return found;
+    }
     constexpr bool kDefer = kSph && AMVPT_SPHERE_DEFER && !AMVPT_PAIR_PRIMS;
     uint64_t dm = 0;
     auto test = [&](const DPrim &p) {

@@ -90,6 +90,18 @@ struct DView {
 constexpr uint32_t kTabBytes = 8192, kViewTabBytes = 8192;
 inline __host__ __device__ uint32_t tab_round(uint32_t b) { return (b + 15u) & ~15u; }
 
+/*
+ * A box mesh (a `cube` shape, or any 12-triangle mesh whose triangles tile the faces of a parallelepiped):
+ * m maps world space to box space, where the box is [-1, 1]^3.  Its triangles are copied in face order to
+ * DScene::box_prims[12 * box + 2 * face + j] (face = 2 * axis + (side > 0)), each record's `type` holding
+ * PRIM_TRI | (its index in prims[] << 8).  The brute-force walks screen a box per lane and test only the
+ * triangles of the faces a ray can reach (dgeom.h box_walk).
+ */
+struct alignas(16) DBox {
+    float m[12];
+    uint32_t pad[4];
+};
+
 struct DScene {
     const DNode *nodes;
     const DPrim *prims;
@@ -125,6 +137,12 @@ struct DScene {
      * ordinal): the wave-uniform walks' deferred sphere tests (dgeom.h, kSph = 2) */
     const uint32_t *sph_prims;
     uint32_t n_sph;
+    /* box meshes of brute-force scenes (DBox): the boxes, their triangles in face order, and every other
+     * primitive ("loose", in BVH order, `type` | index << 8); n_boxes = 0: none (the walks scan prims[]) */
+    const DBox *boxes;
+    const DPrim *box_prims;
+    const DPrim *loose_prims;
+    uint32_t n_boxes, n_loose;
 };
 constexpr uint32_t kPortal = 0x80000000u;
 

@@ -17,6 +17,7 @@ CONFIGS = {
     "M": dict(scene="cbox_grid.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),
     "C3": dict(scene="veach_grid.xml", res=1024, spp=256, gx=4, gy=2, reuse=8),
     "mesh": dict(scene="cbox_mesh.xml", res=1024, spp=64, gx=4, gy=2, reuse=8),
+    "C5": dict(scene="cbox_grid.xml", res=2048, spp=16, gx=8, gy=4, reuse=4, adaptive=3),
 }
 
 
@@ -39,11 +40,19 @@ def child(steps=3, kernels=False):
     dev = amvpt.DeviceScene(sd)
     film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
     lanes = p.film_width * p.film_height * spp
-    dev.render(vd, p, film.data_ptr())
+    flags = int(os.environ.get("AB_FLAGS", "0"), 0)   # amvpt_render_opts.flags (e.g. 32: OPT_NO_BINNING)
+
+    def frame(**kw):
+        if flags or kw:
+            dev.render_ex(vd, p, film.data_ptr(), flags=flags | kw.pop("flags", 0), **kw)
+        else:
+            dev.render(vd, p, film.data_ptr())
+
+    frame()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        dev.render(vd, p, film.data_ptr())
+        frame()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"variant": os.environ.get("AB_VARIANT", "lib"), "msamples_s": round(lanes * steps / dt / 1e6, 2),
@@ -52,7 +61,7 @@ def child(steps=3, kernels=False):
         # one instrumented frame with every chunk on one stream (per-kernel event times do not overlap)
         c = amvpt.Counters()
         if hasattr(amvpt, "OPT_ONE_STREAM"):
-            dev.render_ex(vd, p, film.data_ptr(), counters=c, flags=amvpt.OPT_ONE_STREAM)
+            frame(counters=c, flags=amvpt.OPT_ONE_STREAM)
         else:
             dev.render(vd, p, film.data_ptr(), counters=c)
         torch.cuda.synchronize()

@@ -18,6 +18,8 @@ for st in "$@"; do
     fetch) $S 300 fetch_$c -- rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_fetch_$c -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 $P ;;
     write) $S 300 write_$c -- rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_write_$c -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 $P ;;
     sqA) $S 200 sqA_$c -- rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH --output-format csv -d gpurun_out/${T}_sqA_$c -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 $P ;;
+    abflags) $S 600 abflags_$c -- env AB_CONFIG=$c python -u tools/ab_value.py --kernels --env AB_FLAGS=0 --env AB_FLAGS=32 --env AB_FLAGS=0 --env AB_FLAGS=32 ;;
+    ablib) $S 900 ablib_$c -- env AB_CONFIG=${c%%+*} python -u tools/ab_value.py --kernels $(echo ${c#*+} | tr '+' ' ') ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
   if [ -f gpurun_out/${T}.stop ]; then echo "stopped after $st"; break; fi
