@@ -132,6 +132,39 @@ def test_path_integrator_c1(gpu_ready, amvpt_mod, oracle, res):
     _check(amvpt_mod, oracle, s)
 
 
+def _records(amvpt_mod, oracle, sd, vd, p, flags):
+    torch = _torch()
+    plan = oracle.plan(p)
+    dev = amvpt_mod.DeviceScene(sd)
+    film = torch.zeros((p.film_height, p.film_width, 4), dtype=torch.float32, device="cuda")
+    rec = torch.zeros((plan["lanes"], plan["group"], 8), dtype=torch.float32, device="cuda")
+    dev.render_ex(vd, p, film.data_ptr(), flags=flags, records_ptr=rec.data_ptr())
+    torch.cuda.synchronize()
+    return rec.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", ["grazing_top_face", "m_shape"])
+def test_box_screen_keeps_records(gpu_ready, amvpt_mod, oracle, case):
+    """The brute-force walks screen the Cornell cubes (box meshes) per lane and test only the faces a ray can
+    reach (dgeom.h box_walk).  Its records must equal the full scan's (AMVPT_OPT_NO_BOX_SCREEN) bit for bit on
+    large frames: a camera level with the small cube's top face (y = -0.4), whose camera rays graze that face
+    and its edges, at 128^2 x 16 spp (the stock path tracer, max_depth 8: the bounces hit every face at every
+    angle), and the config-M shape (8 views, G = 8) at 64^2 x 16 spp; plus the first against the oracle."""
+    if case == "grazing_top_face":
+        xml = open(CBOX_PATH).read().replace('origin="0, 0, 3.90" target="0, 0, 0"', 'origin="0, -0.4, 3.9" target="0, -0.4, 0"')
+        assert 'origin="0, -0.4, 3.9"' in xml
+        s = amvpt_mod.load_string(xml, res=128, spp=16)
+    else:
+        s = amvpt_mod.load_file(CBOX, res=64, spp=16, gx=4, gy=2, reuse=8)
+    sd, vd, p = s.describe(0, 0, 0)
+    a = _records(amvpt_mod, oracle, sd, vd, p, 0)
+    b = _records(amvpt_mod, oracle, sd, vd, p, amvpt_mod.OPT_NO_BOX_SCREEN)
+    eq = _bit_equal(a, b).all(axis=(1, 2))
+    assert eq.all(), "%d of %d lanes differ with the box screen" % ((~eq).sum(), eq.size)
+    if case == "grazing_top_face":
+        _check(amvpt_mod, oracle, amvpt_mod.load_string(xml, res=48, spp=16))
+
+
 def _path_with_samples_per_pass(amvpt_mod, n, **defines):
     xml = open(CBOX_PATH).read().replace('<integrator type="path">',
                                          '<integrator type="path"><integer name="samples_per_pass" value="%d"/>' % n)
