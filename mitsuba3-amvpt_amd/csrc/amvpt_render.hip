@@ -1815,6 +1815,91 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(const DScene *Sp, Bufs B
     }
 }
 
+/*
+ * Tile binning inside the walk kernels (AMVPT_BIN_MODE 2; no pass of its own, no copy of the rays): a block takes
+ * tiles of up to kTileRays consecutive entries of its partition, reads each entry's ray once to form its key
+ * (direction octant, Morton code of a 4 x 4 x 4 origin cell: kTileBins keys, octant major, so neighbouring keys
+ * are neighbouring cells), counting-sorts the tile's entry offsets in LDS, and then walks the entries in key
+ * order, re-reading each ray (the tile's rays are still in L2 / the Infinity Cache).  A wave's 64 rays then share
+ * an octant and a small neighbourhood of cells; the result of each walk does not depend on which lane runs it.
+ */
+#ifndef AMVPT_BIN_MODE
+#define AMVPT_BIN_MODE 2   /* 1: k_bin_sort (a partition-wide sort pass with a sorted copy), 2: tile sort in the walks */
+#endif
+#ifndef AMVPT_TILE_CELL_BITS
+#define AMVPT_TILE_CELL_BITS 2
+#endif
+constexpr uint32_t kTileRays = 4096, kTileBins = 8u << (3 * AMVPT_TILE_CELL_BITS);
+AD uint32_t tile_key(const DNode &root, f3 o, f3 d) {
+    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+    auto cell = [&](float v, float lo, float hi) {
+        const float f = (v - lo) / fmaxf(hi - lo, 1e-30f) * (float) (1u << AMVPT_TILE_CELL_BITS);
+        return (uint32_t) min(max((int) f, 0), (int) (1u << AMVPT_TILE_CELL_BITS) - 1);
+    };
+    const uint32_t cx = cell(o.x, root.lo[0], root.hi[0]), cy = cell(o.y, root.lo[1], root.hi[1]),
+                   cz = cell(o.z, root.lo[2], root.hi[2]);
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < AMVPT_TILE_CELL_BITS; ++b)
+        m |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
+    return (oct << (3 * AMVPT_TILE_CELL_BITS)) | m;
+}
+struct TileLds {
+    uint16_t key[kTileRays];
+    uint16_t perm[kTileRays];
+    uint32_t hist[kTileBins];
+};
+/* entries [0, count) of the block's partition, tiles of `tile` entries dealt to the partition's blocks in turn;
+ * key_of(e) -> key, work(e) in key order */
+template <class KeyF, class WorkF>
+AD void tile_binned(uint32_t count, TileLds &L, KeyF key_of, WorkF work) {
+    const uint32_t bpp = gridDim.x / kQParts, bi = blockIdx.x / kQParts;
+    /* tiles of 1024..4096 entries: every block of the partition gets one when the partition is small */
+    uint32_t tile = (count + bpp - 1) / bpp;
+    tile = min(kTileRays, max(1024u, (tile + 255u) & ~255u));
+    constexpr uint32_t per = kTileBins >= 256 ? kTileBins / 256 : 1u;
+    for (uint32_t t0 = bi * tile; t0 < count; t0 += bpp * tile) {
+        const uint32_t n = min(tile, count - t0);
+        for (uint32_t k = threadIdx.x; k < kTileBins; k += blockDim.x) L.hist[k] = 0u;
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+            const uint32_t key = key_of(t0 + e);
+            L.key[e] = (uint16_t) key;
+            (void) atomicAdd(&L.hist[key], 1u);
+        }
+        __syncthreads();
+        /* exclusive scan of the histogram (256 threads, `per` bins each) */
+        uint32_t v[per], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < per; ++k) {
+            v[k] = threadIdx.x * per + k < kTileBins ? L.hist[threadIdx.x * per + k] : 0u;
+            sum += v[k];
+        }
+        const int lane = (int) __lane_id();
+        uint32_t inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o);
+            if (lane >= o) inc += t;
+        }
+        __shared__ uint32_t wsum[4];
+        if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += wsum[w];
+#pragma unroll
+        for (uint32_t k = 0; k < per; ++k) {
+            if (threadIdx.x * per + k < kTileBins) L.hist[threadIdx.x * per + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) L.perm[atomicAdd(&L.hist[L.key[e]], 1u)] = (uint16_t) e;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) work(t0 + L.perm[j]);
+        __syncthreads();
+    }
+}
+
 template <int kWalk, bool kBin = false>
 __global__ void __launch_bounds__(256, (AMVPT_EXTEND_RAYS == 2 && (kWalk == WALK_LANE || kWalk == WALK_LANE_NS)) ? AMVPT_EXTEND2_WAVES
                                                                                                                   : AMVPT_EXTEND_WAVES)
@@ -1827,6 +1912,22 @@ k_extend(KParams P, const DScene *Sp, Bufs B) {
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
     if (blockIdx.x == 0) {
         for (uint32_t q = threadIdx.x; q < kQParts; q += blockDim.x) { B.cnt_out[q * kCntStride] = 0u; B.cnt_nee[q * kCntStride] = 0u; }
+    }
+    if constexpr (kBin && AMVPT_BIN_MODE == 2) {
+        __shared__ TileLds T;
+        const DNode root = load_uniform(S.nodes, 0u);
+        tile_binned(count, T,
+            [&](uint32_t e) {
+                const float4 a = B.q_in[0][pbase + e], b = B.q_in[1][pbase + e];
+                return tile_key(root, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y));
+            },
+            [&](uint32_t e) {
+                const uint32_t i = pbase + e;
+                const float4 a = B.q_in[0][i], b = B.q_in[1][i];
+                const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest};
+                B.hit[i] = hit_rec(walk_closest<kWalk>(sc, r));
+            });
+        return;
     }
     if constexpr (kBin) {
         /* the partition's rays in bin order (k_bin_sort); the hit goes back to the ray's entry */
@@ -1891,6 +1992,22 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
         d = d / dist;
         return Ray{o, d, dist * (1.f - kShadowEps)};
     };
+    if constexpr (kBin && AMVPT_BIN_MODE == 2) {
+        __shared__ TileLds T;
+        const DNode root = load_uniform(S.nodes, 0u);
+        tile_binned(count, T,
+            [&](uint32_t e) {
+                const float4 a = B.nee[0][pbase + e], b = B.nee[1][pbase + e];
+                const f3 o = mk(a.x, a.y, a.z);
+                return tile_key(root, o, mk(b.x, b.y, b.z) - o);
+            },
+            [&](uint32_t e) {
+                const uint32_t i = pbase + e;
+                const float4 a = B.nee[0][i], b = B.nee[1][i];
+                if (!walk_any<kWalk>(sc, nee_ray(a, b))) visible(i, a, b);
+            });
+        return;
+    }
     if constexpr (kBin) {
         /* the partition's NEE rays in bin order (k_bin_sort): (origin, destination), (target, entry); a visible
          * light's result is read from the entry's record */
@@ -4258,7 +4375,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.cnt_nee = cs.cntN;
         B.qcap = qcap;
         B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G * chunk);
-        if (bin_ext || bin_nee)
+        if ((bin_ext || bin_nee) && AMVPT_BIN_MODE == 1)
             for (int k = 0; k < 2; ++k) B.sray[k] = (float4 *) carve(16 * qlen);
         if (wide) {
             for (int k = 0; k < mplanes; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
@@ -4318,7 +4435,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.cnt_in = a_is_in ? cntA : cntB;
             B.cnt_out = a_is_in ? cntB : cntA;
             /* k_extend zeroes cnt_out and cnt_nee */
-            if (bin_ext) {
+            if (bin_ext && AMVPT_BIN_MODE == 1) {
                 T.begin(AMVPT_K_BIN, st);
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false>), dim3(kQParts), dim3(kBinBlock), 0, st, dS, B);
                 T.end(st);
@@ -4336,7 +4453,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             launch_bounce(tab_b, diff, fuse_nee ? walk : -1, dim3(bgrid), lds, st, P, dS, B);
             T.end(st);
             if (!fuse_nee) {
-                if (bin_nee) {
+                if (bin_nee && AMVPT_BIN_MODE == 1) {
                     T.begin(AMVPT_K_BIN, st);
                     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<true>), dim3(kQParts), dim3(kBinBlock), 0, st, dS, B);
                     T.end(st);
