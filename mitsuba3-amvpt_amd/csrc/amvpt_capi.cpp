@@ -798,6 +798,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.n_boxes = n_boxes;
     D.n_loose = n_loose;
     sc->n_boxes = n_boxes;
+    for (int a = 0; a < 3; ++a) { sc->root_lo[a] = nodes[0].lo[a]; sc->root_hi[a] = nodes[0].hi[a]; }
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;

@@ -131,6 +131,7 @@ struct KParams {
      * the lane's virtual index in the render's lane set */
     unsigned long long *rng_in, *rng_out;
     uint32_t box_screen;  /* the brute-force suffix walks screen box meshes (box_walk); 0: AMVPT_OPT_NO_BOX_SCREEN */
+    float bin_lo[3], bin_scale[3];   /* ray binning: the scene box's low corner and cells per unit (bin_key) */
 };
 
 /* the PCG32 a stock-path lane starts the pass with: TEA-seeded, or the previous pass's state (same
@@ -179,6 +180,7 @@ struct Bufs {
     uint4 *lmask_w[24];   /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (mask_planes<G>() each) */
     float *vstate;        /* runtime groups whose per-view state exceeds LDS: VS_FIELDS x G x vs_stride floats */
     float4 *sray[2];      /* ray binning (k_bin_sort): a partition's rays in bin order, (o, d.x | dest), (d.yz | target, entry) */
+    uint16_t *key_out, *key_in, *key_nee;   /* ray binning: bin keys of the pushed paths / NEE records (null: off) */
 };
 
 /* ------------------------------------------------------------------ */
@@ -1523,6 +1525,25 @@ struct PathState {
  * holds it exactly.  The PCG increment's seed v1 is re-derived from the slot (path_seq), not
  * stored.  k_shadow adds NEE into q4's xyz in place.
  */
+/* the bin key of a ray (ray binning, k_bin_sort): direction octant (major) and the Morton code of the
+ * origin's cell in a 2^kBinCellBits-per-axis grid over the scene box */
+#ifndef AMVPT_BIN_CELL_BITS
+#define AMVPT_BIN_CELL_BITS 3   /* origin cells per axis of the bin key: 2^bits (A/B) */
+#endif
+constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
+AD uint32_t bin_key(const KParams &P, f3 o, f3 d) {
+    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+    auto cell = [&](float v, int a) {
+        const float f = (v - P.bin_lo[a]) * P.bin_scale[a];
+        return (uint32_t) min(max((int) f, 0), (int) (1u << kBinCellBits) - 1);
+    };
+    const uint32_t cx = cell(o.x, 0), cy = cell(o.y, 1), cz = cell(o.z, 2);
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < kBinCellBits; ++b)
+        m |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
+    return (oct << (3 * kBinCellBits)) | m;
+}
 AD void store_state(float4 *const *q, uint32_t slot, const PathState &s) {
     const uint32_t bits = (s.depth & 0x1fffffffu) | (s.eta_zero ? 0x20000000u : 0u) |
                           (s.prev_delta ? 0x40000000u : 0u) | (s.valid_ray ? 0x80000000u : 0u);
@@ -1533,6 +1554,12 @@ AD void store_state(float4 *const *q, uint32_t slot, const PathState &s) {
     q[4][slot] = make_float4(s.res.r, s.res.g, s.res.b, bitsf((uint32_t) (s.rng_state >> 32)));
 }
 
+/* a push into the output queue; with ray binning on, also the continuation ray's bin key (k_bin_sort's
+ * histogram pass then reads 2 B per entry instead of the 32-B ray) */
+AD void push_state(const KParams &P, const Bufs &B, uint32_t slot, const PathState &s) {
+    store_state(B.q_out, slot, s);
+    if (B.key_out) B.key_out[slot] = (uint16_t) bin_key(P, s.ray.o, s.ray.d);
+}
 AD PathState load_state(float4 *const *q, uint32_t slot) {
     PathState s;
     float4 a = q[0][slot], b = q[1][slot], c = q[2][slot], d = q[3][slot], e = q[4][slot];
@@ -1621,7 +1648,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
         }
     }
     uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
-    if (ok) store_state(B.q_out, qslot, s);
+    if (ok) push_state(P, B, qslot, s);
     if (B.stats) stat_add(B.stats, 8, ok ? 1ull : 0ull);
 }
 
@@ -1672,7 +1699,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
         }
     }
     uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
-    if (ok) store_state(B.q_out, qslot, s);
+    if (ok) push_state(P, B, qslot, s);
     if (B.stats) stat_add(B.stats, 8, ok ? 1ull : 0ull);
 }
 
@@ -1744,42 +1771,18 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #ifndef AMVPT_BIN_UNI
 #define AMVPT_BIN_UNI 0   /* 1: binned waves take the wave-uniform walk (scalar node loads) instead of the per-lane one */
 #endif
-#ifndef AMVPT_BIN_CELL_BITS
-#define AMVPT_BIN_CELL_BITS 3   /* origin cells per axis of the bin key: 2^bits (A/B) */
-#endif
-constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
-AD uint32_t bin_cell(float v, float lo, float hi) {
-    const float f = (v - lo) / fmaxf(hi - lo, 1e-30f) * (float) (1u << kBinCellBits);
-    return (uint32_t) min(max((int) f, 0), (int) (1u << kBinCellBits) - 1);
-}
-AD uint32_t bin_key(const DNode &root, f3 o, f3 d) {
-    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
-    const uint32_t cx = bin_cell(o.x, root.lo[0], root.hi[0]), cy = bin_cell(o.y, root.lo[1], root.hi[1]),
-                   cz = bin_cell(o.z, root.lo[2], root.hi[2]);
-    uint32_t m = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < kBinCellBits; ++b)
-        m |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
-    return (oct << (3 * kBinCellBits)) | m;
-}
 template <bool kNee>
-__global__ void __launch_bounds__(kBinBlock) k_bin_sort(const DScene *Sp, Bufs B) {
+__global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
     __shared__ uint32_t h[kBins];
     __shared__ uint32_t wsum[kBinBlock / 64];
     const uint32_t part = blockIdx.x;
     const uint32_t count = (kNee ? B.cnt_nee : B.cnt_in)[part * kCntStride], pbase = part * B.qcap;
-    const DNode root = load_uniform(Sp->nodes, 0u);   /* every node ordering starts at the root */
     float4 *const *src = kNee ? B.nee : B.q_in;
-    auto key_of = [&](const float4 &a, const float4 &b) {
-        const f3 o = mk(a.x, a.y, a.z);
-        return bin_key(root, o, kNee ? mk(b.x, b.y, b.z) - o : mk(a.w, b.x, b.y));
-    };
+    const uint16_t *const keys = kNee ? B.key_nee : B.key_in;
     for (uint32_t k = threadIdx.x; k < kBins; k += kBinBlock) h[k] = 0u;
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) {
-        const uint32_t i = pbase + e;
-        (void) atomicAdd(&h[key_of(src[0][i], src[1][i])], 1u);
-    }
+    /* the histogram of the producers' keys (2 B per entry) */
+    for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) (void) atomicAdd(&h[keys[pbase + e]], 1u);
     __syncthreads();
     /* exclusive scan of the histogram: thread t owns bins [t * per, t * per + per) */
     constexpr uint32_t per = kBins >= kBinBlock ? kBins / kBinBlock : 1u;
@@ -1806,97 +1809,22 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(const DScene *Sp, Bufs B
         run += v[k];
     }
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) {
-        const uint32_t i = pbase + e;
-        const float4 a = src[0][i], b = src[1][i];
-        const uint32_t j = pbase + atomicAdd(&h[key_of(a, b)], 1u);
+    /* the scatter, two entries per thread in flight: each ray (32 B) to its bin's next position */
+    auto place = [&](uint32_t i, const float4 &a, const float4 &b, uint32_t key) {
+        const uint32_t j = pbase + atomicAdd(&h[key], 1u);
         B.sray[0][j] = a;
         B.sray[1][j] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
-    }
-}
-
-/*
- * Tile binning inside the walk kernels (AMVPT_BIN_MODE 2; no pass of its own, no copy of the rays): a block takes
- * tiles of up to kTileRays consecutive entries of its partition, reads each entry's ray once to form its key
- * (direction octant, Morton code of a 4 x 4 x 4 origin cell: kTileBins keys, octant major, so neighbouring keys
- * are neighbouring cells), counting-sorts the tile's entry offsets in LDS, and then walks the entries in key
- * order, re-reading each ray (the tile's rays are still in L2 / the Infinity Cache).  A wave's 64 rays then share
- * an octant and a small neighbourhood of cells; the result of each walk does not depend on which lane runs it.
- */
-#ifndef AMVPT_BIN_MODE
-#define AMVPT_BIN_MODE 2   /* 1: k_bin_sort (a partition-wide sort pass with a sorted copy), 2: tile sort in the walks */
-#endif
-#ifndef AMVPT_TILE_CELL_BITS
-#define AMVPT_TILE_CELL_BITS 2
-#endif
-constexpr uint32_t kTileRays = 4096, kTileBins = 8u << (3 * AMVPT_TILE_CELL_BITS);
-AD uint32_t tile_key(const DNode &root, f3 o, f3 d) {
-    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
-    auto cell = [&](float v, float lo, float hi) {
-        const float f = (v - lo) / fmaxf(hi - lo, 1e-30f) * (float) (1u << AMVPT_TILE_CELL_BITS);
-        return (uint32_t) min(max((int) f, 0), (int) (1u << AMVPT_TILE_CELL_BITS) - 1);
     };
-    const uint32_t cx = cell(o.x, root.lo[0], root.hi[0]), cy = cell(o.y, root.lo[1], root.hi[1]),
-                   cz = cell(o.z, root.lo[2], root.hi[2]);
-    uint32_t m = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < AMVPT_TILE_CELL_BITS; ++b)
-        m |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
-    return (oct << (3 * AMVPT_TILE_CELL_BITS)) | m;
-}
-struct TileLds {
-    uint16_t key[kTileRays];
-    uint16_t perm[kTileRays];
-    uint32_t hist[kTileBins];
-};
-/* entries [0, count) of the block's partition, tiles of `tile` entries dealt to the partition's blocks in turn;
- * key_of(e) -> key, work(e) in key order */
-template <class KeyF, class WorkF>
-AD void tile_binned(uint32_t count, TileLds &L, KeyF key_of, WorkF work) {
-    const uint32_t bpp = gridDim.x / kQParts, bi = blockIdx.x / kQParts;
-    /* tiles of 1024..4096 entries: every block of the partition gets one when the partition is small */
-    uint32_t tile = (count + bpp - 1) / bpp;
-    tile = min(kTileRays, max(1024u, (tile + 255u) & ~255u));
-    constexpr uint32_t per = kTileBins >= 256 ? kTileBins / 256 : 1u;
-    for (uint32_t t0 = bi * tile; t0 < count; t0 += bpp * tile) {
-        const uint32_t n = min(tile, count - t0);
-        for (uint32_t k = threadIdx.x; k < kTileBins; k += blockDim.x) L.hist[k] = 0u;
-        __syncthreads();
-        for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
-            const uint32_t key = key_of(t0 + e);
-            L.key[e] = (uint16_t) key;
-            (void) atomicAdd(&L.hist[key], 1u);
-        }
-        __syncthreads();
-        /* exclusive scan of the histogram (256 threads, `per` bins each) */
-        uint32_t v[per], sum = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < per; ++k) {
-            v[k] = threadIdx.x * per + k < kTileBins ? L.hist[threadIdx.x * per + k] : 0u;
-            sum += v[k];
-        }
-        const int lane = (int) __lane_id();
-        uint32_t inc = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(inc, o);
-            if (lane >= o) inc += t;
-        }
-        __shared__ uint32_t wsum[4];
-        if (lane == 63) wsum[threadIdx.x >> 6] = inc;
-        __syncthreads();
-        uint32_t run = inc - sum;
-        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += wsum[w];
-#pragma unroll
-        for (uint32_t k = 0; k < per; ++k) {
-            if (threadIdx.x * per + k < kTileBins) L.hist[threadIdx.x * per + k] = run;
-            run += v[k];
-        }
-        __syncthreads();
-        for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) L.perm[atomicAdd(&L.hist[L.key[e]], 1u)] = (uint16_t) e;
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) work(t0 + L.perm[j]);
-        __syncthreads();
+    for (uint32_t e = threadIdx.x; e < count; e += 2 * kBinBlock) {
+        const uint32_t i0 = pbase + e, i1 = i0 + kBinBlock;
+        const bool two = e + kBinBlock < count;
+        const float4 a0 = src[0][i0], b0 = src[1][i0];
+        const uint32_t k0 = keys[i0];
+        float4 a1 = a0, b1 = b0;
+        uint32_t k1 = 0;
+        if (two) { a1 = src[0][i1]; b1 = src[1][i1]; k1 = keys[i1]; }
+        place(i0, a0, b0, k0);
+        if (two) place(i1, a1, b1, k1);
     }
 }
 
@@ -1912,22 +1840,6 @@ k_extend(KParams P, const DScene *Sp, Bufs B) {
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
     if (blockIdx.x == 0) {
         for (uint32_t q = threadIdx.x; q < kQParts; q += blockDim.x) { B.cnt_out[q * kCntStride] = 0u; B.cnt_nee[q * kCntStride] = 0u; }
-    }
-    if constexpr (kBin && AMVPT_BIN_MODE == 2) {
-        __shared__ TileLds T;
-        const DNode root = load_uniform(S.nodes, 0u);
-        tile_binned(count, T,
-            [&](uint32_t e) {
-                const float4 a = B.q_in[0][pbase + e], b = B.q_in[1][pbase + e];
-                return tile_key(root, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y));
-            },
-            [&](uint32_t e) {
-                const uint32_t i = pbase + e;
-                const float4 a = B.q_in[0][i], b = B.q_in[1][i];
-                const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest};
-                B.hit[i] = hit_rec(walk_closest<kWalk>(sc, r));
-            });
-        return;
     }
     if constexpr (kBin) {
         /* the partition's rays in bin order (k_bin_sort); the hit goes back to the ray's entry */
@@ -1992,22 +1904,6 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
         d = d / dist;
         return Ray{o, d, dist * (1.f - kShadowEps)};
     };
-    if constexpr (kBin && AMVPT_BIN_MODE == 2) {
-        __shared__ TileLds T;
-        const DNode root = load_uniform(S.nodes, 0u);
-        tile_binned(count, T,
-            [&](uint32_t e) {
-                const float4 a = B.nee[0][pbase + e], b = B.nee[1][pbase + e];
-                const f3 o = mk(a.x, a.y, a.z);
-                return tile_key(root, o, mk(b.x, b.y, b.z) - o);
-            },
-            [&](uint32_t e) {
-                const uint32_t i = pbase + e;
-                const float4 a = B.nee[0][i], b = B.nee[1][i];
-                if (!walk_any<kWalk>(sc, nee_ray(a, b))) visible(i, a, b);
-            });
-        return;
-    }
     if constexpr (kBin) {
         /* the partition's NEE rays in bin order (k_bin_sort): (origin, destination), (target, entry); a visible
          * light's result is read from the entry's record */
@@ -2193,7 +2089,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             if (ok && !keep) B.lane_out[s.idx] = make_float4(s.res.r, s.res.g, s.res.b, s.valid_ray ? 1.f : 0.f);
         }
         const uint32_t slot = push_slot(keep, B.cnt_out, B.qcap);
-        if (keep) store_state(B.q_out, slot, s);
+        if (keep) push_state(P, B, slot, s);
         if constexpr (kNee >= 0) continue;
         const uint32_t ns = push_slot(nee, B.cnt_nee, B.qcap);
         if (nee) {
@@ -2203,6 +2099,7 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
             B.nee[0][ns] = make_float4(shr.o.x, shr.o.y, shr.o.z, bitsf(dest));
             B.nee[1][ns] = make_float4(nee_to.x, nee_to.y, nee_to.z, res_nee.r);
             B.nee_gb[ns] = make_float2(res_nee.g, res_nee.b);
+            if (B.key_nee) B.key_nee[ns] = (uint16_t) bin_key(P, shr.o, nee_to - shr.o);
         }
     }
     if (B.stats) { stat_add(B.stats, 0, verts); stat_add(B.stats, 5, shadows); }
@@ -3262,7 +3159,7 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
         }
     }
     const uint32_t qslot = push_slot(push, B.cnt_out, B.qcap);
-    if (push) store_state(B.q_out, qslot, ps);
+    if (push) push_state(P, B, qslot, ps);
     if (B.stats) {
         stat_add(B.stats, 1, st_reuse);
         stat_add(B.stats, 2, st_vis);
@@ -4153,6 +4050,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     P.adapt_w = 1.f / (float) (n_adapt + 1);
     P.trav_mode = trav;
     P.box_screen = (opts.flags & AMVPT_OPT_NO_BOX_SCREEN) ? 0u : 1u;
+    for (int a = 0; a < 3; ++a) {
+        const float ext = scene->root_hi[a] - scene->root_lo[a];
+        P.bin_lo[a] = scene->root_lo[a];
+        P.bin_scale[a] = ext > 0.f ? (float) (1u << kBinCellBits) / ext : 0.f;
+    }
     P.sph = !scene->has_spheres ? 0u : (AMVPT_SPHERE_DEFER && scene->n_sph <= 64u) ? 2u : 1u;
     P.win_rs = K.win_rs;
     P.range_begin = rect ? 0 : lane_begin;
@@ -4217,7 +4119,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds_tab_views = (AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views))
                                      ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;
     const bool vs_global = wide && lds_tab_views + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 65536;
-    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + 32 /* binned rays */ +
+    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + 32 + 6 /* binned rays and their keys */ +
                             (size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G + (G + 7) / 8 +
                             (wide ? (size_t) 4 * 16 * mplanes : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
@@ -4354,6 +4256,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     struct ChunkSet {
         Bufs B{};
         float4 *qa[kQPlanes], *qb[kQPlanes];
+        uint16_t *ka, *kb;              /* ray binning: bin keys of queues A / B (null: off) */
         uint32_t *cntA, *cntB, *cntN;   /* [kQParts * kCntStride] each */
         hipStream_t st;
     } sets[2];
@@ -4375,8 +4278,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.cnt_nee = cs.cntN;
         B.qcap = qcap;
         B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G * chunk);
-        if ((bin_ext || bin_nee) && AMVPT_BIN_MODE == 1)
+        cs.ka = cs.kb = nullptr;
+        B.key_out = B.key_in = B.key_nee = nullptr;
+        if (bin_ext || bin_nee)
             for (int k = 0; k < 2; ++k) B.sray[k] = (float4 *) carve(16 * qlen);
+        if (bin_ext) { cs.ka = (uint16_t *) carve(2 * qlen); cs.kb = (uint16_t *) carve(2 * qlen); }
+        if (bin_nee) B.key_nee = (uint16_t *) carve(2 * qlen);
         if (wide) {
             for (int k = 0; k < mplanes; ++k) B.vreq_w[k] = (uint4 *) carve(16 * chunk);
             for (int k = 0; k < 3 * mplanes; ++k) B.lmask_w[k] = (uint4 *) carve(16 * chunk);
@@ -4434,10 +4341,12 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             }
             B.cnt_in = a_is_in ? cntA : cntB;
             B.cnt_out = a_is_in ? cntB : cntA;
+            B.key_in = a_is_in ? cs.ka : cs.kb;
+            B.key_out = a_is_in ? cs.kb : cs.ka;
             /* k_extend zeroes cnt_out and cnt_nee */
-            if (bin_ext && AMVPT_BIN_MODE == 1) {
+            if (bin_ext) {
                 T.begin(AMVPT_K_BIN, st);
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false>), dim3(kQParts), dim3(kBinBlock), 0, st, dS, B);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false>), dim3(kQParts), dim3(kBinBlock), 0, st, P, B);
                 T.end(st);
             }
             T.begin(AMVPT_K_EXTEND, st);
@@ -4453,9 +4362,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             launch_bounce(tab_b, diff, fuse_nee ? walk : -1, dim3(bgrid), lds, st, P, dS, B);
             T.end(st);
             if (!fuse_nee) {
-                if (bin_nee && AMVPT_BIN_MODE == 1) {
+                if (bin_nee) {
                     T.begin(AMVPT_K_BIN, st);
-                    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<true>), dim3(kQParts), dim3(kBinBlock), 0, st, dS, B);
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<true>), dim3(kQParts), dim3(kBinBlock), 0, st, P, B);
                     T.end(st);
                 }
                 T.begin(AMVPT_K_SHADOW, st);
@@ -4506,6 +4415,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
             for (int k = 0; k < kQPlanes; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
             B.cnt_out = cntA; B.cnt_in = cntB;
+            B.key_out = cs.ka; B.key_in = cs.kb;
             T.mark(st);
             {
                 RoctxScope range_primary("amvpt primary vertex (raygen, visibility, camera selection, MIS)");
@@ -4625,6 +4535,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 HIPCHK(hipMemsetAsync(cntA, 0, (size_t) kQParts * kCntStride * 4, st));
                 for (int k = 0; k < kQPlanes; ++k) { B.q_out[k] = qa[k]; B.q_in[k] = qb[k]; }
                 B.cnt_out = cntA; B.cnt_in = cntB;
+                B.key_out = cs.ka; B.key_in = cs.kb;
                 T.begin(AMVPT_K_RAYGEN, st);
                 hipLaunchKernelGGL(k_raygen_adapt, dim3((cn + 255) / 256), dim3(256), 0, st, P, dviews, B);
                 T.end(st);

@@ -475,7 +475,7 @@ def test_ray_binning_keeps_records(gpu_ready, amvpt_mod, oracle, kw):
         cnt = amvpt_mod.Counters()
         dev.render_ex(vd, p, film.data_ptr(), counters=cnt, flags=flags)
         torch.cuda.synchronize()
-        assert (cnt.as_dict()["kernel_launches"]["k_bin"] > 0) == launched
+        assert (cnt.as_dict()["kernel_launches"]["k_bin"] > 0) == launched, flags
 
 
 @pytest.mark.parametrize("chunk", [8192, 5000])
