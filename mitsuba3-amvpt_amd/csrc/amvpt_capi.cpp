@@ -502,12 +502,15 @@ static void find_boxes(const amvpt_scene_desc *d, const std::vector<DPrim> &prim
         boxes.push_back(B);
     }
     if (boxes.empty()) return;
-    for (uint32_t pi = 0; pi < (uint32_t) prims.size(); ++pi)
-        if (!in_box[pi]) {
-            DPrim q = prims[pi];
-            q.type |= pi << 8;
-            loose.push_back(q);
-        }
+    /* grouped by type (rectangles, triangles, spheres), BVH order within a group: the walks loop over each
+     * group with its own test (the closest-hit rule does not depend on the order) */
+    for (uint32_t type : {(uint32_t) PRIM_RECT, (uint32_t) PRIM_TRI, (uint32_t) PRIM_SPHERE})
+        for (uint32_t pi = 0; pi < (uint32_t) prims.size(); ++pi)
+            if (!in_box[pi] && prims[pi].type == type) {
+                DPrim q = prims[pi];
+                q.type |= pi << 8;
+                loose.push_back(q);
+            }
 }
 
 amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
@@ -797,6 +800,11 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.loose_prims = (const DPrim *) p_loose;
     D.n_boxes = n_boxes;
     D.n_loose = n_loose;
+    D.n_loose_rect = D.n_loose_tri = 0;
+    for (uint32_t j = 0; j < n_loose; ++j) {
+        D.n_loose_rect += (loose_prims[j].type & 0xffu) == PRIM_RECT ? 1u : 0u;
+        D.n_loose_tri += (loose_prims[j].type & 0xffu) == PRIM_TRI ? 1u : 0u;
+    }
     sc->n_boxes = n_boxes;
     for (int a = 0; a < 3; ++a) { sc->root_lo[a] = nodes[0].lo[a]; sc->root_hi[a] = nodes[0].hi[a]; }
     D.n_prims = (uint32_t) prims.size();

@@ -179,7 +179,8 @@ struct Bufs {
     uint4 *vreq_w[8];     /* groups > 16 views (G <= 0 instances): the lane's visibility-request mask (mstore) */
     uint4 *lmask_w[24];   /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (mask_planes<G>() each) */
     float *vstate;        /* runtime groups whose per-view state exceeds LDS: VS_FIELDS x G x vs_stride floats */
-    float4 *sray[2];      /* ray binning (k_bin_sort): a partition's rays in bin order, (o, d.x | dest), (d.yz | target, entry) */
+    float4 *sray[2];      /* ray binning (k_bin_sort): a partition's rays in bin order, 32-B records [2 j], [2 j + 1]:
+                           * (o, d.x | dest), (d.yz | target, entry); sray[1] unused */
     uint16_t *key_out, *key_in, *key_nee;   /* ray binning: bin keys of the pushed paths / NEE records (null: off) */
 };
 
@@ -255,6 +256,8 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.loose_prims = S.loose_prims;
     sc.n_boxes = boxes ? S.n_boxes : 0u;
     sc.n_loose = S.n_loose;
+    sc.n_loose_rect = S.n_loose_rect;
+    sc.n_loose_tri = S.n_loose_tri;
     sc.tnodes = nullptr;
     sc.t_n = 0;
     sc.onodes = nullptr;
@@ -1528,7 +1531,7 @@ struct PathState {
 /* the bin key of a ray (ray binning, k_bin_sort): direction octant (major) and the Morton code of the
  * origin's cell in a 2^kBinCellBits-per-axis grid over the scene box */
 #ifndef AMVPT_BIN_CELL_BITS
-#define AMVPT_BIN_CELL_BITS 3   /* origin cells per axis of the bin key: 2^bits (A/B) */
+#define AMVPT_BIN_CELL_BITS 2   /* origin cells per axis of the bin key: 2^bits; 3 (4096 keys): walks 3 ms faster, sort 16 ms slower (r05d) */
 #endif
 constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
 AD uint32_t bin_key(const KParams &P, f3 o, f3 d) {
@@ -1811,9 +1814,10 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
     __syncthreads();
     /* the scatter, two entries per thread in flight: each ray (32 B) to its bin's next position */
     auto place = [&](uint32_t i, const float4 &a, const float4 &b, uint32_t key) {
+        /* one 32-B record per ray (a whole memory sector per scattered write, not two 16-B halves in two planes) */
         const uint32_t j = pbase + atomicAdd(&h[key], 1u);
-        B.sray[0][j] = a;
-        B.sray[1][j] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
+        B.sray[0][2 * (size_t) j] = a;
+        B.sray[0][2 * (size_t) j + 1] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
     };
     for (uint32_t e = threadIdx.x; e < count; e += 2 * kBinBlock) {
         const uint32_t i0 = pbase + e, i1 = i0 + kBinBlock;
@@ -1846,7 +1850,7 @@ k_extend(KParams P, const DScene *Sp, Bufs B) {
         for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
             const uint32_t j = pbase + e0 + threadIdx.x;
             if (e0 + threadIdx.x < count) {
-                const float4 a = B.sray[0][j], b = B.sray[1][j];
+                const float4 a = B.sray[0][2 * (size_t) j], b = B.sray[0][2 * (size_t) j + 1];
                 const Ray r{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), kLargest};
                 const Hit h = AMVPT_BIN_UNI ? trace_closest<true, 0, kWalk != WALK_LANE_NS>(sc, r) : walk_closest<kWalk>(sc, r);
                 B.hit[fbits(b.z)] = hit_rec(h);
@@ -1910,7 +1914,7 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
         for (uint32_t e0 = blockIdx.x / kQParts * blockDim.x; e0 < count; e0 += pstride) {
             const uint32_t j = pbase + e0 + threadIdx.x;
             if (e0 + threadIdx.x < count) {
-                const float4 a = B.sray[0][j], b = B.sray[1][j];
+                const float4 a = B.sray[0][2 * (size_t) j], b = B.sray[0][2 * (size_t) j + 1];
                 const Ray r = nee_ray(a, b);
                 const bool occ = AMVPT_BIN_UNI ? trace_any<true, 0, kWalk != WALK_LANE_NS>(sc, r) : walk_any<kWalk>(sc, r);
                 if (!occ) {
@@ -4280,8 +4284,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         B.vrec = (float4 *) carve((size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G * chunk);
         cs.ka = cs.kb = nullptr;
         B.key_out = B.key_in = B.key_nee = nullptr;
-        if (bin_ext || bin_nee)
-            for (int k = 0; k < 2; ++k) B.sray[k] = (float4 *) carve(16 * qlen);
+        if (bin_ext || bin_nee) { B.sray[0] = (float4 *) carve(32 * qlen); B.sray[1] = nullptr; }
         if (bin_ext) { cs.ka = (uint16_t *) carve(2 * qlen); cs.kb = (uint16_t *) carve(2 * qlen); }
         if (bin_nee) B.key_nee = (uint16_t *) carve(2 * qlen);
         if (wide) {

@@ -44,7 +44,7 @@ struct SceneRef {
     const DBox *boxes;
     const DPrim *box_prims;
     const DPrim *loose_prims;
-    uint32_t n_boxes, n_loose;
+    uint32_t n_boxes, n_loose, n_loose_rect, n_loose_tri;
 };
 
 
@@ -1114,13 +1114,14 @@ template <bool kSph> AD bool brute_pair_any(const DPrim &a, const DPrim &b, cons
  * can report a hit at all; only those are tested -- with the exact tri_hit and the same (t, scene-order index)
  * rule as the scan, so the walk's hit is the scan's hit, bit for bit.  A face is skipped only when that is
  * certain:
- *   - the crossing point lies more than kBoxEps (box units) outside the face square, or its t lies outside
- *     [0, maxt] by more than kBoxEpsT (1 + |t|), AND the ray is not grazing the face plane
- *     (|d_axis| >= kBoxGraze |d|_max): then tri_hit's own rounding (relative ~1e-7 / sin of the angle to the
- *     plane, below 1e-4 here) cannot move its barycentrics or t across the boundary;
+ *   - the crossing point lies more than kBoxEps (box units) outside the face square -- its t lies outside
+ *     one of the other two axes' slabs widened by kBoxEps -- or its t lies outside [0, maxt] by more than
+ *     kBoxEpsT (1 + |t|), AND the ray is not grazing the face plane (|d_axis| >= kBoxGraze |d|_max): then
+ *     tri_hit's own rounding (relative ~1e-7 / sin of the angle to the plane, below 1e-4 here) cannot move its
+ *     barycentrics or t across the boundary; a NaN anywhere keeps the face;
  *   - in the closest-hit walk, its crossing t exceeds the best hit so far by more than kBoxEpsT (1 + |t|): any
  *     hit on it is farther.
- * A grazing face whose crossing is anywhere near the square is always tested (first).  Lanes take their
+ * A grazing face is always tested (first).  Lanes take their
  * candidate faces in ascending crossing order, one face (two per-lane triangle loads) per round, so a lane
  * that hits its entry face is done after one round; the wave runs until its last lane is.
  */
@@ -1134,26 +1135,48 @@ AD void box_candidates(const DBox &B, const Ray &r, float maxt, float *key, uint
                     fmaf(B.m[10], r.d.z, fmaf(B.m[9], r.d.y, B.m[8] * r.d.x)));
     const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
     const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    /* per axis: the crossings of its two face planes (t0: x = -1, t1: x = +1), and the interval of t over which
+     * the ray lies within the axis's slab widened by kBoxEps ([lo, hi]; empty or unbounded for d = 0) */
+    float t0[3], t1[3], lo[3], hi[3];
+    bool graze[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float inv = __builtin_amdgcn_rcpf(da[a]), oi = -oa[a] * inv;
+        t0[a] = fmaf(-1.f, inv, oi);
+        t1[a] = fmaf(1.f, inv, oi);
+        const float e0 = fmaf(-1.f - kBoxEps, inv, oi), e1 = fmaf(1.f + kBoxEps, inv, oi);
+        lo[a] = fminf(e0, e1);
+        hi[a] = fmaxf(e0, e1);
+        graze[a] = !(fabsf(da[a]) >= kBoxGraze * dmax);
+    }
     cand = 0u;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const int b = (a + 1) % 3, c = (a + 2) % 3;
-        const bool graze = !(fabsf(da[a]) >= kBoxGraze * dmax);
-        const float inv = __builtin_amdgcn_rcpf(da[a]);
+        /* a face's crossing lies within kBoxEps of its square iff it lies in the other two widened slabs */
+        const float l = fmaxf(lo[b], lo[c]), h = fminf(hi[b], hi[c]);
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            const float t = ((side ? 1.f : -1.f) - oa[a]) * inv;
-            const float qb = fabsf(fmaf(da[b], t, oa[b])), qc = fabsf(fmaf(da[c], t, oa[c]));
+            const float t = side ? t1[a] : t0[a];
             const float et = kBoxEpsT * (1.f + fabsf(t));
-            /* near the square; a grazing face: its crossing anywhere within 0.1 of the square (its t is
-             * unreliable), or the ray running within 0.1 of the face plane (tri_hit's determinant is then
-             * rounding noise), NaN included */
-            const bool in_sq = qb <= 1.f + kBoxEps && qc <= 1.f + kBoxEps && t >= -et && t <= maxt + et;
-            const bool near_g = !(qb > 1.1f) || !(qc > 1.1f) || !(fabsf((side ? 1.f : -1.f) - oa[a]) > .1f);
-            const bool c_ = graze ? near_g : in_sq;
-            key[2 * a + side] = graze ? -kInf : t;
-            cand |= c_ ? 1u << (2 * a + side) : 0u;
+            const bool in_sq = !(t < l) && !(t > h) && !(t < -et) && !(t > maxt + et);
+            /* a grazing face is always a candidate, tested first (its crossing's t is unreliable) */
+            key[2 * a + side] = graze[a] ? -kInf : t;
+            cand |= (graze[a] || in_sq) ? 1u << (2 * a + side) : 0u;
         }
+    }
+}
+/* loose primitives [j0, j1) of one type, two records in flight (each reloaded right after its own test, as
+ * brute_closest's scan) */
+template <class F> AD void loose_scan(const SceneRef &sc, uint32_t j0, uint32_t j1, F test) {
+    if (j0 >= j1) return;
+    const uint32_t last = j1 - 1u;
+    DPrim a = load_uniform(sc.loose_prims, j0), b = load_uniform(sc.loose_prims, min(j0 + 1u, last));
+    for (uint32_t j = j0; j < j1; j += 2) {
+        test(a);
+        a = load_uniform(sc.loose_prims, min(j + 2u, last));
+        if (j + 1 < j1) test(b);
+        b = load_uniform(sc.loose_prims, min(j + 3u, last));
     }
 }
 /* kAny: any hit in [0, ray.maxt] (found); else the closest hit (best, best_orig) */
@@ -1210,25 +1233,27 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
     if (sc.n_boxes) {
-        /* the loose primitives (their BVH index in `type`'s upper bits), then the boxes */
-        const uint32_t nl = ufirst(sc.n_loose);
+        /* the loose primitives (their BVH index in `type`'s upper bits) by type -- rectangles, triangles, then
+         * spheres, each group with its own test (one uniform type branch per primitive let the compiler
+         * if-convert both tests into every iteration) -- then the boxes */
+        const uint32_t nl = ufirst(sc.n_loose), nr = ufirst(sc.n_loose_rect), nt = nr + ufirst(sc.n_loose_tri);
         uint64_t dm = 0;
-        for (uint32_t j = 0; j < nl; ++j) {
-            const DPrim p = load_uniform(sc.loose_prims, j);
-            const uint32_t tw = ufirst(p.type), type = tw & 0xffu;
-            if (kSph && type == PRIM_SPHERE) {
-                if (wave_any(sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
-                continue;
-            }
-            float t, u, v;
-            if (prim_hit_b<false>(p, type, ray, t, u, v)) {
+        auto upd = [&](const DPrim &p, bool h, float t, float u, float v) {
+            if (h) {
                 const uint32_t orig = ufirst(p.pad);
                 if (t < best.t || (t == best.t && orig < best_orig)) {
-                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) (tw >> 8);
+                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) (ufirst(p.type) >> 8);
                     best_orig = orig;
                 }
             }
-        }
+        };
+        loose_scan(sc, 0u, nr, [&](const DPrim &p) { float t, u, v; const bool h = rect_hit(p, ray, t, u, v); upd(p, h, t, u, v); });
+        loose_scan(sc, nr, nt, [&](const DPrim &p) { float t, u, v; const bool h = tri_hit(p, ray, t, u, v); upd(p, h, t, u, v); });
+        if constexpr (kSph)
+            for (uint32_t j = nt; j < nl; ++j) {
+                const DPrim p = load_uniform(sc.loose_prims, j);
+                if (wave_any(sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
+            }
         bool found = false;
         box_walk<false>(sc, ray, best, best_orig, found);
         if constexpr (kSph) {
@@ -1302,20 +1327,17 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
     const uint32_t np = ufirst(sc.g->n_prims);
     bool found = skip;
     if (sc.n_boxes) {
-        const uint32_t nl = ufirst(sc.n_loose);
+        const uint32_t nl = ufirst(sc.n_loose), nr = ufirst(sc.n_loose_rect), nt = nr + ufirst(sc.n_loose_tri);
         uint64_t dm = 0;
-        for (uint32_t j = 0; j < nl; ++j) {
-            const DPrim p = load_uniform(sc.loose_prims, j);
-            const uint32_t type = ufirst(p.type) & 0xffu;
-            if (kSph && type == PRIM_SPHERE) {
+        loose_scan(sc, 0u, nr, [&](const DPrim &p) { float t, u, v; const bool h = rect_hit(p, ray, t, u, v); found = found || h; });
+        if (!wave_any(!found)) return found;
+        loose_scan(sc, nr, nt, [&](const DPrim &p) { float t, u, v; const bool h = tri_hit(p, ray, t, u, v); found = found || h; });
+        if (!wave_any(!found)) return found;
+        if constexpr (kSph)
+            for (uint32_t j = nt; j < nl; ++j) {
+                const DPrim p = load_uniform(sc.loose_prims, j);
                 if (wave_any(!found && sphere_maybe(p, ray))) dm |= 1ull << ufirst(p.face);
-                continue;
             }
-            float t, u, v;
-            const bool h = prim_hit_b<false>(p, type, ray, t, u, v);
-            found = found || h;
-            if (!wave_any(!found)) return found;
-        }
         Hit best_unused{kInf, 0.f, 0.f, -1};
         uint32_t orig_unused = 0u;
         box_walk<true>(sc, ray, best_unused, orig_unused, found);

@@ -143,6 +143,7 @@ struct DScene {
     const DPrim *box_prims;
     const DPrim *loose_prims;
     uint32_t n_boxes, n_loose;
+    uint32_t n_loose_rect, n_loose_tri;   /* loose_prims: rectangles, then triangles, then spheres */
 };
 constexpr uint32_t kPortal = 0x80000000u;
 
