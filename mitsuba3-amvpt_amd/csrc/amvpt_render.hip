@@ -1534,6 +1534,10 @@ struct PathState {
 #define AMVPT_BIN_CELL_BITS 2   /* origin cells per axis of the bin key: 2^bits; 3 (4096 keys): walks 3 ms faster, sort 16 ms slower (r05d) */
 #endif
 constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCellBits), kBinBlock = 1024;
+#ifndef AMVPT_BIN_UNROLL
+#define AMVPT_BIN_UNROLL 4   /* entries per thread in flight in k_bin_sort's passes (one 1024-thread block per partition) */
+#endif
+constexpr uint32_t kBinUnroll = AMVPT_BIN_UNROLL;
 AD uint32_t bin_key(const KParams &P, f3 o, f3 d) {
     const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
     auto cell = [&](float v, int a) {
@@ -1784,8 +1788,18 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
     const uint16_t *const keys = kNee ? B.key_nee : B.key_in;
     for (uint32_t k = threadIdx.x; k < kBins; k += kBinBlock) h[k] = 0u;
     __syncthreads();
-    /* the histogram of the producers' keys (2 B per entry) */
-    for (uint32_t e = threadIdx.x; e < count; e += kBinBlock) (void) atomicAdd(&h[keys[pbase + e]], 1u);
+    /* the histogram of the producers' keys (2 B per entry), kBinUnroll loads in flight per thread */
+    for (uint32_t e0 = threadIdx.x; e0 < count; e0 += kBinUnroll * kBinBlock) {
+        uint32_t k[kBinUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kBinUnroll; ++u) {
+            const uint32_t e = e0 + u * kBinBlock;
+            k[u] = e < count ? keys[pbase + e] : kBins;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kBinUnroll; ++u)
+            if (k[u] < kBins) (void) atomicAdd(&h[k[u]], 1u);
+    }
     __syncthreads();
     /* exclusive scan of the histogram: thread t owns bins [t * per, t * per + per) */
     constexpr uint32_t per = kBins >= kBinBlock ? kBins / kBinBlock : 1u;
@@ -1819,16 +1833,17 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
         B.sray[0][2 * (size_t) j] = a;
         B.sray[0][2 * (size_t) j + 1] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
     };
-    for (uint32_t e = threadIdx.x; e < count; e += 2 * kBinBlock) {
-        const uint32_t i0 = pbase + e, i1 = i0 + kBinBlock;
-        const bool two = e + kBinBlock < count;
-        const float4 a0 = src[0][i0], b0 = src[1][i0];
-        const uint32_t k0 = keys[i0];
-        float4 a1 = a0, b1 = b0;
-        uint32_t k1 = 0;
-        if (two) { a1 = src[0][i1]; b1 = src[1][i1]; k1 = keys[i1]; }
-        place(i0, a0, b0, k0);
-        if (two) place(i1, a1, b1, k1);
+    for (uint32_t e0 = threadIdx.x; e0 < count; e0 += kBinUnroll * kBinBlock) {
+        float4 a[kBinUnroll], b[kBinUnroll];
+        uint32_t k[kBinUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kBinUnroll; ++u) {
+            const uint32_t e = min(e0 + u * kBinBlock, count - 1u), i = pbase + e;
+            a[u] = src[0][i]; b[u] = src[1][i]; k[u] = keys[i];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kBinUnroll; ++u)
+            if (e0 + u * kBinBlock < count) place(pbase + e0 + u * kBinBlock, a[u], b[u], k[u]);
     }
 }
 

@@ -1141,7 +1141,9 @@ AD void box_candidates(const DBox &B, const Ray &r, float maxt, float *key, uint
     bool graze[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float inv = __builtin_amdgcn_rcpf(da[a]), oi = -oa[a] * inv;
+        /* box_rcp: a zero component gives +-1e30, not inf -- with inf, (1 + eps) inf - o inf would be NaN and drop
+         * the slab of a ray running parallel to it (AMVPT r05e: one lane in 37 k) */
+        const float inv = box_rcp(da[a]), oi = -oa[a] * inv;
         t0[a] = fmaf(-1.f, inv, oi);
         t1[a] = fmaf(1.f, inv, oi);
         const float e0 = fmaf(-1.f - kBoxEps, inv, oi), e1 = fmaf(1.f + kBoxEps, inv, oi);
