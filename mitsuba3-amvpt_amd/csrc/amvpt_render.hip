@@ -1561,8 +1561,10 @@ AD void store_state(float4 *const *q, uint32_t slot, const PathState &s) {
     q[4][slot] = make_float4(s.res.r, s.res.g, s.res.b, bitsf((uint32_t) (s.rng_state >> 32)));
 }
 
-/* a push into the output queue; with ray binning on, also the continuation ray's bin key (k_bin_sort's
- * histogram pass then reads 2 B per entry instead of the 32-B ray) */
+/* k_bounce's push into the output queue; with ray binning on, also the continuation ray's bin key (k_bin_sort's
+ * histogram pass then reads 2 B per entry instead of the 32-B ray).  The primary stage's pushes carry no key
+ * (the key code would sit in every primary kernel: k_mv_primary 38.9 -> 41.2 ms at config M, r05f), so the
+ * first depth's k_bin_sort forms its keys from the rays */
 AD void push_state(const KParams &P, const Bufs &B, uint32_t slot, const PathState &s) {
     store_state(B.q_out, slot, s);
     if (B.key_out) B.key_out[slot] = (uint16_t) bin_key(P, s.ray.o, s.ray.d);
@@ -1655,7 +1657,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_single(KParams P,
         }
     }
     uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
-    if (ok) push_state(P, B, qslot, s);
+    if (ok) store_state(B.q_out, qslot, s);
     if (B.stats) stat_add(B.stats, 8, ok ? 1ull : 0ull);
 }
 
@@ -1706,7 +1708,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
         }
     }
     uint32_t qslot = push_slot(ok, B.cnt_out, B.qcap);
-    if (ok) push_state(P, B, qslot, s);
+    if (ok) store_state(B.q_out, qslot, s);
     if (B.stats) stat_add(B.stats, 8, ok ? 1ull : 0ull);
 }
 
@@ -1778,7 +1780,7 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #ifndef AMVPT_BIN_UNI
 #define AMVPT_BIN_UNI 0   /* 1: binned waves take the wave-uniform walk (scalar node loads) instead of the per-lane one */
 #endif
-template <bool kNee>
+template <bool kNee, bool kFromRays = false>
 __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
     __shared__ uint32_t h[kBins];
     __shared__ uint32_t wsum[kBinBlock / 64];
@@ -1794,7 +1796,15 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
 #pragma unroll
         for (uint32_t u = 0; u < kBinUnroll; ++u) {
             const uint32_t e = e0 + u * kBinBlock;
-            k[u] = e < count ? keys[pbase + e] : kBins;
+            if (kFromRays) {
+                k[u] = kBins;
+                if (e < count) {
+                    const float4 a = src[0][pbase + e], b = src[1][pbase + e];
+                    k[u] = bin_key(P, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y));
+                }
+            } else {
+                k[u] = e < count ? keys[pbase + e] : kBins;
+            }
         }
 #pragma unroll
         for (uint32_t u = 0; u < kBinUnroll; ++u)
@@ -1839,7 +1849,8 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
 #pragma unroll
         for (uint32_t u = 0; u < kBinUnroll; ++u) {
             const uint32_t e = min(e0 + u * kBinBlock, count - 1u), i = pbase + e;
-            a[u] = src[0][i]; b[u] = src[1][i]; k[u] = keys[i];
+            a[u] = src[0][i]; b[u] = src[1][i];
+            k[u] = kFromRays ? bin_key(P, mk(a[u].x, a[u].y, a[u].z), mk(a[u].w, b[u].x, b[u].y)) : keys[i];
         }
 #pragma unroll
         for (uint32_t u = 0; u < kBinUnroll; ++u)
@@ -3178,7 +3189,7 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
         }
     }
     const uint32_t qslot = push_slot(push, B.cnt_out, B.qcap);
-    if (push) push_state(P, B, qslot, ps);
+    if (push) store_state(B.q_out, qslot, ps);
     if (B.stats) {
         stat_add(B.stats, 1, st_reuse);
         stat_add(B.stats, 2, st_vis);
@@ -4364,7 +4375,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             /* k_extend zeroes cnt_out and cnt_nee */
             if (bin_ext) {
                 T.begin(AMVPT_K_BIN, st);
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false>), dim3(kQParts), dim3(kBinBlock), 0, st, P, B);
+                if (bnc == 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false, true>), dim3(kQParts), dim3(kBinBlock), 0, st, P, B);
+                else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bin_sort<false>), dim3(kQParts), dim3(kBinBlock), 0, st, P, B);
                 T.end(st);
             }
             T.begin(AMVPT_K_EXTEND, st);
