@@ -1538,6 +1538,9 @@ constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCe
 #define AMVPT_BIN_UNROLL 4   /* entries per thread in flight in k_bin_sort's passes (one 1024-thread block per partition) */
 #endif
 constexpr uint32_t kBinUnroll = AMVPT_BIN_UNROLL;
+#ifndef AMVPT_BIN_STAGE
+#define AMVPT_BIN_STAGE 0   /* 1: k_bin_sort stages each batch in LDS and writes runs of one bin (A/B) */
+#endif
 AD uint32_t bin_key(const KParams &P, f3 o, f3 d) {
     const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
     auto cell = [&](float v, int a) {
@@ -1843,6 +1846,74 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
         B.sray[0][2 * (size_t) j] = a;
         B.sray[0][2 * (size_t) j + 1] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
     };
+#if AMVPT_BIN_STAGE
+    /* staged scatter: batches of kStage entries are counting-sorted in LDS first, so the global writes go out
+     * as runs of consecutive records of one bin (consecutive threads, consecutive addresses) */
+    constexpr uint32_t kStage = 2 * kBinBlock;
+    __shared__ float4 stg[2 * kStage];
+    __shared__ uint16_t skey[kStage];
+    __shared__ uint32_t lh[kBins], lbase[kBins];
+    for (uint32_t b0 = 0; b0 < count; b0 += kStage) {
+        const uint32_t n = min(kStage, count - b0);
+        for (uint32_t k = threadIdx.x; k < kBins; k += kBinBlock) lh[k] = 0u;
+        __syncthreads();
+        float4 a[2], b[2];
+        uint32_t k[2], r[2];
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t e = b0 + threadIdx.x + u * kBinBlock, i = pbase + min(e, count - 1u);
+            a[u] = src[0][i]; b[u] = src[1][i];
+            k[u] = kFromRays ? bin_key(P, mk(a[u].x, a[u].y, a[u].z), mk(a[u].w, b[u].x, b[u].y)) : keys[i];
+            r[u] = e < count ? atomicAdd(&lh[k[u]], 1u) : 0u;
+        }
+        __syncthreads();
+        /* the batch's run of each bin: its position in the batch (a scan of lh) and in the partition */
+        for (uint32_t q = threadIdx.x; q < kBins; q += kBinBlock) {
+            const uint32_t c = lh[q];
+            lbase[q] = c ? atomicAdd(&h[q], c) : 0u;   /* the partition position of the run */
+        }
+        uint32_t vv[per], sm = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < per; ++q) {
+            vv[q] = threadIdx.x * per + q < kBins ? lh[threadIdx.x * per + q] : 0u;
+            sm += vv[q];
+        }
+        uint32_t in2 = sm;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(in2, o);
+            if (lane >= o) in2 += t;
+        }
+        __syncthreads();   /* (lh read above, wsum reused) */
+        if (lane == 63) wsum[wave] = in2;
+        __syncthreads();
+        uint32_t run2 = in2 - sm;
+        for (int w = 0; w < wave; ++w) run2 += wsum[w];
+#pragma unroll
+        for (uint32_t q = 0; q < per; ++q) {
+            if (threadIdx.x * per + q < kBins) lh[threadIdx.x * per + q] = run2;   /* batch offset of bin q */
+            run2 += vv[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t e = b0 + threadIdx.x + u * kBinBlock;
+            if (e < count) {
+                const uint32_t sp = lh[k[u]] + r[u], i = pbase + e;
+                stg[2 * sp] = a[u];
+                stg[2 * sp + 1] = kNee ? make_float4(b[u].x, b[u].y, b[u].z, bitsf(i)) : make_float4(b[u].x, b[u].y, bitsf(i), 0.f);
+                skey[sp] = (uint16_t) k[u];
+            }
+        }
+        __syncthreads();
+        for (uint32_t sp = threadIdx.x; sp < n; sp += kBinBlock) {
+            const uint32_t q = skey[sp], j = pbase + lbase[q] + (sp - lh[q]);
+            B.sray[0][2 * (size_t) j] = stg[2 * sp];
+            B.sray[0][2 * (size_t) j + 1] = stg[2 * sp + 1];
+        }
+        __syncthreads();
+    }
+#else
     for (uint32_t e0 = threadIdx.x; e0 < count; e0 += kBinUnroll * kBinBlock) {
         float4 a[kBinUnroll], b[kBinUnroll];
         uint32_t k[kBinUnroll];
@@ -1856,6 +1927,7 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
         for (uint32_t u = 0; u < kBinUnroll; ++u)
             if (e0 + u * kBinBlock < count) place(pbase + e0 + u * kBinBlock, a[u], b[u], k[u]);
     }
+#endif
 }
 
 template <int kWalk, bool kBin = false>
