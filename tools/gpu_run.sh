@@ -11,6 +11,7 @@ for st in "$@"; do
   if [ "$c" = M ] || [ "$c" = "$kind" ]; then P=""; else P="--config $c"; fi
   case $kind in
     tests) $S 900 tests -- python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ;;
+    testslib) $S 900 tests_$c -- env AMVPT_LIB_DIR=$GRAFT_REPO_ROOT/mitsuba3-amvpt_amd/$c python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ;;
     smoke) $S 300 smoke -- python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) $S 500 bench_$c -- python -u bench.py --steps 5 --warmup 1 $P ;;
     quick) $S 300 quick_$c -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --rmse-lanes 0 $P ;;
