@@ -246,6 +246,10 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *desc, amvpt_scene **out)
 amvpt_status amvpt_scene_destroy(amvpt_scene *scene);
 /* BVH statistics for tests / DESIGN: node and primitive count. */
 amvpt_status amvpt_scene_stats(const amvpt_scene *scene, uint32_t *n_nodes, uint32_t *n_prims);
+/* ABI 9, host only (no device needed): the box meshes amvpt_scene_create recognises in a descriptor (a `cube`,
+ * or any 12-triangle mesh tiling the faces of a parallelepiped; used by the brute-force walks of scenes of at
+ * most 48 primitives, DESIGN.md "Box meshes") */
+amvpt_status amvpt_scene_desc_boxes(const amvpt_scene_desc *d, uint32_t *n_boxes);
 
 /* Number of channels of the ImageBlock (4 = RGBW, 5 = RGBAW). */
 uint32_t amvpt_film_channels(const amvpt_params *params);

@@ -158,7 +158,7 @@ def hip_lib():
         for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
                    "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
                    "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal",
-                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build", "amvpt_render_ex"):
+                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build", "amvpt_render_ex", "amvpt_scene_desc_boxes"):
             if hasattr(L, fn):   # older variant builds (AMVPT_LIB_DIR A/B runs) may lack the newest knobs
                 getattr(L, fn).restype = ctypes.c_int
         L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,

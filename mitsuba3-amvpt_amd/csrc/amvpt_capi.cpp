@@ -838,6 +838,30 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     return AMVPT_OK;
 }
 
+amvpt_status amvpt_scene_desc_boxes(const amvpt_scene_desc *d, uint32_t *n_boxes) {
+    if (!d || !n_boxes) { set_error("amvpt_scene_desc_boxes: null argument"); return AMVPT_ERR_INVALID; }
+    const amvpt_status vs = validate_scene(d);
+    if (vs != AMVPT_OK) return vs;
+    /* the primitives in scene order (find_boxes reads type, shape and face only) */
+    std::vector<DPrim> prims;
+    for (uint32_t i = 0; i < d->shape_count; ++i) {
+        const amvpt_shape_desc &s = d->shapes[i];
+        const uint32_t n = s.type == AMVPT_SHAPE_MESH ? s.face_count : 1u;
+        for (uint32_t f = 0; f < n; ++f) {
+            DPrim p{};
+            p.type = s.type == AMVPT_SHAPE_MESH ? PRIM_TRI : s.type == AMVPT_SHAPE_SPHERE ? PRIM_SPHERE : PRIM_RECT;
+            p.shape = i;
+            p.face = f;
+            prims.push_back(p);
+        }
+    }
+    std::vector<DBox> boxes;
+    std::vector<DPrim> bp, lp;
+    find_boxes(d, prims, boxes, bp, lp);
+    *n_boxes = (uint32_t) boxes.size();
+    return AMVPT_OK;
+}
+
 amvpt_status amvpt_scene_destroy(amvpt_scene *scene) {
     if (!scene) return AMVPT_OK;
     for (void *p : scene->allocations) (void) hipFree(p);

@@ -1170,9 +1170,6 @@ AD FilterCoeffs default_filter() {
                         0x1p+1f};
 }
 
-#ifndef AMVPT_SPLAT_OWN
-#define AMVPT_SPLAT_OWN 1   /* row splat: evaluate the lane's own footprint weights and place them in the union box (A/B) */
-#endif
 #ifndef AMVPT_SPLAT_PK
 #define AMVPT_SPLAT_PK 1   /* row splat: packed-f32 products of the two row halves: config-M splat 101.8 -> 97.7 ms (r03y; 0: A/B) */
 #endif
@@ -1207,45 +1204,9 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
         /* inactive lanes hand over v = 0, so their (finite) weights need no masking: the weights are
          * straight-line code, not a branch per evaluation */
         const FilterCoeffs F = default_filter();
-        float wx[6], wyu[6];
-#if AMVPT_SPLAT_OWN
-        /* the lane's own footprint weights (cnt per axis: 5 coalesced, 4 otherwise -- the reference's evaluations,
-         * eval(r + t) for cell t of the footprint), placed into the union box: union cell c is footprint cell
-         * c - s, s = x0 - ux0 in [0, 6 - cnt] when every footprint of the row starts inside the film (a
-         * wave-uniform test; else the per-cell union evaluation).  12 -> 8 / 10 evaluations per lane and view */
-        const int cntf = coalesce ? 5 : 4;   /* ImageBlock::put's cells per axis for the default Gaussian */
-        const bool inner = !wave_any(act && (f.x0 < 0 || f.y0 < 0 || f.nx != cntf || f.ny != cntf));
-        if (inner) {
-            auto place = [&](float r, int s, int hi, int u0, float *w, auto cnt_tag) {
-                constexpr int cnt = decltype(cnt_tag)::value;
-                float own[cnt];
+        float wx[6];
 #pragma unroll
-                for (int t = 0; t < cnt; ++t) own[t] = gaussian_eval(F, r + (float) t);
-#pragma unroll
-                for (int c = 0; c < 6; ++c) {
-                    float v = 0.f;
-#pragma unroll
-                    for (int ss = 0; ss <= 6 - cnt; ++ss)
-                        if (c - ss >= 0 && c - ss < cnt) v = s == ss ? own[c - ss] : v;
-                    w[c] = u0 + c < hi ? v : 0.f;   /* cells past a footprint clipped at the film edge */
-                }
-            };
-            if (coalesce) {
-                place(f.rx, f.x0 - ux0, x1, ux0, wx, std::integral_constant<int, 5>{});
-                place(f.ry, f.y0 - uy0, y1, uy0, wyu, std::integral_constant<int, 5>{});
-            } else {
-                place(f.rx, f.x0 - ux0, x1, ux0, wx, std::integral_constant<int, 4>{});
-                place(f.ry, f.y0 - uy0, y1, uy0, wyu, std::integral_constant<int, 4>{});
-            }
-        } else
-#endif
-        {
-#pragma unroll
-            for (int c = 0; c < 6; ++c) {
-                wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
-                wyu[c] = union_weight(F, f.ry, f.y0, uy0 + c, y0c, y1);
-            }
-        }
+        for (int c = 0; c < 6; ++c) wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
         WinT *const wch = wbase + ch * wn.plane;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -1253,7 +1214,7 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
             float Ky[2], B1y[2], B2y[2], B3y[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const float wy = (h ^ b2) ? wyu[r + 3] : wyu[r];
+                const float wy = union_weight(F, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1);
                 Ky[h] = K * wy;
                 B1y[h] = B1 * dpp_f<DPP_XOR1>(wy);
                 B2y[h] = B2 * dpp_f<DPP_XOR2>(wy);
@@ -1578,7 +1539,8 @@ constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCe
 #endif
 constexpr uint32_t kBinUnroll = AMVPT_BIN_UNROLL;
 #ifndef AMVPT_BIN_STAGE
-#define AMVPT_BIN_STAGE 0   /* 1: k_bin_sort stages each batch in LDS and writes runs of one bin (A/B) */
+#define AMVPT_BIN_STAGE 1   /* k_bin_sort stages each batch in LDS and writes runs of one bin: sort 54.0 -> 50.3 ms,
+                                     * mesh 857 -> 876 Msamples/s (r05h); 0: one scattered write per entry (A/B) */
 #endif
 AD uint32_t bin_key(const KParams &P, f3 o, f3 d) {
     const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);

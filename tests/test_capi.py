@@ -170,3 +170,28 @@ def test_scene_create_accepts_the_loaded_descriptor(amvpt_mod, name):
         L.amvpt_scene_destroy(h)
     else:
         assert rc == 5, L.amvpt_last_error()   # AMVPT_ERR_NO_DEVICE
+
+
+def _box_count(amvpt_mod, nd):
+    L = amvpt_mod.hip_lib()
+    L.amvpt_scene_desc_boxes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+    n = ctypes.c_uint32()
+    assert L.amvpt_scene_desc_boxes(ctypes.byref(nd), ctypes.byref(n)) == 0, L.amvpt_last_error()
+    return n.value
+
+
+def test_box_meshes_are_recognised(amvpt_mod):
+    """amvpt_scene_create's box-mesh detection (find_boxes, host side): the Cornell box's two `cube`s are
+    boxes; its rectangles and the OBJ/PLY meshes are not; a cube with one vertex moved off its corner is not."""
+    s, sd, vd, p = _cbox_desc(amvpt_mod, "cbox_grid.xml")
+    nd, shapes, bsdfs, ems = _copy_scene(amvpt_mod, sd)
+    assert _box_count(amvpt_mod, nd) == 2
+    s2, sd2, _, _ = _cbox_desc(amvpt_mod, "cbox_mesh.xml")
+    nd2, *_keep2 = _copy_scene(amvpt_mod, sd2)
+    assert _box_count(amvpt_mod, nd2) == 0
+    cube = next(i for i in range(nd.shape_count) if shapes[i].type == 1 and shapes[i].face_count == 12)
+    n = 3 * shapes[cube].vertex_count
+    pos = (ctypes.c_float * n)(*[shapes[cube].positions[k] for k in range(n)])
+    pos[0] += 0.05   # vertex 0 leaves its corner
+    shapes[cube].positions = ctypes.cast(pos, ctypes.POINTER(ctypes.c_float))
+    assert _box_count(amvpt_mod, nd) == 1
