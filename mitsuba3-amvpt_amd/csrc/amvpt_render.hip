@@ -247,12 +247,13 @@ template <typename T> AD T *copy_to_lds(const T *src, uint32_t bytes, char *&dst
  */
 template <bool kTab, bool kBvh = true, bool kTree = false, bool kOct = false>
 AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = nullptr, uint32_t n_views = 0,
-                        bool boxes = false) {
+                        bool boxes = false, bool stage_boxes = false) {
     SceneRef sc;
     sc.g = &S;
     /* the brute-force walks' box screening (box_walk) where the kernel asks for it */
     sc.boxes = S.boxes;
     sc.box_prims = S.box_prims;
+    sc.box_lds = false;
     sc.loose_prims = S.loose_prims;
     sc.n_boxes = boxes ? S.n_boxes : 0u;
     sc.n_loose = S.n_loose;
@@ -312,6 +313,12 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
         S.bsdfs = copy_to_lds(S.bsdfs, S.n_bsdfs * (uint32_t) sizeof(DBsdf), dst);
         S.emitters = copy_to_lds(S.emitters, S.n_emitters * (uint32_t) sizeof(DEmitter), dst);
         if (V) *V = copy_to_lds(*V, n_views * (uint32_t) sizeof(DView), dst);
+        sync = true;
+    }
+    /* the box triangles for box_walk's per-lane loads (the caller's dynamic LDS holds box_lds_bytes more) */
+    if (stage_boxes && sc.n_boxes) {
+        sc.box_prims = copy_to_lds(S.box_prims, sc.n_boxes * 12u * (uint32_t) sizeof(DPrim), dst);
+        sc.box_lds = true;
         sync = true;
     }
     if (sync) __syncthreads();
@@ -2219,6 +2226,9 @@ __global__ void __launch_bounds__(256, AMVPT_BOUNCE_WAVES) k_bounce(KParams P, c
  * are the same operations in the same order as the k_extend / k_bounce wavefronts.
  * The work counters (cnt_out of the queue pair) are zeroed by the host before the launch.
  */
+#ifndef AMVPT_BOX_LDS
+#define AMVPT_BOX_LDS 1   /* k_suffix_fused stages the box triangles in LDS for box_walk's per-lane loads (0: L1/L2, A/B) */
+#endif
 #ifndef AMVPT_FUSE_BVH
 /* 1: BVH scenes run k_suffix_fused too (per-lane / wave-uniform walks inside the fused loop).  Off:
  * on the 3.6 k-triangle mesh it measured 519 vs 608 Msamples/s for the wavefront suffix (r03m) --
@@ -2318,7 +2328,8 @@ __global__ void __launch_bounds__(kFusedBlock, kDiff ? AMVPT_FUSED_WAVES : AMVPT
     /* the parked state sits in front of the staged tables (dynamic LDS: [park][tables]) */
     const LdsPark<kPk> pk{(lds_float *) (uint32_t) (uintptr_t) lds + threadIdx.x};
     DScene S = *Sp;
-    SceneRef sc = stage_scene<kTab, false>(S, lds + kFusedParkBytes, P.trav_mode, nullptr, 0, P.box_screen != 0);
+    SceneRef sc = stage_scene<kTab, false>(S, lds + kFusedParkBytes, P.trav_mode, nullptr, 0, P.box_screen != 0,
+                                           AMVPT_BOX_LDS != 0);
     const uint32_t part = blockIdx.x % kQParts;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     uint32_t *const work = B.cnt_out + part * kCntStride;
@@ -4402,6 +4413,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const DScene *dS = (const DScene *) scene->dev_scene_struct;
     const uint32_t fused_blocks = K.fused_blocks;
     const size_t lds = tab_b ? scene->dev.tab_bytes : 0u;                                           /* k_bounce */
+    /* k_suffix_fused: the box triangles staged for box_walk (AMVPT_BOX_LDS) */
+    const size_t box_lds = (AMVPT_BOX_LDS && P.box_screen) ? (size_t) scene->n_boxes * 12u * sizeof(DPrim) : 0u;
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
     const size_t lds_any = lds_ext + ((AMVPT_TREELETS & 1) ? tree_lds_bytes(scene->dev, trav) : 0u);     /* k_shadow: + any-hit treelet */
     const size_t lds_vis = lds_ext + ((AMVPT_TREELETS & 4) ? tree_lds_bytes(scene->dev, trav) : 0u);     /* k_vis */
@@ -4427,7 +4440,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             B.cnt_out = cntB;
             HIPCHK(hipMemsetAsync(cntB, 0, (size_t) kQParts * kCntStride * 4, st));
             T.begin(AMVPT_K_SUFFIX, st);
-            launch_suffix_fused(tab_b, diff, walk, dim3(kQParts * fused_blocks), kFusedParkBytes + lds, st, P, dS, B);
+            launch_suffix_fused(tab_b, diff, walk, dim3(kQParts * fused_blocks), kFusedParkBytes + lds + box_lds, st, P, dS, B);
             T.end(st);
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);

@@ -45,6 +45,7 @@ struct SceneRef {
     const DPrim *box_prims;
     const DPrim *loose_prims;
     uint32_t n_boxes, n_loose, n_loose_rect, n_loose_tri;
+    bool box_lds;             /* box_prims points into the block's LDS (stage_scene stage_boxes) */
 };
 
 
@@ -1209,7 +1210,7 @@ AD void box_walk(const SceneRef &sc, const Ray &ray, Hit &best, uint32_t &best_o
                 cand &= ~(1u << k);
 #pragma unroll
                 for (uint32_t j = 0; j < 2; ++j) {
-                    const DPrim p = load_global(bt, 2u * k + j);
+                    const DPrim p = sc.box_lds ? load_lds(bt, 2u * k + j) : load_global(bt, 2u * k + j);
                     float t, u, v;
                     if (tri_hit(p, ray, t, u, v)) {
                         if (kAny) {
