@@ -1169,6 +1169,23 @@ AD void box_candidates(const DBox &B, const Ray &r, float maxt, float *key, uint
         }
     }
 }
+/*
+ * Does rect_hit certainly miss (for an any-hit segment)?  With the object-space o.z and d.z formed exactly as
+ * rect_hit forms them, rect_hit's t = -o.z / d.z (correctly rounded) is negative when o.z and d.z are nonzero
+ * with the same sign, and exceeds maxt when |o.z| > maxt |d.z| (1 + 2^-20) -- the quotient then exceeds
+ * maxt (1 + 2^-21) before rounding, so its rounded value does too.  Zero or NaN operands never count as a miss.
+ */
+#ifndef AMVPT_RECT_CULL
+#define AMVPT_RECT_CULL 1   /* brute_any skips rectangles its wave certainly misses (A/B) */
+#endif
+AD bool rect_plane_miss(const DPrim &p, const Ray &r) {
+    const float oz = fmadd(p.c[2], r.o.z, fmadd(p.c[1], r.o.y, fmadd(p.c[0], r.o.x, p.c[3])));
+    const float dz = fmadd(p.c[2], r.d.z, fmadd(p.c[1], r.d.y, p.c[0] * r.d.x));
+    const bool nz = oz != 0.f && dz != 0.f && oz == oz && dz == dz;
+    const bool behind = (fbits(oz) >> 31) == (fbits(dz) >> 31);
+    const bool beyond = fabs_(oz) > (r.maxt * fabs_(dz)) * (1.f + 0x1p-20f);
+    return nz && (behind || beyond);
+}
 /* loose primitives [j0, j1) of one type, two records in flight (each reloaded right after its own test, as
  * brute_closest's scan) */
 template <class F> AD void loose_scan(const SceneRef &sc, uint32_t j0, uint32_t j1, F test) {
@@ -1332,7 +1349,15 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
     if (sc.n_boxes) {
         const uint32_t nl = ufirst(sc.n_loose), nr = ufirst(sc.n_loose_rect), nt = nr + ufirst(sc.n_loose_tri);
         uint64_t dm = 0;
-        loose_scan(sc, 0u, nr, [&](const DPrim &p) { float t, u, v; const bool h = rect_hit(p, ray, t, u, v); found = found || h; });
+        loose_scan(sc, 0u, nr, [&](const DPrim &p) {
+            /* a rectangle the wave's open segments certainly do not cross is skipped (rect_plane_miss: its plane
+             * lies behind every origin or beyond every segment's end) -- the NEE segments of a closed room stay
+             * inside it, so its walls drop out; the exact test otherwise */
+            if (AMVPT_RECT_CULL && !wave_any(!found && !rect_plane_miss(p, ray))) return;
+            float t, u, v;
+            const bool h = rect_hit(p, ray, t, u, v);
+            found = found || h;
+        });
         if (!wave_any(!found)) return found;
         loose_scan(sc, nr, nt, [&](const DPrim &p) { float t, u, v; const bool h = tri_hit(p, ray, t, u, v); found = found || h; });
         if (!wave_any(!found)) return found;
