@@ -501,7 +501,7 @@ static void find_boxes(const amvpt_scene_desc *d, const std::vector<DPrim> &prim
         }
         boxes.push_back(B);
     }
-    if (boxes.empty()) return;
+    /* (with no box, every primitive is loose: the typed scans and the rectangle cull still apply) */
     /* grouped by type (rectangles, triangles, spheres), BVH order within a group: the walks loop over each
      * group with its own test (the closest-hit rule does not depend on the order) */
     for (uint32_t type : {(uint32_t) PRIM_RECT, (uint32_t) PRIM_TRI, (uint32_t) PRIM_SPHERE})

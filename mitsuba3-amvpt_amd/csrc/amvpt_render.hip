@@ -255,8 +255,9 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.box_prims = S.box_prims;
     sc.box_lds = false;
     sc.loose_prims = S.loose_prims;
+    /* off (AMVPT_OPT_NO_BOX_SCREEN, or a kernel without brute-force walks): the plain scan of prims[] */
     sc.n_boxes = boxes ? S.n_boxes : 0u;
-    sc.n_loose = S.n_loose;
+    sc.n_loose = boxes ? S.n_loose : 0u;
     sc.n_loose_rect = S.n_loose_rect;
     sc.n_loose_tri = S.n_loose_tri;
     sc.tnodes = nullptr;

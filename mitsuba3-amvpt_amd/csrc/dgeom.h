@@ -267,6 +267,13 @@ struct BoxRay { f3 o, inv, oinv; };
 #ifndef AMVPT_WALK_WW
 #define AMVPT_WALK_WW 2
 #endif
+/* nodes per fetch of the per-lane while-while walks (1: one node per dependent load).  A threaded walk
+ * only moves forward (node + 1 or the skip link), so the nodes [base, base + K) are loaded together and
+ * visited in one unrolled pass -- a descent (node + 1) and a leaf's successor stay inside the fetched
+ * nodes and cost no further round trip to L2.  Same nodes, same order, same hit. */
+#ifndef AMVPT_WALK_WIN
+#define AMVPT_WALK_WIN 1
+#endif
 AD float box_rcp(float d) {
 #if AMVPT_EXACT_BOX
     return 1.f / (d != 0.f ? d : mulsign(1e-30f, d));
@@ -549,17 +556,29 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const Scene
         for (;;) {
             uint32_t lf = 0, lc = 0;
             bool stop = false;
+            auto step = [&](const DNode &n) {
+                const bool hit = box_hit(n, br, tmax_box);
+                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                if (hit && count) {
+                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                    else stop = true;   /* the second leaf: revisit it next round */
+                } else {
+                    node = hit ? node + 1 : skip;
+                }
+            };
             for (;;) {
                 if (!wave_any(lc == 0u && node < nn)) break;
                 if (node < nn && !stop && (kWW == 2 || lc == 0u)) {
-                    const DNode n = ld_node(node);
-                    const bool hit = box_hit(n, br, tmax_box);
-                    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-                    if (hit && count) {
-                        if (lc == 0u) { lf = n.first; lc = count; node = skip; }
-                        else stop = true;   /* the second leaf: revisit it next round */
+                    if constexpr (AMVPT_WALK_WIN > 1) {
+                        const uint32_t base = node;
+                        DNode w[AMVPT_WALK_WIN];
+#pragma unroll
+                        for (int k = 0; k < AMVPT_WALK_WIN; ++k) w[k] = ld_node(min(base + (uint32_t) k, nn - 1u));
+#pragma unroll
+                        for (int k = 0; k < AMVPT_WALK_WIN; ++k)
+                            if (node == base + (uint32_t) k && !stop && (kWW == 2 || lc == 0u)) step(w[k]);
                     } else {
-                        node = hit ? node + 1 : skip;
+                        step(ld_node(node));
                     }
                 }
             }
@@ -770,17 +789,30 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
         for (;;) {
             uint32_t lf = 0, lc = 0;
             bool stop = false;
+            auto step = [&](const DNode &n) {
+                const bool hit = box_hit(n, br, ray.maxt);
+                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+                if (hit && count) {
+                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                    else stop = true;
+                } else {
+                    node = hit ? node + 1 : skip;
+                }
+            };
             for (;;) {
                 if (!wave_any(!found && lc == 0u && node < nn)) break;
                 if (!found && node < nn && !stop && (kWW == 2 || lc == 0u)) {
-                    const DNode n = ld_node(node);
-                    const bool hit = box_hit(n, br, ray.maxt);
-                    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-                    if (hit && count) {
-                        if (lc == 0u) { lf = n.first; lc = count; node = skip; }
-                        else stop = true;
+                    if constexpr (AMVPT_WALK_WIN > 1) {
+                        /* (see trace_closest) */
+                        const uint32_t base = node;
+                        DNode w[AMVPT_WALK_WIN];
+#pragma unroll
+                        for (int k = 0; k < AMVPT_WALK_WIN; ++k) w[k] = ld_node(min(base + (uint32_t) k, nn - 1u));
+#pragma unroll
+                        for (int k = 0; k < AMVPT_WALK_WIN; ++k)
+                            if (node == base + (uint32_t) k && !stop && (kWW == 2 || lc == 0u)) step(w[k]);
                     } else {
-                        node = hit ? node + 1 : skip;
+                        step(ld_node(node));
                     }
                 }
             }
@@ -1252,7 +1284,7 @@ AD void box_walk(const SceneRef &sc, const Ray &ray, Hit &best, uint32_t &best_o
 template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
-    if (sc.n_boxes) {
+    if (sc.n_loose) {
         /* the loose primitives (their BVH index in `type`'s upper bits) by type -- rectangles, triangles, then
          * spheres, each group with its own test (one uniform type branch per primitive let the compiler
          * if-convert both tests into every iteration) -- then the boxes */
@@ -1346,7 +1378,7 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
 template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool skip = false) {
     const uint32_t np = ufirst(sc.g->n_prims);
     bool found = skip;
-    if (sc.n_boxes) {
+    if (sc.n_loose) {
         const uint32_t nl = ufirst(sc.n_loose), nr = ufirst(sc.n_loose_rect), nt = nr + ufirst(sc.n_loose_tri);
         uint64_t dm = 0;
         loose_scan(sc, 0u, nr, [&](const DPrim &p) {
