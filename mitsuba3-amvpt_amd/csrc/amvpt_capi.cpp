@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -439,6 +440,11 @@ static void scene_bsphere(const amvpt_scene_desc *d, float center[3], float &rad
     radius = std::max(ray_eps, radius * (1.f + ray_eps));
 }
 
+#ifndef AMVPT_BVH_OUTER
+#define AMVPT_BVH_OUTER 1    /* BVH scenes keep up to kOuterMax rectangles out of the BVH (0: all in it, A/B) */
+#endif
+static constexpr uint32_t kBrutePrimsHost = 48;   /* dgeom.h kBrutePrims: brute-force scenes have no BVH walk */
+static constexpr float kInf32 = std::numeric_limits<float>::infinity();
 #ifndef AMVPT_BOX_SCREEN
 #define AMVPT_BOX_SCREEN 1   /* box meshes of brute-force scenes get DBox records (0: none, A/B) */
 #endif
@@ -633,6 +639,23 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (!vnrm.empty()) vnrm.resize(vpos.size(), 0.f);
     if (!vuv.empty()) vuv.resize(2 * (vpos.size() / 3), 0.f);
 
+    /* the scene's bounds (all primitives): the ray-binning grid (render_impl) */
+    float scene_lo[3] = {kInf32, kInf32, kInf32}, scene_hi[3] = {-kInf32, -kInf32, -kInf32};
+    for (const BuildPrim &bp : bprims)
+        for (int k = 0; k < 3; ++k) { scene_lo[k] = std::min(scene_lo[k], bp.box.lo[k]); scene_hi[k] = std::max(scene_hi[k], bp.box.hi[k]); }
+    /* BVH scenes with a few rectangles (a room's walls and lights): the rectangles stay out of the BVH and
+     * every walk tests them first (DScene::outer, dgeom.h outer_closest / outer_any) -- their boxes span the
+     * scene, so every ray crossing it descended to their leaves and tested them in divergent leaf code */
+    std::vector<uint32_t> outer_idx;
+    if (AMVPT_BVH_OUTER && scene_prims.size() > kBrutePrimsHost) {
+        std::vector<BuildPrim> keep;
+        for (const BuildPrim &bp : bprims) {
+            if (scene_prims[bp.idx].type == PRIM_RECT) outer_idx.push_back(bp.idx);
+            else keep.push_back(bp);
+        }
+        if (outer_idx.size() <= kOuterMax && !keep.empty()) bprims.swap(keep);
+        else outer_idx.clear();
+    }
     std::vector<DNode> nodes, tnodes, onodes;
     std::vector<DPrim> prims;
     uint32_t oct_stride = 0;   /* nodes per octant copy (0: one copy) */
@@ -686,6 +709,15 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         prims.resize(bprims.size());
         for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
     }
+    std::vector<DPrim> outer;
+    for (uint32_t idx : outer_idx) {
+        DPrim q = scene_prims[idx];
+        q.type |= (uint32_t) prims.size() << 8;
+        outer.push_back(q);
+        prims.push_back(scene_prims[idx]);
+    }
+    const uint32_t n_outer = (uint32_t) outer.size();
+    if (outer.empty()) outer.resize(1);
     if (prims.empty()) prims.resize(1); /* keep a valid pointer */
 
     std::vector<DBsdf> bsdfs(d->bsdf_count);
@@ -762,7 +794,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (box_prims.empty()) box_prims.resize(1);
     if (loose_prims.empty()) loose_prims.resize(1);
     void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes, *p_sph;
-    void *p_boxes, *p_box_prims, *p_loose;
+    void *p_boxes, *p_box_prims, *p_loose, *p_outer;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
     if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
@@ -773,7 +805,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
     UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
-    UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose)
+    UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose) UP(outer, p_outer)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -806,7 +838,13 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         D.n_loose_tri += (loose_prims[j].type & 0xffu) == PRIM_TRI ? 1u : 0u;
     }
     sc->n_boxes = n_boxes;
-    for (int a = 0; a < 3; ++a) { sc->root_lo[a] = nodes[0].lo[a]; sc->root_hi[a] = nodes[0].hi[a]; }
+    D.outer = (const DPrim *) p_outer;
+    D.n_outer = n_outer;
+    sc->n_outer = n_outer;
+    for (int a = 0; a < 3; ++a) {
+        sc->root_lo[a] = bprims.empty() ? nodes[0].lo[a] : scene_lo[a];
+        sc->root_hi[a] = bprims.empty() ? nodes[0].hi[a] : scene_hi[a];
+    }
     D.n_prims = (uint32_t) prims.size();
     D.n_shapes = d->shape_count;
     D.n_emitters = d->emitter_count;
@@ -826,7 +864,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     D.lds_bytes = (uint32_t) ((size_t) D.n_nodes * sizeof(DNode) + prims.size() * sizeof(DPrim));
     sc->n_nodes = D.n_nodes;
-    sc->n_prims = (uint32_t) bprims.size();
+    sc->n_prims = (uint32_t) (bprims.size() + n_outer);
     sc->all_diffuse = d->bsdf_count > 0;
     for (uint32_t i = 0; i < d->bsdf_count; ++i) sc->all_diffuse = sc->all_diffuse && d->bsdfs[i].type == AMVPT_BSDF_DIFFUSE;
     std::vector<DScene> one(1, D);

@@ -46,6 +46,9 @@ struct SceneRef {
     const DPrim *loose_prims;
     uint32_t n_boxes, n_loose, n_loose_rect, n_loose_tri;
     bool box_lds;             /* box_prims points into the block's LDS (stage_scene stage_boxes) */
+    /* BVH scenes: rectangles kept out of the BVH (DScene::outer), tested by every walk before its BVH */
+    const DPrim *outer;
+    uint32_t n_outer;
 };
 
 
@@ -66,6 +69,23 @@ AD bool rect_hit(const DPrim &p, const Ray &r, float &t, float &lx, float &ly) {
     return t >= 0.f && t <= r.maxt && fabs_(local.x) <= 1.f && fabs_(local.y) <= 1.f;
 }
 
+/*
+ * Does rect_hit certainly miss (for an any-hit segment)?  With the object-space o.z and d.z formed exactly as
+ * rect_hit forms them, rect_hit's t = -o.z / d.z (correctly rounded) is negative when o.z and d.z are nonzero
+ * with the same sign, and exceeds maxt when |o.z| > maxt |d.z| (1 + 2^-20) -- the quotient then exceeds
+ * maxt (1 + 2^-21) before rounding, so its rounded value does too.  Zero or NaN operands never count as a miss.
+ */
+#ifndef AMVPT_RECT_CULL
+#define AMVPT_RECT_CULL 1   /* brute_any skips rectangles its wave certainly misses (A/B) */
+#endif
+AD bool rect_plane_miss(const DPrim &p, const Ray &r) {
+    const float oz = fmadd(p.c[2], r.o.z, fmadd(p.c[1], r.o.y, fmadd(p.c[0], r.o.x, p.c[3])));
+    const float dz = fmadd(p.c[2], r.d.z, fmadd(p.c[1], r.d.y, p.c[0] * r.d.x));
+    const bool nz = oz != 0.f && dz != 0.f && oz == oz && dz == dz;
+    const bool behind = (fbits(oz) >> 31) == (fbits(dz) >> 31);
+    const bool beyond = fabs_(oz) > (r.maxt * fabs_(dz)) * (1.f + 0x1p-20f);
+    return nz && (behind || beyond);
+}
 AD bool tri_hit(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
     const f3 p0 = ld3(p.a), e1 = ld3(p.b), e2 = ld3(p.c);   /* edges precomputed by the host */
     f3 pvec = cross(r.d, e2);
@@ -267,12 +287,9 @@ struct BoxRay { f3 o, inv, oinv; };
 #ifndef AMVPT_WALK_WW
 #define AMVPT_WALK_WW 2
 #endif
-/* nodes per fetch of the per-lane while-while walks (1: one node per dependent load).  A threaded walk
- * only moves forward (node + 1 or the skip link), so the nodes [base, base + K) are loaded together and
- * visited in one unrolled pass -- a descent (node + 1) and a leaf's successor stay inside the fetched
- * nodes and cost no further round trip to L2.  Same nodes, same order, same hit. */
-#ifndef AMVPT_WALK_WIN
-#define AMVPT_WALK_WIN 1
+/* the while-while node step's leaf bookkeeping as selects instead of nested branches (0: branches, A/B) */
+#ifndef AMVPT_WALK_SEL
+#define AMVPT_WALK_SEL 1
 #endif
 AD float box_rcp(float d) {
 #if AMVPT_EXACT_BOX
@@ -393,16 +410,50 @@ AD uint32_t mask_pop(uint64_t &m) {
  * lane's result (its box is padded and inclusive), so both walks are exact.
  */
 /*
+ * The rectangles a BVH scene keeps out of its BVH (DScene::outer: a room's walls and lights, whose boxes
+ * span the scene -- every ray crossing the room descended to their leaves).  Each walk tests them first,
+ * wave-uniformly (scalar record loads, no divergence): the closest-hit walks start their BVH walk with the
+ * nearest wall's t as the box-test bound, the any-hit walks skip a rectangle whose plane the wave's open
+ * segments do not cross (rect_plane_miss) and walk the BVH only for the lanes still open.  The (t,
+ * scene-order index) rule and any-hit do not depend on the order of the tests: the same hits.
+ */
+AD void outer_closest(const SceneRef &sc, const Ray &ray, Hit &best, uint32_t &best_orig) {
+    const uint32_t n = ufirst(sc.n_outer);
+    for (uint32_t j = 0; j < n; ++j) {
+        const DPrim p = load_uniform(sc.outer, j);
+        float t, u, v;
+        if (rect_hit(p, ray, t, u, v)) {
+            const uint32_t orig = ufirst(p.pad);
+            if (t < best.t || (t == best.t && orig < best_orig)) {
+                best.t = t; best.u = u; best.v = v; best.prim = (int32_t) (ufirst(p.type) >> 8);
+                best_orig = orig;
+            }
+        }
+    }
+}
+/* skip: the lane needs no test (no ray, or already found) */
+AD bool outer_any(const SceneRef &sc, const Ray &ray, bool skip) {
+    const uint32_t n = ufirst(sc.n_outer);
+    bool found = false;
+    for (uint32_t j = 0; j < n; ++j) {
+        const DPrim p = load_uniform(sc.outer, j);
+        if (!wave_any(!skip && !found && !rect_plane_miss(p, ray))) continue;
+        float t, u, v;
+        const bool h = !skip && rect_hit(p, ray, t, u, v);
+        found = found || h;
+    }
+    return found;
+}
+
+/*
  * Closest hit over the octant treelets (per-lane walks of large BVHs): the ray's direction-octant
  * ordering starts in its LDS treelet and continues at a portal in the same ordering's global copy
  * (indices local to the copy), returning to the treelet at the end of the portal's subtree.  The node
  * sequence is the global walk's, so the hit is the same; speculative while-while as trace_closest.
  */
-AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
-    Hit best{kInf, 0.f, 0.f, -1};
-    uint32_t best_orig = 0xffffffffu;
+AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray, Hit best, uint32_t best_orig) {
     const BoxRay br = box_ray(ray);
-    float tmax_box = ray.maxt;
+    float tmax_box = fminf(ray.maxt, best.t);
     const uint32_t o = (fbits(ray.d.x) >> 31) | ((fbits(ray.d.y) >> 31) << 1) | ((fbits(ray.d.z) >> 31) << 2);
     const DNode *const tn = sc.onodes + (size_t) o * sc.o_n;
     const DNode *const gn = sc.gnodes + (size_t) o * sc.oct_stride;
@@ -461,11 +512,12 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray) {
 template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v);
 /* kSph = false (per-lane walks): the scene has no sphere, the primitive tests carry no float64 code */
 template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
-    if (!kUni && sc.o_n) return trace_closest_tl(sc, ray);
     Hit best{kInf, 0.f, 0.f, -1};
     uint32_t best_orig = 0xffffffffu;
+    outer_closest(sc, ray, best, best_orig);
+    if (!kUni && sc.o_n) return trace_closest_tl(sc, ray, best, best_orig);
     const BoxRay br = box_ray(ray);
-    float tmax_box = ray.maxt;
+    float tmax_box = fminf(ray.maxt, best.t);
     if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
         /* BVHs with direction-octant copies (large ones, walked uniformly by the coherent primary
@@ -556,30 +608,27 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const Scene
         for (;;) {
             uint32_t lf = 0, lc = 0;
             bool stop = false;
-            auto step = [&](const DNode &n) {
-                const bool hit = box_hit(n, br, tmax_box);
-                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-                if (hit && count) {
-                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
-                    else stop = true;   /* the second leaf: revisit it next round */
-                } else {
-                    node = hit ? node + 1 : skip;
-                }
-            };
             for (;;) {
                 if (!wave_any(lc == 0u && node < nn)) break;
                 if (node < nn && !stop && (kWW == 2 || lc == 0u)) {
-                    if constexpr (AMVPT_WALK_WIN > 1) {
-                        const uint32_t base = node;
-                        DNode w[AMVPT_WALK_WIN];
-#pragma unroll
-                        for (int k = 0; k < AMVPT_WALK_WIN; ++k) w[k] = ld_node(min(base + (uint32_t) k, nn - 1u));
-#pragma unroll
-                        for (int k = 0; k < AMVPT_WALK_WIN; ++k)
-                            if (node == base + (uint32_t) k && !stop && (kWW == 2 || lc == 0u)) step(w[k]);
+                    const DNode n = ld_node(node);
+                    const bool hit = box_hit(n, br, tmax_box);
+                    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+#if AMVPT_WALK_SEL
+                    /* one branch per step: the leaf bookkeeping as selects */
+                    const bool leaf = hit && count != 0u, take = leaf && lc == 0u;
+                    stop = leaf && !take;   /* the second leaf: revisit it next round */
+                    lf = take ? n.first : lf;
+                    lc = take ? count : lc;
+                    node = (hit && count == 0u) ? node + 1 : (stop ? node : skip);
+#else
+                    if (hit && count) {
+                        if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                        else stop = true;   /* the second leaf: revisit it next round */
                     } else {
-                        step(ld_node(node));
+                        node = hit ? node + 1 : skip;
                     }
+#endif
                 }
             }
             if (!wave_any(lc != 0u)) break;
@@ -607,7 +656,7 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const Scene
  * of its subtree, and the walk returns to the treelet there.  The nodes tested are the same as the
  * global walk's (same boxes, same order), so the verdict is the same.
  */
-AD bool trace_any_tl(const SceneRef &sc, const Ray &ray) {
+AD bool trace_any_tl(const SceneRef &sc, const Ray &ray, bool found = false) {
     const BoxRay br = box_ray(ray);
     auto leaf_any = [&](uint32_t first, uint32_t count) {
         bool f = false;
@@ -620,7 +669,7 @@ AD bool trace_any_tl(const SceneRef &sc, const Ray &ray) {
     };
     const uint32_t nt = sc.t_n;
     uint32_t node = 0, gend = 0, tres = 0;
-    bool glob = false, found = false;
+    bool glob = false;
     /* speculative while-while (trace_any kWW = 2): a lane holding a leaf steps on until the wave's
      * other lanes hold one too, and stops at a second leaf */
     for (;;) {
@@ -665,6 +714,8 @@ AD void trace_any_uni_tl(const SceneRef &sc, const Ray &r0, bool act0, const Ray
     const BoxRay b0 = box_ray(r0), b1 = box_ray(r1);
     f0 = !act0;
     f1 = !act1 || !two;
+    f0 = f0 || outer_any(sc, r0, f0);
+    f1 = f1 || outer_any(sc, r1, f1);
     const uint32_t nt = ufirst(sc.t_n);
     uint32_t t = 0, g = 0, gend = 0, tres = 0;
     bool glob = false;
@@ -722,12 +773,13 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
             trace_any_uni_tl(sc, ray, true, ray, false, false, f0, f1);
             return f0;
         }
-        return trace_any_tl(sc, ray);
+        return trace_any_tl(sc, ray, outer_any(sc, ray, false));
     }
     const BoxRay br = box_ray(ray);
+    const bool outer_found = outer_any(sc, ray, false);
     if (kUni) {
         const uint32_t nn = ufirst(sc.n_nodes);
-        bool found = false;
+        bool found = outer_found;
         uint32_t node = 0;
         uint64_t dm = 0;   /* kSph = 2: deferred spheres */
         while (node < nn) {
@@ -785,35 +837,30 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
         const uint32_t nn = sc.n_nodes;
         uint32_t node = 0;
         if constexpr (kWW != 0) {
-        bool found = false;
+        bool found = outer_found;
         for (;;) {
             uint32_t lf = 0, lc = 0;
             bool stop = false;
-            auto step = [&](const DNode &n) {
-                const bool hit = box_hit(n, br, ray.maxt);
-                const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
-                if (hit && count) {
-                    if (lc == 0u) { lf = n.first; lc = count; node = skip; }
-                    else stop = true;
-                } else {
-                    node = hit ? node + 1 : skip;
-                }
-            };
             for (;;) {
                 if (!wave_any(!found && lc == 0u && node < nn)) break;
                 if (!found && node < nn && !stop && (kWW == 2 || lc == 0u)) {
-                    if constexpr (AMVPT_WALK_WIN > 1) {
-                        /* (see trace_closest) */
-                        const uint32_t base = node;
-                        DNode w[AMVPT_WALK_WIN];
-#pragma unroll
-                        for (int k = 0; k < AMVPT_WALK_WIN; ++k) w[k] = ld_node(min(base + (uint32_t) k, nn - 1u));
-#pragma unroll
-                        for (int k = 0; k < AMVPT_WALK_WIN; ++k)
-                            if (node == base + (uint32_t) k && !stop && (kWW == 2 || lc == 0u)) step(w[k]);
+                    const DNode n = ld_node(node);
+                    const bool hit = box_hit(n, br, ray.maxt);
+                    const uint32_t count = n.skip_count >> kNodeCountShift, skip = n.skip_count & kNodeSkipMask;
+#if AMVPT_WALK_SEL
+                    const bool leaf = hit && count != 0u, take = leaf && lc == 0u;
+                    stop = leaf && !take;
+                    lf = take ? n.first : lf;
+                    lc = take ? count : lc;
+                    node = (hit && count == 0u) ? node + 1 : (stop ? node : skip);
+#else
+                    if (hit && count) {
+                        if (lc == 0u) { lf = n.first; lc = count; node = skip; }
+                        else stop = true;
                     } else {
-                        step(ld_node(node));
+                        node = hit ? node + 1 : skip;
                     }
+#endif
                 }
             }
             if (!wave_any(lc != 0u)) break;
@@ -821,6 +868,7 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
         }
         return found;
         }
+        if (outer_found) return true;
         while (node < nn) {
             const DNode n = ld_node(node);
             const bool hit = box_hit(n, br, ray.maxt);
@@ -852,6 +900,8 @@ AD void trace_any2_uni(const SceneRef &sc, const Ray &r0, bool act0, const Ray &
     const RayPair R2 = ray_pair(r0, r1);
     const uint32_t nn = ufirst(sc.n_nodes);
     f0 = !act0; f1 = !act1;
+    f0 = f0 || outer_any(sc, r0, f0);
+    f1 = f1 || outer_any(sc, r1, f1);
     uint32_t node = 0;
     uint64_t dm = 0;   /* kSph = 2: deferred spheres */
     while (node < nn) {
@@ -933,7 +983,7 @@ AD void trace_any_lane2(const SceneRef &sc, const Ray &r0, bool act0, const Ray 
         };
         const uint32_t nn = sc.n_nodes;
         LaneWalk w0{act0 ? 0u : nn, 0u, 0u, false}, w1{act1 ? 0u : nn, 0u, 0u, false};
-        bool h0 = false, h1 = false;
+        bool h0 = outer_any(sc, r0, !act0), h1 = outer_any(sc, r1, !act1);
         for (;;) {
             w0.lf = w0.lc = w1.lf = w1.lc = 0u;
             w0.stop = w1.stop = false;
@@ -964,7 +1014,9 @@ AD void trace_closest_lane2(const SceneRef &sc, const Ray &r0, bool act0, const 
     const DNode *const nodes0 = octant_nodes(sc, r0.d), *const nodes1 = octant_nodes(sc, r1.d);
     Hit best0{kInf, 0.f, 0.f, -1}, best1{kInf, 0.f, 0.f, -1};
     uint32_t orig0 = 0xffffffffu, orig1 = 0xffffffffu;
-    float tmax0 = r0.maxt, tmax1 = r1.maxt;
+    outer_closest(sc, r0, best0, orig0);
+    outer_closest(sc, r1, best1, orig1);
+    float tmax0 = fminf(r0.maxt, best0.t), tmax1 = fminf(r1.maxt, best1.t);
     auto walk = [&](auto lds_tag) {
         constexpr bool kL = decltype(lds_tag)::value;
         auto ld_node = [&](const DNode *nodes, uint32_t i) { return kL ? load_lds(nodes, i) : load_global(nodes, i); };
@@ -1014,7 +1066,7 @@ template <int kSph, int N>
 AD void trace_anyN_uni(const SceneRef &sc, const Ray *r, const bool *act, bool *f) {
     BoxRay b[N];
 #pragma unroll
-    for (int h = 0; h < N; ++h) { b[h] = box_ray(r[h]); f[h] = !act[h]; }
+    for (int h = 0; h < N; ++h) { b[h] = box_ray(r[h]); f[h] = !act[h]; f[h] = f[h] || outer_any(sc, r[h], f[h]); }
     const uint32_t nn = ufirst(sc.n_nodes);
     uint32_t node = 0;
     uint64_t dm = 0;   /* kSph = 2: deferred spheres */
@@ -1200,23 +1252,6 @@ AD void box_candidates(const DBox &B, const Ray &r, float maxt, float *key, uint
             cand |= (graze[a] || in_sq) ? 1u << (2 * a + side) : 0u;
         }
     }
-}
-/*
- * Does rect_hit certainly miss (for an any-hit segment)?  With the object-space o.z and d.z formed exactly as
- * rect_hit forms them, rect_hit's t = -o.z / d.z (correctly rounded) is negative when o.z and d.z are nonzero
- * with the same sign, and exceeds maxt when |o.z| > maxt |d.z| (1 + 2^-20) -- the quotient then exceeds
- * maxt (1 + 2^-21) before rounding, so its rounded value does too.  Zero or NaN operands never count as a miss.
- */
-#ifndef AMVPT_RECT_CULL
-#define AMVPT_RECT_CULL 1   /* brute_any skips rectangles its wave certainly misses (A/B) */
-#endif
-AD bool rect_plane_miss(const DPrim &p, const Ray &r) {
-    const float oz = fmadd(p.c[2], r.o.z, fmadd(p.c[1], r.o.y, fmadd(p.c[0], r.o.x, p.c[3])));
-    const float dz = fmadd(p.c[2], r.d.z, fmadd(p.c[1], r.d.y, p.c[0] * r.d.x));
-    const bool nz = oz != 0.f && dz != 0.f && oz == oz && dz == dz;
-    const bool behind = (fbits(oz) >> 31) == (fbits(dz) >> 31);
-    const bool beyond = fabs_(oz) > (r.maxt * fabs_(dz)) * (1.f + 0x1p-20f);
-    return nz && (behind || beyond);
 }
 /* loose primitives [j0, j1) of one type, two records in flight (each reloaded right after its own test, as
  * brute_closest's scan) */

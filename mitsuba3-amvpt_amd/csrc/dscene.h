@@ -144,7 +144,12 @@ struct DScene {
     const DPrim *loose_prims;
     uint32_t n_boxes, n_loose;
     uint32_t n_loose_rect, n_loose_tri;   /* loose_prims: rectangles, then triangles, then spheres */
+    /* BVH scenes: the rectangles kept out of the BVH (amvpt_capi.cpp, at most kOuterMax), each record's
+     * `type` | its index in prims[] << 8 (they follow the BVH's primitives there); n_outer = 0: none */
+    const DPrim *outer;
+    uint32_t n_outer;
 };
+constexpr uint32_t kOuterMax = 8;
 constexpr uint32_t kPortal = 0x80000000u;
 
 } // namespace amvpt
