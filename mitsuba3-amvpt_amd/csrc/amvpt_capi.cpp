@@ -767,6 +767,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
 
     amvpt_scene *sc = new amvpt_scene();
     sc->has_spheres = has_spheres;
+    sc->bvh_tri_only = !bprims.empty();
+    for (const BuildPrim &bp : bprims) sc->bvh_tri_only = sc->bvh_tri_only && scene_prims[bp.idx].type == PRIM_TRI;
     (void) hipGetDevice(&sc->device);
     auto upload = [&](const void *src, size_t bytes, void **dst) -> amvpt_status {
         hipError_t e = hipMalloc(dst, bytes);

@@ -68,17 +68,24 @@ void *g_exchange_ctx = nullptr;
  * k_vis 90 -> 248 ms, k_prim_hit 12 -> 30 ms). */
 /* WALK_LANE_NS: the per-lane walk of a scene without spheres (no float64 sphere code in the suffix walks:
  * the sphere branch cost the mesh k_shadow 191 -> 207 ms once the sphere screen grew it, r04g) */
-enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */, WALK_LANE_NS = 4 };
+/* WALK_LANE_TRI: the per-lane walk of a BVH of triangles only (no type dispatch in the leaf tests: the mesh scenes,
+ * whose rectangles stay out of the BVH, DScene::outer) */
+enum : int { WALK_LANE = 0, WALK_UNI = 1, WALK_BRUTE = 2, WALK_BRUTE_NS = 3 /* no spheres */, WALK_LANE_NS = 4, WALK_LANE_TRI = 5 };
+#ifndef AMVPT_LANE_TRI
+#define AMVPT_LANE_TRI 1   /* triangle-only BVHs take the WALK_LANE_TRI suffix walks (0: WALK_LANE_NS, A/B) */
+#endif
+/* the per-lane walks' primitive set (dgeom.h trace_closest / trace_any kSph): -1 triangles, 0 no spheres, 1 any */
+template <int kWalk> constexpr int walk_sph() { return kWalk == WALK_LANE_TRI ? -1 : kWalk != WALK_LANE_NS ? 1 : 0; }
 #ifndef AMVPT_LANE_NS
 #define AMVPT_LANE_NS 1   /* sphere-free scenes take the WALK_LANE_NS suffix walks (0: WALK_LANE, A/B) */
 #endif
 template <int kWalk> AD Hit walk_closest(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_closest<kWalk == WALK_BRUTE>(sc, r);
-    return trace_closest<kWalk == WALK_UNI, AMVPT_WALK_WW, kWalk != WALK_LANE_NS>(sc, r);
+    return trace_closest<kWalk == WALK_UNI, AMVPT_WALK_WW, walk_sph<kWalk>()>(sc, r);
 }
 template <int kWalk> AD bool walk_any(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_any<kWalk == WALK_BRUTE>(sc, r);
-    return trace_any<kWalk == WALK_UNI, AMVPT_WALK_WW, kWalk != WALK_LANE_NS>(sc, r);
+    return trace_any<kWalk == WALK_UNI, AMVPT_WALK_WW, walk_sph<kWalk>()>(sc, r);
 }
 
 struct KParams {
@@ -3527,11 +3534,13 @@ AMVPT_TU_LOCAL __global__ void k_develop(const float *film, float *out, uint32_t
 void launch_shadow(int walk, bool bin, dim3 grid, size_t lds, hipStream_t st, const KParams &P, const DScene *dS, const Bufs &B)
 #ifdef AMVPT_SHADOW_TU
 {
-    if (bin && walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_NS, true>), grid, dim3(256), lds, st, P, dS, B);
+    if (bin && walk == WALK_LANE_TRI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_TRI, true>), grid, dim3(256), lds, st, P, dS, B);
+    else if (bin && walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_NS, true>), grid, dim3(256), lds, st, P, dS, B);
     else if (bin && walk == WALK_LANE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE, true>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE_NS>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_BRUTE>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_UNI>), grid, dim3(256), lds, st, P, dS, B);
+    else if (walk == WALK_LANE_TRI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_TRI>), grid, dim3(256), lds, st, P, dS, B);
     else if (walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE_NS>), grid, dim3(256), lds, st, P, dS, B);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_shadow<WALK_LANE>), grid, dim3(256), lds, st, P, dS, B);
 }
@@ -4258,7 +4267,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * (AMVPT_COH_UNI, see launch_primary); the incoherent suffix rays keep the per-lane walk */
     const bool uni_coh = uni || (AMVPT_COH_UNI && trav == 0u);
     /* suffix walk: brute force for tiny scenes in auto mode */
-    int walk = uni ? WALK_UNI : (scene->has_spheres || !AMVPT_LANE_NS) ? WALK_LANE : WALK_LANE_NS;
+    int walk = uni ? WALK_UNI : (scene->has_spheres || !AMVPT_LANE_NS) ? WALK_LANE
+                              : (scene->bvh_tri_only && AMVPT_LANE_TRI) ? WALK_LANE_TRI : WALK_LANE_NS;
     if (uni && trav == 0u && K.brute && scene->dev.n_prims <= kBrutePrims) walk = scene->has_spheres ? WALK_BRUTE : WALK_BRUTE_NS;
     const bool diff = diff_rec;                                                                           /* kDiff instances */
     /* NEE traced inside k_bounce (brute-force walks; AMVPT_OPT_SPLIT_NEE keeps k_shadow) */
@@ -4273,7 +4283,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * fused-suffix scenes gain 0.0-0.5 % (r03i) and keep one stream, so their per-kernel HIP-event
      * times are not overlapped (AMVPT_OPT_ONE_STREAM forces one stream everywhere) */
     /* ray binning (k_bin_sort) for the per-lane suffix walks of BVHs read from device memory */
-    const bool lane_walk = (walk == WALK_LANE || walk == WALK_LANE_NS) && !fuse_suffix && scene_lds_bytes(scene->dev, trav) == 0u;
+    const bool lane_walk = (walk == WALK_LANE || walk == WALK_LANE_NS || walk == WALK_LANE_TRI) && !fuse_suffix && scene_lds_bytes(scene->dev, trav) == 0u;
     const bool bin_ext = lane_walk && (AMVPT_BIN & 1) && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const bool bin_nee = lane_walk && (AMVPT_BIN & 2) && !fuse_nee && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
@@ -4469,11 +4479,13 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                 T.end(st);
             }
             T.begin(AMVPT_K_EXTEND, st);
-            if (bin_ext && walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_NS, true>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
+            if (bin_ext && walk == WALK_LANE_TRI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_TRI, true>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
+            else if (bin_ext && walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_NS, true>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             else if (bin_ext) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE, true>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             else if (walk == WALK_BRUTE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE_NS>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_BRUTE) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_BRUTE>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
             else if (walk == WALK_UNI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_UNI>), dim3(bgrid), dim3(256), lds_ext, st, P, dS, B);
+            else if (walk == WALK_LANE_TRI) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_TRI>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             else if (walk == WALK_LANE_NS) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE_NS>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_extend<WALK_LANE>), dim3(bgrid), dim3(256), lds_close, st, P, dS, B);
             T.end(st);

@@ -381,6 +381,7 @@ template <typename T> AD T load_global(const T *base, uint32_t idx) { return loa
  * same bits.
  */
 template <int kSph = 1> AD bool prim_hit_u(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v) {
+    if (kSph < 0) return tri_hit(p, r, t, u, v);   /* a BVH of triangles only (WALK_LANE_TRI) */
     if (type == PRIM_RECT) return rect_hit(p, r, t, u, v);
     if (kSph != 1 || type == PRIM_TRI) return tri_hit(p, r, t, u, v);
     u = v = 0.f;
@@ -510,6 +511,11 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray, Hit best, uint32_t b
 }
 
 template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v);
+/* the per-lane walks' leaf test: kSph -1 a triangle-only BVH (no type dispatch), 0 no spheres, 1 any */
+template <int kSph> AD bool prim_hit_l(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
+    if constexpr (kSph < 0) return tri_hit(p, r, t, u, v);
+    else return prim_hit_b<kSph != 0>(p, p.type, r, t, u, v);
+}
 /* kSph = false (per-lane walks): the scene has no sphere, the primitive tests carry no float64 code */
 template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const SceneRef &sc, const Ray &ray) {
     Hit best{kInf, 0.f, 0.f, -1};
@@ -587,7 +593,7 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const Scene
                 const uint32_t pi = first + i;
                 const DPrim p = !AMVPT_WALK_AS ? sc.prims[pi] : kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
                 float t, u, v;
-                if (prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v)) {
+                if (prim_hit_l<kSph>(p, ray, t, u, v)) {
                     if (t < best.t || (t == best.t && p.pad < best_orig)) {
                         best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
                         best_orig = p.pad;
@@ -830,7 +836,7 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
                 const DPrim p = !AMVPT_WALK_AS ? sc.prims[first + i]
                                 : kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
                 float t, u, v;
-                f = prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v);
+                f = prim_hit_l<kSph>(p, ray, t, u, v);
             }
             return f;
         };
@@ -977,7 +983,7 @@ AD void trace_any_lane2(const SceneRef &sc, const Ray &r0, bool act0, const Ray 
             for (uint32_t i = 0; i < count && !f; ++i) {
                 const DPrim p = kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
                 float t, u, v;
-                f = prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v);
+                f = prim_hit_l<kSph>(p, ray, t, u, v);
             }
             return f;
         };
@@ -1025,7 +1031,7 @@ AD void trace_closest_lane2(const SceneRef &sc, const Ray &r0, bool act0, const 
                 const uint32_t pi = first + i;
                 const DPrim p = kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
                 float t, u, v;
-                if (prim_hit_b<kSph != 0>(p, p.type, ray, t, u, v)) {
+                if (prim_hit_l<kSph>(p, ray, t, u, v)) {
                     if (t < best.t || (t == best.t && p.pad < best_orig)) {
                         best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
                         best_orig = p.pad;

@@ -15,7 +15,8 @@ struct amvpt_scene {
     std::vector<void *> allocations;
     uint32_t n_nodes = 0, n_prims = 0;
     uint32_t n_sph = 0;         /* spheres (<= 64: the wave-uniform walks defer their float64 tests) */
-    uint32_t n_outer = 0;       /* rectangles kept out of the BVH (DScene::outer) */
+    uint32_t n_outer = 0;
+    bool bvh_tri_only = false;  /* every BVH primitive is a triangle (the WALK_LANE_TRI suffix walks) */       /* rectangles kept out of the BVH (DScene::outer) */
     uint32_t n_boxes = 0;       /* box meshes the brute-force walks screen (DScene::boxes) */
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   /* the BVH root box (ray binning's grid) */
     bool has_spheres = false;   /* the brute-force suffix walks take their sphere-free instances otherwise */
