@@ -796,24 +796,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (box_prims.empty()) box_prims.resize(1);
     if (loose_prims.empty()) loose_prims.resize(1);
     void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes, *p_sph;
-    void *p_boxes, *p_box_prims, *p_loose, *p_outer, *p_tris;
-    /* triangle-only BVHs: the BVH's primitives as 48-B records (dscene.h DTri) */
-    std::vector<DTri> tris;
-    {
-        bool tri_only = !bprims.empty();
-        for (const BuildPrim &bp : bprims) tri_only = tri_only && scene_prims[bp.idx].type == PRIM_TRI;
-        if (tri_only)
-            for (size_t i = 0; i < bprims.size(); ++i) {
-                const DPrim &p = prims[i];
-                DTri q{};
-                q.a[0] = p.a[0]; q.a[1] = p.a[1]; q.a[2] = p.a[2]; q.a[3] = p.b[0];
-                q.b[0] = p.b[1]; q.b[1] = p.b[2]; q.b[2] = p.c[0]; q.b[3] = p.c[1];
-                q.c[0] = p.c[2];
-                std::memcpy(&q.c[1], &p.pad, 4);
-                tris.push_back(q);
-            }
-        if (tris.empty()) tris.resize(1);
-    }
+    void *p_boxes, *p_box_prims, *p_loose, *p_outer;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
     if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
@@ -824,7 +807,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
     UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
-    UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose) UP(outer, p_outer) UP(tris, p_tris)
+    UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose) UP(outer, p_outer)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -858,7 +841,6 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     sc->n_boxes = n_boxes;
     D.outer = (const DPrim *) p_outer;
-    D.tris = (const DTri *) p_tris;
     D.n_outer = n_outer;
     sc->n_outer = n_outer;
     for (int a = 0; a < 3; ++a) {

@@ -269,7 +269,6 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.n_loose_tri = S.n_loose_tri;
     sc.outer = S.outer;   /* every BVH walk tests these (dgeom.h outer_closest / outer_any) */
     sc.n_outer = S.n_outer;
-    sc.tris = S.tris;
     sc.tnodes = nullptr;
     sc.t_n = 0;
     sc.onodes = nullptr;

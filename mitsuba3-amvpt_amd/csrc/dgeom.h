@@ -49,7 +49,6 @@ struct SceneRef {
     /* BVH scenes: rectangles kept out of the BVH (DScene::outer), tested by every walk before its BVH */
     const DPrim *outer;
     uint32_t n_outer;
-    const DTri *tris;         /* DScene::tris (global) */
 };
 
 
@@ -512,25 +511,6 @@ AD Hit trace_closest_tl(const SceneRef &sc, const Ray &ray, Hit best, uint32_t b
 }
 
 template <bool kSph> AD bool prim_hit_b(const DPrim &p, uint32_t type, const Ray &r, float &t, float &u, float &v);
-#ifndef AMVPT_TRI48
-#define AMVPT_TRI48 1   /* WALK_LANE_TRI walks read 48-B triangle records (DScene::tris) instead of 64-B DPrims (A/B) */
-#endif
-/* the per-lane walks' record of leaf primitive pi: a triangle-only BVH in device memory reads its 48-B DTri
- * (only the fields tri_hit and the tie-break read are set) */
-template <int kSph, bool kL> AD DPrim leaf_prim(const SceneRef &sc, uint32_t pi) {
-    if constexpr (kSph < 0 && !kL && AMVPT_TRI48) {
-        const DTri q = load_global(sc.tris, pi);
-        DPrim p;
-        p.a[0] = q.a[0]; p.a[1] = q.a[1]; p.a[2] = q.a[2];
-        p.b[0] = q.a[3]; p.b[1] = q.b[0]; p.b[2] = q.b[1];
-        p.c[0] = q.b[2]; p.c[1] = q.b[3]; p.c[2] = q.c[0];
-        p.pad = fbits(q.c[1]);
-        p.type = PRIM_TRI;
-        return p;
-    } else {
-        return !AMVPT_WALK_AS ? sc.prims[pi] : kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
-    }
-}
 /* the per-lane walks' leaf test: kSph -1 a triangle-only BVH (no type dispatch), 0 no spheres, 1 any */
 template <int kSph> AD bool prim_hit_l(const DPrim &p, const Ray &r, float &t, float &u, float &v) {
     if constexpr (kSph < 0) return tri_hit(p, r, t, u, v);
@@ -611,7 +591,7 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD Hit trace_closest(const Scene
         auto leaf_test = [&](uint32_t first, uint32_t count) {
             for (uint32_t i = 0; i < count; ++i) {
                 const uint32_t pi = first + i;
-                const DPrim p = leaf_prim<kSph, kL>(sc, pi);
+                const DPrim p = !AMVPT_WALK_AS ? sc.prims[pi] : kL ? load_lds(sc.prims, pi) : load_global(sc.prims, pi);
                 float t, u, v;
                 if (prim_hit_l<kSph>(p, ray, t, u, v)) {
                     if (t < best.t || (t == best.t && p.pad < best_orig)) {
@@ -853,7 +833,8 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
         auto leaf_any = [&](uint32_t first, uint32_t count) {
             bool f = false;
             for (uint32_t i = 0; i < count && !f; ++i) {
-                const DPrim p = leaf_prim<kSph, kL>(sc, first + i);
+                const DPrim p = !AMVPT_WALK_AS ? sc.prims[first + i]
+                                : kL ? load_lds(sc.prims, first + i) : load_global(sc.prims, first + i);
                 float t, u, v;
                 f = prim_hit_l<kSph>(p, ray, t, u, v);
             }

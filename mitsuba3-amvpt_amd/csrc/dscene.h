@@ -43,12 +43,6 @@ struct alignas(16) DPrim {
     uint32_t pad;            /* scene-order primitive index: closest-hit tie-break */
 };
 
-/* a triangle-only BVH's primitives as 48-B records for the per-lane walks (DScene::tris, same order as prims[]):
- * (p0, e1.x), (e1.yz, e2.xy), (e2.z, scene-order index, 0, 0) -- the fields tri_hit reads, one load in four less */
-struct alignas(16) DTri {
-    float a[4], b[4], c[4];
-};
-
 struct DShape {
     uint32_t type, flip;
     int32_t bsdf, emitter;
@@ -154,7 +148,6 @@ struct DScene {
      * `type` | its index in prims[] << 8 (they follow the BVH's primitives there); n_outer = 0: none */
     const DPrim *outer;
     uint32_t n_outer;
-    const DTri *tris;       /* triangle-only BVHs: prims[] as DTri records (WALK_LANE_TRI walks); else unused */
 };
 constexpr uint32_t kOuterMax = 8;
 constexpr uint32_t kPortal = 0x80000000u;
