@@ -76,8 +76,7 @@ AD bool rect_hit(const DPrim &p, const Ray &r, float &t, float &lx, float &ly) {
  * maxt (1 + 2^-21) before rounding, so its rounded value does too.  Zero or NaN operands never count as a miss.
  */
 #ifndef AMVPT_RECT_CULL
-#define AMVPT_RECT_CULL 3   /* bit 0: the any-hit scans skip rectangles their wave certainly misses; bit 1: the
-                                  * closest-hit scans skip those beyond every lane's best hit so far (A/B) */
+#define AMVPT_RECT_CULL 1   /* brute_any skips rectangles its wave certainly misses (A/B) */
 #endif
 AD bool rect_plane_miss(const DPrim &p, const Ray &r) {
     const float oz = fmadd(p.c[2], r.o.z, fmadd(p.c[1], r.o.y, fmadd(p.c[0], r.o.x, p.c[3])));
@@ -423,13 +422,6 @@ AD void outer_closest(const SceneRef &sc, const Ray &ray, Hit &best, uint32_t &b
     const uint32_t n = ufirst(sc.n_outer);
     for (uint32_t j = 0; j < n; ++j) {
         const DPrim p = load_uniform(sc.outer, j);
-        if (AMVPT_RECT_CULL & 2) {
-            /* a rectangle every lane's plane crossing puts behind its origin or beyond its best hit so far
-             * cannot become (or tie) the closest hit (rect_plane_miss against [0, best.t]) */
-            Ray rr = ray;
-            rr.maxt = fminf(ray.maxt, best.t);
-            if (!wave_any(!rect_plane_miss(p, rr))) continue;
-        }
         float t, u, v;
         if (rect_hit(p, ray, t, u, v)) {
             const uint32_t orig = ufirst(p.pad);
@@ -1348,16 +1340,7 @@ template <bool kSph> AD Hit brute_closest(const SceneRef &sc, const Ray &ray) {
                 }
             }
         };
-        loose_scan(sc, 0u, nr, [&](const DPrim &p) {
-            if (AMVPT_RECT_CULL & 2) {   /* (see outer_closest) */
-                Ray rr = ray;
-                rr.maxt = fminf(ray.maxt, best.t);
-                if (!wave_any(!rect_plane_miss(p, rr))) return;
-            }
-            float t, u, v;
-            const bool h = rect_hit(p, ray, t, u, v);
-            upd(p, h, t, u, v);
-        });
+        loose_scan(sc, 0u, nr, [&](const DPrim &p) { float t, u, v; const bool h = rect_hit(p, ray, t, u, v); upd(p, h, t, u, v); });
         loose_scan(sc, nr, nt, [&](const DPrim &p) { float t, u, v; const bool h = tri_hit(p, ray, t, u, v); upd(p, h, t, u, v); });
         if constexpr (kSph)
             for (uint32_t j = nt; j < nl; ++j) {
@@ -1443,7 +1426,7 @@ template <bool kSph> AD bool brute_any(const SceneRef &sc, const Ray &ray, bool 
             /* a rectangle the wave's open segments certainly do not cross is skipped (rect_plane_miss: its plane
              * lies behind every origin or beyond every segment's end) -- the NEE segments of a closed room stay
              * inside it, so its walls drop out; the exact test otherwise */
-            if ((AMVPT_RECT_CULL & 1) && !wave_any(!found && !rect_plane_miss(p, ray))) return;
+            if (AMVPT_RECT_CULL && !wave_any(!found && !rect_plane_miss(p, ray))) return;
             float t, u, v;
             const bool h = rect_hit(p, ray, t, u, v);
             found = found || h;
