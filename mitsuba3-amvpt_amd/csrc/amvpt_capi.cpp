@@ -607,6 +607,12 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
                             *P2 = s.positions + 3 * s.faces[3 * f + 2];
                 /* p0 and the two edges (the f32 differences tri_hit would form: same bits) */
                 for (int k = 0; k < 3; ++k) { p.a[k] = P0[k]; p.b[k] = P1[k] - P0[k]; p.c[k] = P2[k] - P0[k]; }
+                /* the spare fourth words: the face's absolute vertex indices (compute_si reads the vertices without
+                 * a dependent load of the face table) */
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t vi = o.vbase + s.faces[3 * f + k];
+                    std::memcpy(k == 0 ? &p.a[3] : k == 1 ? &p.b[3] : &p.c[3], &vi, 4);
+                }
                 p.type = PRIM_TRI; p.shape = i; p.face = f;
                 p.pad = (uint32_t) scene_prims.size();
                 BuildPrim bp;

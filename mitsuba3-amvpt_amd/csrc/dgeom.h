@@ -1538,8 +1538,8 @@ AD SI compute_si(const SceneRef &sc, const Ray &ray, const Hit &h) {
         si.sh.n = fn;
         dp_du = ld3(s.frame_s);
     } else if (pr.type == PRIM_TRI) {
-        const uint32_t *fi = sc.g->faces + 3 * (size_t) (s.fbase + pr.face);
-        uint32_t i0 = s.vbase + fi[0], i1 = s.vbase + fi[1], i2 = s.vbase + fi[2];
+        /* the record's fourth words: vbase + faces[3 (fbase + face) + k] (amvpt_capi.cpp) */
+        const uint32_t i0 = fbits(pr.a[3]), i1 = fbits(pr.b[3]), i2 = fbits(pr.c[3]);
         f3 p0 = ld3(sc.g->vpos + 3 * (size_t) i0), p1 = ld3(sc.g->vpos + 3 * (size_t) i1),
            p2 = ld3(sc.g->vpos + 3 * (size_t) i2);
         float b1 = h.u, b2 = h.v, b0 = 1.f - b1 - b2;

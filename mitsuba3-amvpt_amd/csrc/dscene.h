@@ -37,7 +37,8 @@ constexpr uint32_t kNodeSkipMask = 0x0fffffffu, kNodeCountShift = 28, kMaxLeafPr
 constexpr uint32_t kUniformNodeLimit = 255, kLdsSceneBytes = 48 * 1024;
 
 struct alignas(16) DPrim {
-    /* rect: rows 0..2 of to_object; tri: p0, p1 - p0, p2 - p0 (xyz); sphere: a = (center, radius) */
+    /* rect: rows 0..2 of to_object; tri: p0, p1 - p0, p2 - p0 (xyz) and the three absolute vertex indices (the
+     * fourth words, as bits); sphere: a = (center, radius) */
     float a[4], b[4], c[4];
     uint32_t type, shape, face;
     uint32_t pad;            /* scene-order primitive index: closest-hit tie-break */
