@@ -441,7 +441,8 @@ static void scene_bsphere(const amvpt_scene_desc *d, float center[3], float &rad
 }
 
 #ifndef AMVPT_BVH_OUTER
-#define AMVPT_BVH_OUTER 1    /* BVH scenes keep up to kOuterMax rectangles out of the BVH (0: all in it, A/B) */
+#define AMVPT_BVH_OUTER 1    /* BVH scenes keep up to kOuterMax rectangles out of the BVH (0: all in it; 2: the
+                                     * brute-force scenes' BVH too -- their coherent walks, A/B) */
 #endif
 static constexpr uint32_t kBrutePrimsHost = 48;   /* dgeom.h kBrutePrims: brute-force scenes have no BVH walk */
 static constexpr float kInf32 = std::numeric_limits<float>::infinity();
@@ -653,7 +654,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
      * every walk tests them first (DScene::outer, dgeom.h outer_closest / outer_any) -- their boxes span the
      * scene, so every ray crossing it descended to their leaves and tested them in divergent leaf code */
     std::vector<uint32_t> outer_idx;
-    if (AMVPT_BVH_OUTER && scene_prims.size() > kBrutePrimsHost) {
+    if (AMVPT_BVH_OUTER && (scene_prims.size() > kBrutePrimsHost || AMVPT_BVH_OUTER >= 2)) {
         std::vector<BuildPrim> keep;
         for (const BuildPrim &bp : bprims) {
             if (scene_prims[bp.idx].type == PRIM_RECT) outer_idx.push_back(bp.idx);
