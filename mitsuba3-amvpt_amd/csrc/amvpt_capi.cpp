@@ -441,8 +441,9 @@ static void scene_bsphere(const amvpt_scene_desc *d, float center[3], float &rad
 }
 
 #ifndef AMVPT_BVH_OUTER
-#define AMVPT_BVH_OUTER 1    /* BVH scenes keep up to kOuterMax rectangles out of the BVH (0: all in it; 2: the
-                                     * brute-force scenes' BVH too -- their coherent walks, A/B) */
+#define AMVPT_BVH_OUTER 2    /* up to kOuterMax rectangles stay out of the BVH: 2 in every scene (the brute-force
+                                     * scenes' coherent walks too: config-M k_vis 44.2 -> 35.3 ms, r05u), 1 in scenes of
+                                     * more than kBrutePrims primitives only, 0 none (A/B) */
 #endif
 static constexpr uint32_t kBrutePrimsHost = 48;   /* dgeom.h kBrutePrims: brute-force scenes have no BVH walk */
 static constexpr float kInf32 = std::numeric_limits<float>::infinity();
