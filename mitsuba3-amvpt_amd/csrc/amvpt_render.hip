@@ -1188,8 +1188,8 @@ AD FilterCoeffs default_filter() {
 }
 
 #ifndef AMVPT_SPLAT_SEL
-#define AMVPT_SPLAT_SEL 0   /* row splat: bit 0 channel picks as selects; bit 1 the quad column-weight exchanges
-                             * hoisted out of the row loop; bit 2 union-cell arguments from one offset and a mask (A/B) */
+#define AMVPT_SPLAT_SEL 1   /* row splat: the channel picks as selects on lane masks (0: a pick by lane index, which
+                             * compiled to a branch tree; r05v: splat 85.0 -> 83.3 ms at M, 346.8 -> 343.4 at C3) */
 #endif
 #ifndef AMVPT_SPLAT_PK
 #define AMVPT_SPLAT_PK 1   /* row splat: packed-f32 products of the two row halves: config-M splat 101.8 -> 97.7 ms (r03y; 0: A/B) */
@@ -1216,7 +1216,7 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
         float v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = act ? vals[c] : 0.f;
-#if AMVPT_SPLAT_SEL & 1
+#if AMVPT_SPLAT_SEL
         /* v[ch ^ j] as two selects on lane-constant masks (a pick by a lane-varying index compiled to a
          * branch tree with exec-mask juggling) */
         const bool c0 = (lane & 1) != 0, c1 = (lane & 2) != 0;
@@ -1239,28 +1239,8 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
          * straight-line code, not a branch per evaluation */
         const FilterCoeffs F = default_filter();
         float wx[6];
-#if AMVPT_SPLAT_SEL & 4
-        /* union cell c's argument r + (float) (ux0 + c - x0): the integer offset is small, so (float) (ux0 - x0)
-         * + c is exact and the sum the same bits; the own-footprint cells as a bit mask */
-        auto cells = [](int lo, int hi) { return (uint32_t) ((1 << max(hi, 0)) - 1) & ~(uint32_t) ((1 << max(lo, 0)) - 1); };
-        const uint32_t mx = cells(x0c - ux0, x1 - ux0), my = cells(y0c - uy0, y1 - uy0);
-        const float ox = (float) (ux0 - f.x0), oy = (float) (uy0 - f.y0);
-        auto wgt = [&](float r, float o, int c, uint32_t m) {
-            const float w = gaussian_eval(F, r + (o + (float) c));
-            return ((m >> c) & 1u) ? w : 0.f;
-        };
-#pragma unroll
-        for (int c = 0; c < 6; ++c) wx[c] = wgt(f.rx, ox, c, mx);
-#else
 #pragma unroll
         for (int c = 0; c < 6; ++c) wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
-#endif
-#if AMVPT_SPLAT_SEL & 2
-        /* the quad partners' column weights, once for all rows */
-        float wx1[6], wx2[6], wx3[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) { wx1[c] = dpp_f<DPP_XOR1>(wx[c]); wx2[c] = dpp_f<DPP_XOR2>(wx[c]); wx3[c] = dpp_f<DPP_XOR3>(wx[c]); }
-#endif
         WinT *const wch = wbase + ch * wn.plane;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -1268,11 +1248,7 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
             float Ky[2], B1y[2], B2y[2], B3y[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-#if AMVPT_SPLAT_SEL & 4
-                const float wy = wgt(f.ry, oy, r + 3 * (h ^ b2), my);
-#else
                 const float wy = union_weight(F, f.ry, f.y0, uy0 + r + 3 * (h ^ b2), y0c, y1);
-#endif
                 Ky[h] = K * wy;
                 B1y[h] = B1 * dpp_f<DPP_XOR1>(wy);
                 B2y[h] = B2 * dpp_f<DPP_XOR2>(wy);
@@ -1288,15 +1264,10 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
             const f2v Ky2 = {Ky[0], Ky[1]}, B1y2 = {B1y[0], B1y[1]}, B2y2 = {B2y[0], B2y[1]}, B3y2 = {B3y[0], B3y[1]};
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
-#if AMVPT_SPLAT_SEL & 2
-                const float x1v = wx1[c], x2v = wx2[c], x3v = wx3[c];
-#else
-                const float x1v = dpp_f<DPP_XOR1>(wx[c]), x2v = dpp_f<DPP_XOR2>(wx[c]), x3v = dpp_f<DPP_XOR3>(wx[c]);
-#endif
                 f2v a = Ky2 * (f2v) wx[c];
-                a = __builtin_elementwise_fma((f2v) x1v, B1y2, a);
-                a = __builtin_elementwise_fma((f2v) x2v, B2y2, a);
-                a = __builtin_elementwise_fma((f2v) x3v, B3y2, a);
+                a = __builtin_elementwise_fma((f2v) dpp_f<DPP_XOR1>(wx[c]), B1y2, a);
+                a = __builtin_elementwise_fma((f2v) dpp_f<DPP_XOR2>(wx[c]), B2y2, a);
+                a = __builtin_elementwise_fma((f2v) dpp_f<DPP_XOR3>(wx[c]), B3y2, a);
                 z[c] = a.x + dpp_f<DPP_ROR4>(a.y);
             }
 #else
