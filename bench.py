@@ -269,6 +269,8 @@ def main():
         cpu = cpu_baseline(sd, vd, p, args.cpu_seconds)
     rmse = None
     if rank == 0 and args.rmse_lanes > 0 and not p.adaptive:
+        print("[bench] RMSE window: %d lanes of every pass through the oracle" % args.rmse_lanes, file=sys.stderr,
+              flush=True)
         rmse = rmse_window(dev, sd, vd, p, plan, args.rmse_lanes, stream)
     elif rank == 0 and args.rmse_lanes > 0:
         # the adaptive fill compacts and re-traces over the WHOLE pass, so no lane window of the full-size
@@ -555,6 +557,7 @@ def cpu_baseline(sd, vd, p, target_seconds):
         n = 1 << 16
         while True:
             _, _, st = O.render(sd, vd, p, lane_begin=0, lane_end=n, threads=threads)
+            print("[bench] cpu baseline: %d lanes in %.1f s" % (n, st["seconds"]), file=sys.stderr, flush=True)
             if st["seconds"] >= 0.6 * target_seconds or n >= (1 << 27):
                 break
             n = int(min(1 << 27, n * max(2.0, 1.2 * target_seconds / max(st["seconds"], 1e-3))))
