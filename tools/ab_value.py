@@ -42,12 +42,8 @@ def child(steps=3, kernels=False):
     lanes = p.film_width * p.film_height * spp
     flags = int(os.environ.get("AB_FLAGS", "0"), 0)   # amvpt_render_opts.flags (e.g. 32: OPT_NO_BINNING)
 
-    chunk = int(os.environ.get("AB_CHUNK", "0"), 0)   # amvpt_render_opts.chunk_lanes (0: automatic)
-
     def frame(**kw):
-        if flags or kw or chunk:
-            if chunk:
-                kw["chunk_lanes"] = chunk
+        if flags or kw:
             dev.render_ex(vd, p, film.data_ptr(), flags=flags | kw.pop("flags", 0), **kw)
         else:
             dev.render(vd, p, film.data_ptr())

@@ -20,7 +20,7 @@ for st in "$@"; do
     write) $S 300 write_$c -- rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_write_$c -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 $P ;;
     sqA) $S 200 sqA_$c -- rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH --output-format csv -d gpurun_out/${T}_sqA_$c -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --rmse-lanes 0 $P ;;
     abflags) $S 600 abflags_$c -- env AB_CONFIG=$c python -u tools/ab_value.py --kernels --env AB_FLAGS=0 --env AB_FLAGS=32 --env AB_FLAGS=0 --env AB_FLAGS=32 ;;
-    abchunk) $S 600 abchunk_$c -- env AB_CONFIG=$c python -u tools/ab_value.py --kernels --env AB_CHUNK=0 --env AB_CHUNK=0x2000000 --env AB_CHUNK=0x1000000 --env AB_CHUNK=0x8000000 --env AB_CHUNK=0 --env AB_CHUNK=0x2000000 ;;
+    abchunk) $S 600 abchunk_$c -- env AB_CONFIG=$c python -u tools/ab_value.py --kernels --env AB_CHUNK=0 --env AB_CHUNK=33554432 --env AB_CHUNK=16777216 --env AB_CHUNK=0 --env AB_CHUNK=33554432 ;;
     ablib) $S 900 ablib_$c -- env AB_CONFIG=${c%%+*} python -u tools/ab_value.py --kernels $(echo ${c#*+} | tr '+' ' ') ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
