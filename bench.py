@@ -291,7 +291,7 @@ def main():
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "strong" if lane_sharded else "weak",
-            "chunk_streams": 1 if args.one_stream else "auto (2 for the per-depth wavefront suffix of BVH scenes)",
+            "chunk_streams": 1 if args.one_stream else "auto (up to 4 for the per-depth wavefront suffix of BVH scenes)",
             "rmse_vs_oracle": rmse,
             "vs_baseline": None,
             "dtype": "f32",

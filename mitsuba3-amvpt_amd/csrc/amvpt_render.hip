@@ -2872,7 +2872,8 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
 #define AMVPT_FUSED_TWO_STREAMS 0   /* 1: fused-suffix scenes alternate chunks over two streams too (A/B) */
 #endif
 #ifndef AMVPT_CHUNK_STREAMS
-#define AMVPT_CHUNK_STREAMS 2   /* chunk streams of a render (1: every chunk on the render stream, A/B) */
+#define AMVPT_CHUNK_STREAMS 4   /* chunk streams of a per-depth-suffix render (1: every chunk on the render stream; mesh
+                                 * 962-973 / 984-988 / 1001-1002 Msamples/s with 2 / 3 / 4, r05zi; A/B) */
 #endif
 #ifndef AMVPT_TILE_SLOTS
 /* 4 x 4 pixel tiles per row-splat block (see tile_slot_lane): config M 1472 -> 1521 Msamples/s (splat
@@ -3857,6 +3858,7 @@ struct RoctxScope {
  * buffers (hipStreamWaitEvent when it runs on another stream), and a buffer is only
  * freed for a larger one after the event completed.
  */
+constexpr int kMaxChunkStreams = 4;
 struct DevArena {
     std::mutex mu;
     void *base = nullptr, *adapt = nullptr;
@@ -3864,10 +3866,10 @@ struct DevArena {
     hipEvent_t done = nullptr;
     hipStream_t last = nullptr;
     bool pending = false;
-    /* the second chunk stream (AMVPT_CHUNK_STREAMS = 2): created once per device; fork / join
-     * order it after / before the render stream */
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    /* the other chunk streams (AMVPT_CHUNK_STREAMS > 1): created once per device; fork / join
+     * order them after / before the render stream */
+    hipStream_t side[kMaxChunkStreams - 1] = {};
+    hipEvent_t fork = nullptr, join[kMaxChunkStreams - 1] = {};
     void *fx = nullptr;   /* deterministic mode's fixed-point film */
     size_t fxbytes = 0;
     void *carry = nullptr;   /* multi-pass stock path: two per-lane PCG32 state planes (rng_in / rng_out) */
@@ -4308,18 +4310,22 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
      * AMVPT_OPT_WAVEFRONT_SUFFIX keeps the per-depth k_extend / k_bounce wavefronts) */
     const bool fuse_suffix = (fuse_nee || (AMVPT_FUSE_BVH && K.fuse_nee && !(opts.flags & AMVPT_OPT_SPLIT_NEE))) &&
                              K.fuse_suffix && !(opts.flags & AMVPT_OPT_WAVEFRONT_SUFFIX);
-    /* chunks of the per-depth wavefront suffix (BVH scenes) alternate between two buffer sets on two
-     * streams (the render stream and the arena's side stream): one chunk's short deep-bounce launches
-     * and tails leave CUs idle that the other chunk's kernels fill (mesh 550 -> 599 Msamples/s).  The
+    /* chunks of the per-depth wavefront suffix (BVH scenes) take turns over up to four buffer sets on as many
+     * streams (the render stream and the arena's side streams): one chunk's short deep-bounce launches and
+     * tails leave CUs idle that the other chunks' kernels fill (mesh 550 -> 599 Msamples/s with two, round 2;
+     * 967 -> 1001 with four, r05zi).  The
      * fused-suffix scenes gain 0.0-0.5 % (r03i) and keep one stream, so their per-kernel HIP-event
      * times are not overlapped (AMVPT_OPT_ONE_STREAM forces one stream everywhere) */
     /* ray binning (k_bin_sort) for the per-lane suffix walks of BVHs read from device memory */
     const bool lane_walk = (walk == WALK_LANE || walk == WALK_LANE_NS || walk == WALK_LANE_TRI) && !fuse_suffix && scene_lds_bytes(scene->dev, trav) == 0u;
     const bool bin_ext = lane_walk && (AMVPT_BIN & 1) && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const bool bin_nee = lane_walk && (AMVPT_BIN & 2) && !fuse_nee && !(opts.flags & AMVPT_OPT_NO_BINNING);
-    const int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
-                        !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? 2 : 1;
     const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
+    /* as many buffer sets as chunk streams, at most one per chunk of the pass and 192 GB of sets in all */
+    int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
+                  !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? std::min(AMVPT_CHUNK_STREAMS, kMaxChunkStreams) : 1;
+    n_sets = (int) std::min<uint64_t>((uint64_t) n_sets, (span + chunk - 1) / chunk);
+    while (n_sets > 2 && set_bytes * (size_t) n_sets > (192ull << 30)) --n_sets;
     const size_t need = views_bytes + stats_bytes + set_bytes * n_sets;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -4329,29 +4335,31 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* the previous render's buffers may still be in flight on another stream */
     if (A.pending && A.last != st) HIPCHK(hipStreamWaitEvent(st, A.done, 0));
     /* every return below records `done` on this stream (also the error paths) */
-    if (n_sets > 1 && !A.side) {
-        HIPCHK(hipStreamCreateWithFlags(&A.side, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&A.fork, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&A.join, hipEventDisableTiming));
-    }
+    for (int k = 0; k + 1 < n_sets; ++k)
+        if (!A.side[k]) {
+            HIPCHK(hipStreamCreateWithFlags(&A.side[k], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&A.join[k], hipEventDisableTiming));
+        }
+    if (n_sets > 1 && !A.fork) HIPCHK(hipEventCreateWithFlags(&A.fork, hipEventDisableTiming));
     /* every return below joins the side stream into this one and records `done` (also the error paths) */
     struct ArenaRelease {
-        DevArena &A; hipStream_t st; bool side = false;
+        DevArena &A; hipStream_t st; int n_side; bool side = false;
         void join() {
             if (!side) return;
             side = false;
-            if (hipEventRecord(A.join, A.side) == hipSuccess) (void) hipStreamWaitEvent(st, A.join, 0);
+            for (int k = 0; k < n_side; ++k)
+                if (hipEventRecord(A.join[k], A.side[k]) == hipSuccess) (void) hipStreamWaitEvent(st, A.join[k], 0);
         }
         ~ArenaRelease() {
             join();
             if (hipEventRecord(A.done, st) == hipSuccess) { A.pending = true; A.last = st; }
         }
-    } arena_release{A, st};
+    } arena_release{A, st, n_sets - 1};
     /* the side stream starts after `st`'s work so far (views upload, counters) */
     auto fork_side = [&]() -> amvpt_status {
         if (n_sets < 2 || arena_release.side) return AMVPT_OK;
         HIPCHK(hipEventRecord(A.fork, st));
-        HIPCHK(hipStreamWaitEvent(A.side, A.fork, 0));
+        for (int k = 0; k + 1 < n_sets; ++k) HIPCHK(hipStreamWaitEvent(A.side[k], A.fork, 0));
         arena_release.side = true;
         return AMVPT_OK;
     };
@@ -4417,11 +4425,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         uint16_t *ka, *kb;              /* ray binning: bin keys of queues A / B (null: off) */
         uint32_t *cntA, *cntB, *cntN;   /* [kQParts * kCntStride] each */
         hipStream_t st;
-    } sets[2];
+    } sets[kMaxChunkStreams];
     for (int si = 0; si < n_sets; ++si) {
         ChunkSet &cs = sets[si];
         Bufs &B = cs.B;
-        cs.st = si == 0 ? st : A.side;
+        cs.st = si == 0 ? st : A.side[si - 1];
         uint32_t *dcnt = (uint32_t *) carve(cnt_bytes);
         cs.cntA = dcnt; cs.cntB = dcnt + kQParts * kCntStride; cs.cntN = dcnt + 2 * kQParts * kCntStride;
         for (int k = 0; k < kQPlanes; ++k) cs.qa[k] = (float4 *) carve(16 * qlen);
@@ -4558,9 +4566,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         P.rng_out = rng_carry && pass + 1 < n_passes ? carry[(pass + 1) & 1u] : nullptr;
         for (uint64_t c0 = 0; c0 < span; c0 += chunk, ++chunk_index) {   /* virtual indices of the lane set */
             const uint32_t cn = (uint32_t) std::min<uint64_t>(chunk, span - c0);
-            /* odd chunks on the side stream, which starts once the first chunk's primary stage is queued
-             * (the two streams then run offset by about half a chunk) */
-            ChunkSet &cs = sets[chunk_index & (uint64_t) (n_sets - 1)];
+            /* chunk i on set i mod n_sets: the side streams start once the first chunk's primary stage is queued
+             * (the streams then run offset from each other) */
+            ChunkSet &cs = sets[chunk_index % (uint64_t) n_sets];
             Bufs &B = cs.B;
             hipStream_t st = cs.st;
             uint32_t *const cntA = cs.cntA, *const cntB = cs.cntB;
@@ -4592,7 +4600,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             HIPCHK(hipGetLastError());
             HIPCHK(T.err);
             T.mark(st);
-            if (n_sets > 1 && (chunk_index & 1) == 0) {   /* the side stream's start: after this primary stage */
+            if (n_sets > 1 && chunk_index % (uint64_t) n_sets == 0) {   /* the side streams' start: after this primary stage */
                 const amvpt_status fs_ = fork_side();
                 if (fs_ != AMVPT_OK) return fs_;
             }
