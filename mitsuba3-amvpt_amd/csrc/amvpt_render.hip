@@ -4321,10 +4321,11 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool bin_ext = lane_walk && (AMVPT_BIN & 1) && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const bool bin_nee = lane_walk && (AMVPT_BIN & 2) && !fuse_nee && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
-    /* as many buffer sets as chunk streams, at most one per chunk of the pass and 192 GB of sets in all */
+    /* as many buffer sets as chunk streams, at most one per chunk of the render (chunk i on set i mod n across
+     * the passes) and 192 GB of sets in all */
     int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
                   !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? std::min(AMVPT_CHUNK_STREAMS, kMaxChunkStreams) : 1;
-    n_sets = (int) std::min<uint64_t>((uint64_t) n_sets, (span + chunk - 1) / chunk);
+    n_sets = (int) std::min<uint64_t>((uint64_t) n_sets, (uint64_t) n_passes * ((span + chunk - 1) / chunk));
     while (n_sets > 2 && set_bytes * (size_t) n_sets > (192ull << 30)) --n_sets;
     const size_t need = views_bytes + stats_bytes + set_bytes * n_sets;
     int dev = 0;
