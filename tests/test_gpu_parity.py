@@ -494,9 +494,9 @@ def test_many_chunks_per_pass(gpu_ready, amvpt_mod, oracle, chunk):
 
 
 def test_two_chunk_streams(gpu_ready, amvpt_mod, oracle):
-    """BVH scenes (per-depth wavefront suffix) alternate chunks between two buffer sets on two streams:
-    with many small chunks on both streams the records stay bit-identical to the oracle, as they are
-    with every chunk on the render stream (AMVPT_OPT_ONE_STREAM)."""
+    """BVH scenes (per-depth wavefront suffix) take turns over up to four buffer sets on as many streams
+    (16 chunks per pass here, so all four run): with many small chunks on every stream the records stay
+    bit-identical to the oracle, as they are with every chunk on the render stream (AMVPT_OPT_ONE_STREAM)."""
     amvpt_mod.set_chunk_lanes(2048)
     try:
         s = amvpt_mod.load_file(MESH, res=16, spp=16, gx=4, gy=2, reuse=8)
