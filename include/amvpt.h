@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AMVPT_ABI_VERSION 9
+#define AMVPT_ABI_VERSION 10
 
 typedef enum amvpt_status {
     AMVPT_OK = 0,
@@ -214,6 +214,10 @@ typedef struct amvpt_counters {
     /* ABI 9 */
     uint64_t film_range_drops;  /* AMVPT_OPT_DETERMINISTIC: finite footprint-cell adds of |v| >= 2^31 the fixed-point
                                  * film cannot hold, dropped (ImageBlock::put would add them; 0 otherwise) */
+    /* ABI 10: the render's memory plan (amvpt_render_opts.budget_mib) */
+    uint64_t chunk_lanes;       /* lanes per chunk the render ran (the automatic or requested chunk, after the budget) */
+    uint64_t buffer_sets;       /* chunk buffer sets (= chunk streams) */
+    uint64_t arena_bytes;       /* device bytes the device's arena holds after the render (amvpt_release_device_memory) */
 } amvpt_counters;
 
 /* kernels of the pipeline, for amvpt_counters.kernel_ms */
@@ -288,8 +292,13 @@ amvpt_status amvpt_plan(const amvpt_params *params, uint32_t *spp, uint32_t *spp
 amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t width,
                            uint32_t height, uint32_t film_alpha, void *stream);
 
-/* Tuning knobs (0 keeps the default). chunk_lanes bounds the lane arena per launch; 0 restores the
- * automatic chunk (2^25 lanes, halved down to 2^23 while the chunk's arena would exceed 24 GB). */
+/* Tuning knobs (0 keeps the default). chunk_lanes bounds the lanes per chunk; 0 restores the automatic
+ * chunk: 2^26 lanes, halved while one buffer set would exceed 48 GB (about 700 B per lane for a mesh scene at
+ * G = 8, 46 GB per set; 26 GB at config M).  BVH scenes run up to four buffer sets on as many streams (192 GB
+ * at most).  Every render then fits its chunk and sets to a device-memory budget (amvpt_render_opts.budget_mib;
+ * automatic: the device's free memory plus what the arena holds, less max(2 GiB, 1/64 of the device)) by
+ * dropping buffer sets, then halving the chunk; results do not depend on either.  The arena is kept per device
+ * for the next render until amvpt_release_device_memory. */
 amvpt_status amvpt_set_chunk_lanes(uint64_t chunk_lanes);
 /* BVH walk: 0 auto (wave-uniform for <= 255 nodes, else per-lane; scenes of <= 48
  * primitives test every primitive in the suffix walks instead), 1 force the wave-uniform
@@ -396,7 +405,8 @@ typedef struct amvpt_render_opts {
     void *exchange_ctx;
     float *records;                   /* test hook (parity), NULL: off -- as amvpt_render_records: [v * G + slot][8] */
     uint32_t record_pass;             /*   of pass record_pass, v = the lane's index in the lane set (lane order) */
-    uint32_t reserved;
+    uint32_t budget_mib;              /* ABI 10: device memory (MiB) the render's buffers may hold; 0 = automatic (see
+                                       * amvpt_set_chunk_lanes).  A budget below the smallest chunk: AMVPT_ERR_OOM */
 } amvpt_render_opts;
 
 /*
@@ -417,6 +427,15 @@ amvpt_status amvpt_render_ex(amvpt_scene *scene, const amvpt_view_desc *views, c
 amvpt_status amvpt_film_accumulate(float *quilt, uint32_t quilt_width, uint32_t quilt_height, uint32_t channels,
                                    const float *window, uint32_t x0, uint32_t y0, uint32_t width, uint32_t height,
                                    const uint32_t *overflow_entries, uint64_t n_entries, void *stream);
+
+/*
+ * ABI 10: free the lane arena (chunk buffer sets, adaptive / deterministic / sampler-state buffers) renders keep
+ * on `device` between frames, once the last render that used it has finished.  Dr.Jit frees a render's
+ * wavefront buffers when the render returns; here the arena is kept for the next frame (a frame of config M
+ * reuses 26 GB) until this call.  The host scene's destructor calls it for every device it rendered on.  A later
+ * render allocates again.
+ */
+amvpt_status amvpt_release_device_memory(int device);
 
 #ifdef __cplusplus
 }

@@ -77,7 +77,8 @@ class Counters(ctypes.Structure):
                 ("total_ms", f64), ("splat_fallback", u64),
                 ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12),
                 ("record_bytes", u64), ("nonfinite_samples", u64), ("negative_samples", u64),
-                ("pushed_paths", u64), ("film_overflow", u64), ("film_range_drops", u64)]
+                ("pushed_paths", u64), ("film_overflow", u64), ("film_range_drops", u64),
+                ("chunk_lanes", u64), ("buffer_sets", u64), ("arena_bytes", u64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -106,10 +107,11 @@ RunExchangeFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, u32, ctypes.POIN
 
 
 class RenderOpts(ctypes.Structure):
-    """amvpt_render_opts: per-call chunk size, traversal, path-selection flags, run exchange, records."""
+    """amvpt_render_opts: per-call chunk size, traversal, path-selection flags, run exchange, records, and
+    (ABI 10) the device-memory budget in MiB (0: automatic)."""
     _fields_ = [("chunk_lanes", u64), ("traversal", u32), ("flags", u32), ("exchange", RunExchangeFn),
                 ("exchange_ctx", ctypes.c_void_p), ("records", ctypes.c_void_p), ("record_pass", u32),
-                ("reserved", u32)]
+                ("budget_mib", u32)]
 
 
 # amvpt_render_opts.flags (results are identical; kernel-path selection for tests / A/B)
@@ -158,7 +160,8 @@ def hip_lib():
         for fn in ("amvpt_device_count", "amvpt_set_device", "amvpt_scene_create", "amvpt_scene_destroy",
                    "amvpt_scene_stats", "amvpt_render", "amvpt_render_records", "amvpt_plan",
                    "amvpt_develop", "amvpt_set_chunk_lanes", "amvpt_set_traversal",
-                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build", "amvpt_render_ex", "amvpt_scene_desc_boxes"):
+                   "amvpt_set_adaptive_exchange", "amvpt_set_bvh_build", "amvpt_render_ex", "amvpt_scene_desc_boxes",
+                   "amvpt_release_device_memory"):
             if hasattr(L, fn):   # older variant builds (AMVPT_LIB_DIR A/B runs) may lack the newest knobs
                 getattr(L, fn).restype = ctypes.c_int
         L.amvpt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Params), u64, u64,
@@ -181,6 +184,8 @@ def hip_lib():
         if hasattr(L, "amvpt_set_adaptive_exchange"):
             L.amvpt_set_adaptive_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.amvpt_set_device.argtypes = [ctypes.c_int]
+        if hasattr(L, "amvpt_release_device_memory"):
+            L.amvpt_release_device_memory.argtypes = [ctypes.c_int]
         L.amvpt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         _hip = L
     return _hip
@@ -408,6 +413,22 @@ def set_adaptive_exchange(fn):
     _check(L.amvpt_set_adaptive_exchange(_exchange_cb if _exchange_cb else ExchangeFn(), None), L)
 
 
+def scene_box_count(scene, sensor=0):
+    """Box meshes amvpt_scene_create screens in the brute-force walks of `scene` (amvpt_scene_desc_boxes)."""
+    L = hip_lib()
+    sd, _, _ = scene.describe(sensor, 0, 0)
+    L.amvpt_scene_desc_boxes.argtypes = [ctypes.c_void_p, ctypes.POINTER(u32)]
+    n = u32()
+    _check(L.amvpt_scene_desc_boxes(ctypes.cast(sd, ctypes.c_void_p), ctypes.byref(n)), L)
+    return n.value
+
+
+def release_device_memory(device=0):
+    """Free the lane arena renders keep on `device` between frames (amvpt_release_device_memory, ABI 10)."""
+    L = hip_lib()
+    _check(L.amvpt_release_device_memory(int(device)), L)
+
+
 def device_count():
     n = ctypes.c_int(0)
     hip_lib().amvpt_device_count(ctypes.byref(n))
@@ -473,7 +494,7 @@ class DeviceScene:
 
     def render_ex(self, views_ptr, params, film_ptr, lanes=None, window=None, overflow_ptr=None,
                   overflow_capacity=0, stream=None, counters=None, chunk_lanes=None, traversal=None, flags=0,
-                  exchange=None, records_ptr=None, record_pass=0):
+                  exchange=None, records_ptr=None, record_pass=0, budget_mib=0):
         """amvpt_render_ex: `lanes` a LaneSet (None: the whole pass), `window` (x0, y0, width, height)
         of the quilt the film holds (None: the whole quilt), per-call options; `exchange` is
         `fn(run_lane_begin, run_count) -> (run_prefix, total)` (see amvpt.dist.run_exchange)."""
@@ -485,7 +506,8 @@ class DeviceScene:
         fw = FilmWindow(ctypes.c_void_p(film_ptr), x0, y0, w, h, ctypes.c_void_p(overflow_ptr or 0),
                         overflow_capacity)
         cb = wrap_run_exchange(exchange) if exchange is not None else RunExchangeFn()
-        o = RenderOpts(chunk_lanes, traversal, flags, cb, None, ctypes.c_void_p(records_ptr or 0), record_pass, 0)
+        o = RenderOpts(chunk_lanes, traversal, flags, cb, None, ctypes.c_void_p(records_ptr or 0), record_pass,
+                       int(budget_mib))
         _check(self._lib.amvpt_render_ex(self.h, views_ptr, ctypes.byref(params), ctypes.byref(lanes),
                                          ctypes.byref(fw), ctypes.c_void_p(stream), ctypes.byref(o),
                                          ctypes.byref(counters) if counters is not None else None), self._lib)

@@ -454,12 +454,36 @@ static constexpr float kInf32 = std::numeric_limits<float>::infinity();
  * Box meshes (dscene.h DBox): a mesh shape of 12 triangles whose vertices map, through the shape's
  * to_object (in double), to corners of [-1, 1]^3 within 1e-5, every triangle lying in one face plane, two
  * triangles per face covering its four corners -- the `cube` plugin's mesh (cube.cpp:105-160) under any
- * affine to_world.  Boxes whose box-space coordinates would magnify the walks' rounding (a very thin box, or
- * one far from the origin relative to its size: conditioning >= 100) are left to the plain scan.  prims[] is
- * in BVH order; box_prims / loose_prims hold copies with the BVH index in `type`'s upper bits.
+ * affine to_world.  Boxes whose box-space coordinates would magnify the walks' rounding are left to the plain
+ * scan: the screen maps a ray's ORIGIN into box space, and the suffix rays start anywhere on the scene's
+ * surfaces, so the bound is the box's conditioning (largest row norm of to_object) times (1 + the largest
+ * coordinate magnitude of the whole scene, desc_extent), not of the box's own vertices: a small
+ * cube on a ground plane 1000 units wide would have its box-space origins at ~1e4 and f32 rounding near kBoxEps.
+ * prims[] is in BVH order; box_prims / loose_prims hold copies with the BVH index in `type`'s upper bits.
  */
+/* the largest coordinate magnitude of any primitive of the scene (world space): mesh vertices, rectangle corners
+ * (to_world of (+-1, +-1, 0)), sphere centres +- radius */
+static double desc_extent(const amvpt_scene_desc *d) {
+    double e = 0.0;
+    for (uint32_t i = 0; i < d->shape_count; ++i) {
+        const amvpt_shape_desc &s = d->shapes[i];
+        if (s.type == AMVPT_SHAPE_MESH && s.positions) {
+            for (size_t k = 0; k < (size_t) 3 * s.vertex_count; ++k) e = std::max(e, (double) std::fabs(s.positions[k]));
+        } else if (s.type == AMVPT_SHAPE_RECTANGLE) {
+            for (int c = 0; c < 4; ++c) {
+                const double x = (c & 1) ? 1.0 : -1.0, y = (c & 2) ? 1.0 : -1.0;
+                for (int r = 0; r < 3; ++r)
+                    e = std::max(e, std::fabs(s.to_world[4 * r] * x + s.to_world[4 * r + 1] * y + s.to_world[4 * r + 3]));
+            }
+        } else if (s.type == AMVPT_SHAPE_SPHERE) {
+            for (int r = 0; r < 3; ++r) e = std::max(e, (double) std::fabs(s.center[r]) + (double) std::fabs(s.radius));
+        }
+    }
+    return e;
+}
 static void find_boxes(const amvpt_scene_desc *d, const std::vector<DPrim> &prims, std::vector<DBox> &boxes,
                        std::vector<DPrim> &box_prims, std::vector<DPrim> &loose) {
+    const double extent = desc_extent(d);
     std::vector<int> in_box(prims.size(), 0);
     for (uint32_t i = 0; i < d->shape_count; ++i) {
         const amvpt_shape_desc &s = d->shapes[i];
@@ -498,7 +522,7 @@ static void find_boxes(const amvpt_scene_desc *d, const std::vector<DPrim> &prim
             for (int v = 0; v < 3; ++v) corners[face] |= 1u << ((b[v][bx] > 0 ? 1 : 0) + (b[v][cx] > 0 ? 2 : 0));
         }
         for (int f = 0; ok && f < 6; ++f) ok = n_on[f] == 2 && corners[f] == 15u;
-        if (!ok || cond * (1.0 + wmax) >= 100.0) continue;
+        if (!ok || cond * (1.0 + std::max(wmax, extent)) >= 100.0) continue;
         DBox B{};
         for (int k = 0; k < 12; ++k) B.m[k] = (float) M[k];
         for (int k = 0; k < 12; ++k) {
@@ -998,6 +1022,11 @@ amvpt_status amvpt_develop(const float *film_device, float *out_device, uint32_t
                            uint32_t film_alpha, void *stream) {
     if (!device_ok()) { set_error("amvpt_develop: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
     return develop_impl(film_device, out_device, width, height, film_alpha, stream);
+}
+
+amvpt_status amvpt_release_device_memory(int device) {
+    if (!device_ok()) { set_error("amvpt_release_device_memory: no HIP device visible"); return AMVPT_ERR_NO_DEVICE; }
+    return release_impl(device);
 }
 
 } // extern "C"

@@ -4286,13 +4286,10 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         chunk_max = 1ull << 26;
         while (chunk_max > (1ull << 16) && chunk_max * per_lane > (48ull << 30)) chunk_max >>= 1;
     }
-    const uint64_t chunk = std::min<uint64_t>(chunk_max, span);
-    if (P.tile_w && chunk % (4ull * QW * 16ull) != 0) P.tile_w = 0;   /* chunks must hold whole tile bands */
-    P.vs_stride = (uint32_t) chunk;
+    uint64_t chunk = std::min<uint64_t>(chunk_max, span);
     const size_t views_bytes = ((hv.size() * sizeof(DView)) + 255) & ~(size_t) 255;
     /* one partition holds the pushes of every kQParts-th producer block (<= 256 lanes each) */
-    const uint32_t qcap = (uint32_t) (((chunk + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63);
-    const uint64_t qlen = (uint64_t) qcap * kQParts;
+    auto qcap_of = [](uint64_t c) { return (uint32_t) (((c + kQParts - 1) / kQParts + 512 + 63) & ~(uint64_t) 63); };
     const size_t stats_bytes = (size_t) kStats * kStatShards * 8, cnt_bytes = (size_t) 3 * kQParts * kCntStride * 4;
     const bool tab_b = AMVPT_BOUNCE_TAB && tables_staged(scene->dev, 0), tab_p = AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views);
     const bool uni = scene_uniform(scene->dev.n_nodes, trav);
@@ -4320,14 +4317,19 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const bool lane_walk = (walk == WALK_LANE || walk == WALK_LANE_NS || walk == WALK_LANE_TRI) && !fuse_suffix && scene_lds_bytes(scene->dev, trav) == 0u;
     const bool bin_ext = lane_walk && (AMVPT_BIN & 1) && !(opts.flags & AMVPT_OPT_NO_BINNING);
     const bool bin_nee = lane_walk && (AMVPT_BIN & 2) && !fuse_nee && !(opts.flags & AMVPT_OPT_NO_BINNING);
-    const size_t set_bytes = cnt_bytes + per_lane * std::max<uint64_t>(chunk, qlen) + 8192;
+    auto set_bytes_of = [&](uint64_t c) {
+        return cnt_bytes + per_lane * std::max<uint64_t>(c, (uint64_t) qcap_of(c) * kQParts) + 8192;
+    };
     /* as many buffer sets as chunk streams, at most one per chunk of the render (chunk i on set i mod n across
      * the passes) and 192 GB of sets in all */
-    int n_sets = (AMVPT_CHUNK_STREAMS > 1 && span > chunk && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
-                  !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? std::min(AMVPT_CHUNK_STREAMS, kMaxChunkStreams) : 1;
-    n_sets = (int) std::min<uint64_t>((uint64_t) n_sets, (uint64_t) n_passes * ((span + chunk - 1) / chunk));
-    while (n_sets > 2 && set_bytes * (size_t) n_sets > (192ull << 30)) --n_sets;
-    const size_t need = views_bytes + stats_bytes + set_bytes * n_sets;
+    auto sets_for = [&](uint64_t c) {
+        int n = (AMVPT_CHUNK_STREAMS > 1 && span > c && (!fuse_suffix || AMVPT_FUSED_TWO_STREAMS) &&
+                 !(opts.flags & AMVPT_OPT_ONE_STREAM)) ? std::min(AMVPT_CHUNK_STREAMS, kMaxChunkStreams) : 1;
+        n = (int) std::min<uint64_t>((uint64_t) n, (uint64_t) n_passes * ((span + c - 1) / c));
+        while (n > 2 && set_bytes_of(c) * (size_t) n > (192ull << 30)) --n;
+        return n;
+    };
+    int n_sets = sets_for(chunk);
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     DevArena &A = dev_arena(dev);
@@ -4335,14 +4337,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     if (!A.done) HIPCHK(hipEventCreateWithFlags(&A.done, hipEventDisableTiming));
     /* the previous render's buffers may still be in flight on another stream */
     if (A.pending && A.last != st) HIPCHK(hipStreamWaitEvent(st, A.done, 0));
-    /* every return below records `done` on this stream (also the error paths) */
-    for (int k = 0; k + 1 < n_sets; ++k)
-        if (!A.side[k]) {
-            HIPCHK(hipStreamCreateWithFlags(&A.side[k], hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&A.join[k], hipEventDisableTiming));
-        }
-    if (n_sets > 1 && !A.fork) HIPCHK(hipEventCreateWithFlags(&A.fork, hipEventDisableTiming));
-    /* every return below joins the side stream into this one and records `done` (also the error paths) */
+    /* every return below joins the side streams into this one and records `done` (also the error paths) */
     struct ArenaRelease {
         DevArena &A; hipStream_t st; int n_side; bool side = false;
         void join() {
@@ -4355,7 +4350,65 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
             join();
             if (hipEventRecord(A.done, st) == hipSuccess) { A.pending = true; A.last = st; }
         }
-    } arena_release{A, st, n_sets - 1};
+    } arena_release{A, st, 0};
+    /* Device-memory budget (ABI 10; the reference bounds a pass's memory with spp_pass_lim and its wavefront
+     * cap, mvpath.cpp:36-41,133-147): opts.budget_mib, else this device's free memory plus what the arena
+     * already holds, less max(2 GiB, 1/64 of the device).  Sizing drops chunk streams' buffer sets first, then
+     * halves the chunk (records and films do not depend on either); a failing allocation takes the same steps
+     * before the render reports AMVPT_ERR_OOM. */
+    const size_t held = A.bytes + A.abytes + A.fxbytes + A.cbytes;
+    size_t budget = 0;
+    if (opts.budget_mib) {
+        budget = (size_t) opts.budget_mib << 20;
+    } else {
+        size_t fr = 0, tot = 0;
+        HIPCHK(hipMemGetInfo(&fr, &tot));
+        const size_t headroom = std::max<size_t>(2ull << 30, tot / 64);
+        budget = fr + held > headroom ? fr + held - headroom : 0;
+    }
+    /* the span-sized buffers below (deterministic film, sampler states, adaptive fill) */
+    const size_t other_need = (deterministic ? (size_t) QW * QH * (Pp.film_alpha ? 5 : 4) * 8 : 0) +
+                              (rng_carry ? (size_t) 16 * span : 0) + (do_fill ? (size_t) 6 * span + (1u << 20) : 0);
+    const uint64_t min_chunk = std::min<uint64_t>(span, 1ull << 16);
+    auto need_of = [&](uint64_t c, int n) { return views_bytes + stats_bytes + set_bytes_of(c) * (size_t) n; };
+    auto shrink = [&]() {   /* one step down: a buffer set less, then half the chunk (256-lane multiples) */
+        if (n_sets > 1) { --n_sets; return true; }
+        if (chunk <= min_chunk) return false;
+        chunk = std::max<uint64_t>(min_chunk, ((chunk / 2) + 255) & ~(uint64_t) 255);
+        return true;
+    };
+    size_t need = 0;
+    for (;;) {
+        need = need_of(chunk, n_sets);
+        if (need + other_need > budget) {
+            if (shrink()) continue;
+            set_error("amvpt_render: the device-memory budget (" + std::to_string(budget >> 20) + " MiB) cannot hold "
+                      "the smallest lane chunk (" + std::to_string((need + other_need) >> 20) + " MiB)");
+            return AMVPT_ERR_OOM;
+        }
+        /* an arena held from an earlier, larger render is trimmed to this one's budget */
+        if (A.base && A.bytes >= need && held - A.bytes + need + other_need <= budget && A.bytes + other_need > budget) {
+            if (A.pending) HIPCHK(hipEventSynchronize(A.done));
+            (void) hipFree(A.base);
+            A.base = nullptr;
+            A.bytes = 0;
+        }
+        const amvpt_status as_ = arena_reserve(A, A.base, A.bytes, need, "lane arena");
+        if (as_ == AMVPT_OK) break;
+        if (as_ != AMVPT_ERR_OOM || !shrink()) return as_;
+        (void) hipGetLastError();
+    }
+    if (P.tile_w && chunk % (4ull * QW * 16ull) != 0) P.tile_w = 0;   /* chunks must hold whole tile bands */
+    P.vs_stride = (uint32_t) chunk;
+    const uint32_t qcap = qcap_of(chunk);
+    const uint64_t qlen = (uint64_t) qcap * kQParts;
+    for (int k = 0; k + 1 < n_sets; ++k)
+        if (!A.side[k]) {
+            HIPCHK(hipStreamCreateWithFlags(&A.side[k], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&A.join[k], hipEventDisableTiming));
+        }
+    if (n_sets > 1 && !A.fork) HIPCHK(hipEventCreateWithFlags(&A.fork, hipEventDisableTiming));
+    arena_release.n_side = n_sets - 1;
     /* the side stream starts after `st`'s work so far (views upload, counters) */
     auto fork_side = [&]() -> amvpt_status {
         if (n_sets < 2 || arena_release.side) return AMVPT_OK;
@@ -4364,7 +4417,6 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         arena_release.side = true;
         return AMVPT_OK;
     };
-    { const amvpt_status as_ = arena_reserve(A, A.base, A.bytes, need, "lane arena"); if (as_ != AMVPT_OK) return as_; }
     char *base = (char *) A.base;
     DView *dviews = (DView *) base;
     unsigned long long *dstats = (unsigned long long *) (base + views_bytes);
@@ -4766,6 +4818,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.pushed_paths = hs[8];
         c.film_overflow = overflow_added;   /* this render's cells (renders append to the list) */
         c.film_range_drops = hs[9];
+        c.chunk_lanes = chunk;
+        c.buffer_sets = (uint64_t) n_sets;
+        c.arena_bytes = A.bytes + A.abytes + A.fxbytes + A.cbytes;
         T.flush();
         HIPCHK(T.err);
         for (int k = 0; k < AMVPT_K_COUNT; ++k) { c.kernel_ms[k] = T.ms[k]; c.kernel_launches[k] = T.launches[k]; }
@@ -4809,6 +4864,32 @@ amvpt_status accumulate_impl(float *quilt, uint32_t qw, uint32_t qh, uint32_t C,
         hipLaunchKernelGGL(k_overflow_apply, dim3((uint32_t) ((n_ov + 255) / 256)), dim3(256), 0, st, quilt,
                            (uint64_t) qw * qh * C, (const uint4 *) ov, n_ov);
     HIPCHK(hipGetLastError());
+    return AMVPT_OK;
+}
+
+/* amvpt_release_device_memory: the device's lane arena and span buffers, after the last render that used them */
+amvpt_status release_impl(int device) {
+    DevArena *a = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_arenas_mu);
+        auto it = g_arenas.find(device);
+        if (it != g_arenas.end()) a = it->second.get();
+    }
+    if (!a) return AMVPT_OK;
+    std::lock_guard<std::mutex> g(a->mu);
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    HIPCHK(hipSetDevice(device));
+    hipError_t e = a->pending ? hipEventSynchronize(a->done) : hipSuccess;
+    a->pending = false;
+    void **bufs[4] = {&a->base, &a->adapt, &a->fx, &a->carry};
+    for (void **b : bufs) {
+        if (*b) (void) hipFree(*b);
+        *b = nullptr;
+    }
+    a->bytes = a->abytes = a->fxbytes = a->cbytes = 0;
+    (void) hipSetDevice(cur);
+    if (e != hipSuccess) return hip_fail("hipEventSynchronize (release)", (int) e);
     return AMVPT_OK;
 }
 

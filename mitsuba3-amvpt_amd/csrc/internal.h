@@ -15,8 +15,8 @@ struct amvpt_scene {
     std::vector<void *> allocations;
     uint32_t n_nodes = 0, n_prims = 0;
     uint32_t n_sph = 0;         /* spheres (<= 64: the wave-uniform walks defer their float64 tests) */
-    uint32_t n_outer = 0;
-    bool bvh_tri_only = false;  /* every BVH primitive is a triangle (the WALK_LANE_TRI suffix walks) */       /* rectangles kept out of the BVH (DScene::outer) */
+    uint32_t n_outer = 0;       /* rectangles kept out of the BVH (DScene::outer) */
+    bool bvh_tri_only = false;  /* every BVH primitive is a triangle (the WALK_LANE_TRI suffix walks) */
     uint32_t n_boxes = 0;       /* box meshes the brute-force walks screen (DScene::boxes) */
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   /* the BVH root box (ray binning's grid) */
     bool has_spheres = false;   /* the brute-force suffix walks take their sphere-free instances otherwise */
@@ -32,6 +32,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
                          const amvpt_render_opts &opts, amvpt_counters *counters, float *records,
                          uint32_t record_pass);
 amvpt_status develop_impl(const float *film, float *out, uint32_t w, uint32_t h, uint32_t alpha, void *stream);
+amvpt_status release_impl(int device);
 amvpt_status accumulate_impl(float *quilt, uint32_t qw, uint32_t qh, uint32_t C, const float *win, uint32_t x0,
                              uint32_t y0, uint32_t w, uint32_t h, const uint32_t *ov, uint64_t n_ov, void *stream);
 extern uint64_t g_chunk_lanes;

@@ -427,6 +427,7 @@ struct amvpt_host_scene {
             if (d.scene) amvpt_scene_destroy(d.scene);
             if (d.film) (void) hipFree(d.film);
             if (d.image) (void) hipFree(d.image);
+            (void) amvpt_release_device_memory(d.device);   /* the renders' lane arena on this device (ABI 10) */
             if (have) (void) hipSetDevice(cur);
         }
     }
@@ -503,6 +504,20 @@ static int add_bsdf(amvpt_host_scene &S, std::map<const Object *, int> &seen, co
     S.bsdfs.push_back(d);
     seen[&o] = idx;
     return idx;
+}
+
+/* a BSDF add_bsdf can build (its nested BSDFs too) */
+static bool bsdf_implemented(const Object &o) {
+    const std::string t = lower(o.props.plugin);
+    if (t == "diffuse" || t == "roughconductor") return true;
+    if (t != "twosided") return false;
+    for (auto &e : o.props.objects())
+        if (e.second->tag == "bsdf" && !bsdf_implemented(*e.second)) return false;
+    return true;
+}
+static void mark_tree_queried(const Object &o) {
+    o.props.mark_all_queried();
+    for (auto &e : o.props.objects()) mark_tree_queried(*e.second);
 }
 
 /* Cube geometry (src/shapes/cube.cpp:105-160) */
@@ -724,8 +739,13 @@ static void build(amvpt_host_scene &S) {
     {
         amvpt_host_scene scratch;
         std::map<const Object *, int> scratch_seen;
+        /* ... except a BSDF of a plugin this port does not implement (dielectric, plastic, ...): the scene never
+         * renders it, so it loads as the reference's does, its keys unchecked */
         for (auto &e : rp.objects())
-            if (e.second->tag == "bsdf" && !seen.count(e.second)) (void) add_bsdf(scratch, scratch_seen, *e.second);
+            if (e.second->tag == "bsdf" && !seen.count(e.second)) {
+                if (bsdf_implemented(*e.second)) (void) add_bsdf(scratch, scratch_seen, *e.second);
+                else mark_tree_queried(*e.second);
+            }
     }
     if (!have_integrator) {
         /* Scene default: path integrator */

@@ -7,7 +7,7 @@ import re
 
 import pytest
 
-from conftest import REPO
+from conftest import REPO, SCENES
 
 HEADERS = [os.path.join(REPO, "include", h) for h in ("amvpt.h", "amvpt_host.h")]
 
@@ -195,3 +195,15 @@ def test_box_meshes_are_recognised(amvpt_mod):
     pos[0] += 0.05   # vertex 0 leaves its corner
     shapes[cube].positions = ctypes.cast(pos, ctypes.POINTER(ctypes.c_float))
     assert _box_count(amvpt_mod, nd) == 1
+
+
+def test_box_screen_conditioning_counts_the_whole_scene(amvpt_mod):
+    """the screen maps suffix-ray ORIGINS into box space, and those lie anywhere on the scene, so a
+    box is screened only while its conditioning x (1 + the scene's largest coordinate) < 100: the Cornell cubes
+    (conditioning 3.3) stay boxes beside a floor 18 units wide, not beside one 200 units wide."""
+    xml = open(os.path.join(SCENES, "cbox_path.xml")).read()
+    rot = '<rotate x="1" angle="-90"/>\n            <translate y="-1"/>'
+    assert rot in xml
+    for scale, boxes in ((1, 2), (9, 2), (100, 0)):
+        s = amvpt_mod.load_string(xml.replace(rot, '<scale x="%d" y="%d"/>' % (scale, scale) + rot), res=8, spp=4)
+        assert amvpt_mod.scene_box_count(s) == boxes, scale

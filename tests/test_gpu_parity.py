@@ -143,7 +143,11 @@ def _records(amvpt_mod, oracle, sd, vd, p, flags):
     return rec.cpu().numpy()
 
 
-@pytest.mark.parametrize("case", ["grazing_top_face", "m_shape"])
+FAR_FLOOR = ('<rotate x="1" angle="-90"/>\n            <translate y="-1"/>',
+             '<scale x="9" y="9"/><rotate x="1" angle="-90"/>\n            <translate y="-1"/>')
+
+
+@pytest.mark.parametrize("case", ["grazing_top_face", "m_shape", "far_floor"])
 def test_box_screen_keeps_records(gpu_ready, amvpt_mod, oracle, case):
     """The brute-force walks screen the Cornell cubes (box meshes) per lane and test only the faces a ray can
     reach (dgeom.h box_walk).  Its records must equal the full scan's (AMVPT_OPT_NO_BOX_SCREEN) bit for bit on
@@ -154,6 +158,14 @@ def test_box_screen_keeps_records(gpu_ready, amvpt_mod, oracle, case):
         xml = open(CBOX_PATH).read().replace('origin="0, 0, 3.90" target="0, 0, 0"', 'origin="0, -0.4, 3.9" target="0, -0.4, 0"')
         assert 'origin="0, -0.4, 3.9"' in xml
         s = amvpt_mod.load_string(xml, res=128, spp=16)
+    elif case == "far_floor":
+        # a floor 18 units wide out of the room's open front, seen from a raised camera: suffix rays
+        # start up to ~9 units from the cubes (box-space origins ~30), still under the scene-extent conditioning
+        # bound (cond 3.3 x (1 + 9) < 100), so the cubes stay screened
+        xml = open(CBOX_PATH).read().replace(*FAR_FLOOR).replace('origin="0, 0, 3.90"', 'origin="0, 2.5, 6.5"')
+        assert 'scale x="9"' in xml and 'origin="0, 2.5, 6.5"' in xml
+        s = amvpt_mod.load_string(xml, res=128, spp=16)
+        assert amvpt_mod.scene_box_count(s) == 2
     else:
         s = amvpt_mod.load_file(CBOX, res=64, spp=16, gx=4, gy=2, reuse=8)
     sd, vd, p = s.describe(0, 0, 0)
@@ -443,6 +455,43 @@ def test_thinlens_views(gpu_ready, amvpt_mod, oracle, kw):
     and shared by every view's sample_surface; re-gathered by the adaptive fill."""
     s = amvpt_mod.load_file(CBOX, cam="thinlens", aperture="0.05", **kw)
     _check(amvpt_mod, oracle, s)
+
+
+CONE = os.path.join(SCENES, "cbox_cone.xml")
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(cam="thinlens", aperture="0.05"),
+                                dict(revx="true", offx=0.05, offy=0.1, offz=-0.2), dict(adaptive=3, revy="false")],
+                         ids=["perspective", "thinlens", "revx_cam_off", "adaptive"])
+def test_cone_layout_views(gpu_ready, amvpt_mod, oracle, kw):
+    """The grid's light-field cone layout (grid.cpp:108-112,182-205): 8 views on a line, each with its own
+    lens_shift in camera_to_sample (perspective.cpp:178-180, thinlens.cpp:195), so raygen, sensors_visible's
+    reprojection and every Jacobian / film pdf of sample_surface see an off-axis projection; G = 8, sa_mis.
+    The view table itself is pinned by tests/test_grid_layouts.py."""
+    s = amvpt_mod.load_file(CONE, res=24, spp=16, **kw)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert (p.n_views, p.reuse_count) == (8, 8)
+    assert len({round(vd[i].camera_to_sample[2], 6) for i in range(8)}) == 8   # eight distinct lens shifts
+    _check(amvpt_mod, oracle, s)
+
+
+@pytest.mark.parametrize("film_tol", [1e-5, 0], ids=["float_film", "deterministic_film"])
+def test_debug_mode_splats_the_adaptive_mask(gpu_ready, amvpt_mod, oracle, film_tol):
+    """debug = true (mvpath_multi.h:54-56): each lane puts only its primary sample, with the adaptive mask as
+    its value and weight 1, and the fill does not run; G = 8, adaptive 3.  Film against the oracle (the
+    deterministic film bit for bit); the developed film is the local fraction of adaptive lanes."""
+    line = '<integer name="adaptive" value="$adaptive"/>'
+    xml = open(CBOX).read()
+    assert line in xml
+    s = amvpt_mod.load_string(xml.replace(line, line + '<boolean name="debug" value="true"/>'),
+                              res=24, spp=32, gx=4, gy=2, reuse=8, adaptive=3)
+    sd, vd, p = s.describe(0, 0, 0)
+    assert p.debug == 1 and p.adaptive == 3
+    gfilm, _ = _check(amvpt_mod, oracle, s, film_tol=film_tol)
+    frac = gfilm[..., 0] / np.maximum(gfilm[..., -1], 1e-30)
+    assert np.allclose(gfilm[..., 0], gfilm[..., 1]) and np.allclose(gfilm[..., 0], gfilm[..., 2])
+    assert frac.min() >= 0.0 and frac.max() <= 1.0 + 1e-6
+    assert 0.0 < frac.mean() < 1.0   # some lanes are adaptive, not all
 
 
 MESH = os.path.join(SCENES, "cbox_mesh.xml")

@@ -314,6 +314,17 @@ def test_xml_unused_bsdf_and_wrapped_film_load(amvpt_mod):
     assert s.describe(0, 0, 0)[0].contents.bsdf_count == _strict(amvpt_mod).describe(0, 0, 0)[0].contents.bsdf_count
     with pytest.raises(RuntimeError, match=r'"\["alhpa"\]" in bsdf plugin of type "roughconductor"'):
         _strict(amvpt_mod, extra=unused.replace("alpha", "alhpa"))
+    # an unused BSDF of a plugin this port does not implement loads (the scene never renders it) --
+    # also nested in a twosided; a USED one stays a loud error
+    for extra in ('<bsdf type="dielectric" id="glass"><float name="int_ior" value="1.5"/></bsdf>',
+                  '<bsdf type="twosided" id="ts"><bsdf type="plastic"><rgb name="diffuse_reflectance" value="0.5"/>'
+                  '</bsdf></bsdf>'):
+        assert _strict(amvpt_mod, extra=extra).describe(0, 0, 0)[0].contents.bsdf_count == \
+            _strict(amvpt_mod).describe(0, 0, 0)[0].contents.bsdf_count
+    with pytest.raises(RuntimeError, match="not implemented"):
+        _strict(amvpt_mod, bprops="").__class__   # (the base scene's sphere BSDF is diffuse: fine)
+        amvpt_mod.load_string(_STRICT_BASE.replace('<bsdf type="diffuse">{bprops}</bsdf>', '<bsdf type="dielectric"/>')
+                              .format(itype="path", iprops="", sprops="", fprops="", shprops="", eprops="", extra=""))
     wrapped = _STRICT_BASE.replace(
         '<film type="hdrfilm"><integer name="width" value="8"/><integer name="height" value="8"/>{fprops}</film>',
         '<wrap type="wrap"><string name="wrap_class" value="film"/><string name="wrap_type" value="hdrfilm"/>'
