@@ -255,6 +255,7 @@ def main():
     traffic, traffic_src = pmc_traffic(kernel_name, prof_config, rev)
     valu = pmc_valu(kms, kl, G, prof_config, rev)
     hbm_frac = achieved / HBM_PEAK_GBS
+    frame = frame_pmc(prof_config, rev, ms_per_step)
     valu_dom = (valu or {}).get("kernels", {}).get(dom)
     # the measured limiter of the dominant kernel: VALU issue (committed SQ counts of this code revision
     # over this run's launch time) vs algorithmic HBM bytes over the same time
@@ -344,6 +345,13 @@ def main():
                          "HBM bytes are 96 B per pushed path, so its HBM fraction is small by design; bound = "
                          "the larger of its VALU-issue and HBM fractions -- pipeline_model is the metric's "
                          "roofline") if dom == "k_suffix" else None,
+                # the whole frame by the counters: every kernel's PMC bytes (FETCH x2 + WRITE,
+                # committed profiles of this source revision) x its launches per frame, over this run's ms_per_step;
+                # and the frame's VALU issue (committed SQ_INSTS_VALU per frame over ms_per_step x 1228.8 G/s)
+                "frame_traffic": frame["traffic"],
+                "frame_hbm_frac": frame["hbm_frac"],
+                "frame_valu_issue": frame["valu_issue"],
+                "frame_source": frame["source"],
                 "pipeline_model": {"B_sample": round(B_sample, 1), "vbar": round(vbar, 4), "hbar": round(hbar, 4),
                                    "achieved_GBs": round(pipeline_gbs, 2),
                                    "frac": round(pipeline_gbs / HBM_PEAK_GBS, 5)},
@@ -351,7 +359,9 @@ def main():
             "cpu_baseline": cpu,
             "counters": {k: c[k] for k in ("lanes", "vertices", "reuse_lanes", "visibility_rays", "view_splats",
                                              "nonfinite_samples", "negative_samples", "record_bytes",
-                                             "splat_fallback", "pushed_paths", "film_overflow", "film_range_drops")},
+                                             "splat_fallback", "pushed_paths", "film_overflow", "film_range_drops",
+                                             "primary_record_bytes", "splat_record_bytes", "chunk_lanes",
+                                             "buffer_sets", "arena_bytes")},
         }
         print(json.dumps(out))
     if world > 1:
@@ -436,6 +446,8 @@ def kernel_bytes(c, G, C, n_adapt=0):
     suffix = max(0, verts - lanes)        # suffix vertices (k_extend / k_bounce entries)
     pushed = c["pushed_paths"]            # paths that entered the suffix (device counter; = paths that terminate)
     rec = c["record_bytes"] or 16         # lane records (4 x 16 B) + lane_out + view records (amvpt_counters)
+    lane_rec = (80 if c["record_bytes"] else 16) * lanes   # the lane part: 4 lane-record planes + lane_out
+    vrec_w, vrec_r = c.get("primary_record_bytes", 0), c.get("splat_record_bytes", 0)
     adapt = c["adaptive_lanes"]
     state = 80                            # path state: 5 float4 planes (store_state)
     nee = 40                              # NEE record: origin + destination, light point + the visible result
@@ -445,13 +457,18 @@ def kernel_bytes(c, G, C, n_adapt=0):
         "k_prim_hit": (16 + (48 if c["kernel_launches"]["k_prim_req"] == 0 else 0)) * lanes,
         "k_prim_req": (16 + 48) * lanes,                            # hit in, visibility requests out
         "k_vis": (48 + G / 8.0) * lanes,                            # requests in (once), ballots out
-        "k_mv_primary": (16 + G / 8.0 + rec) * lanes + state * pushed,  # hit + ballots in, records + paths out
+        # hit + ballots in, lane records + view records + paths out (view records: the device's count of the bytes
+        # written, 4 per view in all-diffuse waves, 32 otherwise; ABI 10)
+        "k_mv_primary": (16 + G / 8.0) * lanes + lane_rec + (vrec_w if vrec_w else (rec - lane_rec / max(1, lanes)) * lanes)
+                        + state * pushed,
         "k_raygen": state * (lanes if G == 1 else adapt),           # path state out
         "k_extend": 48 * suffix,                                    # ray in, hit out
         # state + hit in; survivors' state out; terminated paths' result out; NEE records out (split)
         "k_bounce": (state + 16) * suffix + state * (suffix - pushed) + 16 * pushed + (0 if fused else nee * shadow),
         "k_shadow": (nee + 12) * shadow,                            # NEE record in, the visible result written
-        "k_splat": rec * lanes + 16 * adapt,                        # records in (film: PMC WRITE_SIZE)
+        # lane records in + the view records it reads (device count: only visited / splatting / indirect views,
+        # ABI 10); film: PMC WRITE_SIZE
+        "k_splat": lane_rec + (vrec_r if vrec_r else (rec - lane_rec / max(1, lanes)) * lanes) + 16 * adapt,
         # fused suffix (brute-force scenes): each path's state in once, its result out once; the
         # vertices in between stay in registers
         "k_suffix": (state + 16) * pushed,
@@ -502,6 +519,27 @@ def pmc_traffic(kernel_name, config, rev):
         if key in k.replace(" ", ""):
             return int(v["hbm_bytes_per_launch"]), src
     return None, src
+
+
+def frame_pmc(config, rev, ms_per_step):
+    """Whole-frame counters from the committed profiles of this config and source revision: HBM bytes per frame
+    (each kernel's FETCH x2 + WRITE per launch x its launches, over the frames the profiled run rendered), their
+    fraction of the HBM peak over ms_per_step, and the frame's VALU wave-instructions over ms_per_step x the issue
+    peak (a time-weighted VALU-issue fraction of the whole frame)."""
+    out = {"traffic": None, "hbm_frac": None, "valu_issue": None, "source": []}
+    t, src = _profile("r*_traffic*.json", config, rev)
+    out["source"].append(src)
+    if t is not None:
+        frames = t.get("frames_profiled", 2)
+        out["traffic"] = int(sum(v["hbm_bytes_per_launch"] * v["launches"] for v in t["kernels"].values()) / frames)
+        out["hbm_frac"] = round(out["traffic"] / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9), 5)
+    v, src = _profile("r*_valu*.json", config, rev)
+    out["source"].append(src)
+    if v is not None:
+        frames = v.get("frames_profiled", 2)
+        insts = sum(k["valu_insts_per_launch"] * k["launches"] for k in v["kernels"].values()) / frames
+        out["valu_issue"] = round(insts / (ms_per_step * 1e-3) / (v["peak_valu_ginst_s"] * 1e9), 5)
+    return out
 
 
 def pmc_valu(kms, kl, G, config, rev):

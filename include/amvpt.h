@@ -218,6 +218,8 @@ typedef struct amvpt_counters {
     uint64_t chunk_lanes;       /* lanes per chunk the render ran (the automatic or requested chunk, after the budget) */
     uint64_t buffer_sets;       /* chunk buffer sets (= chunk streams) */
     uint64_t arena_bytes;       /* device bytes the device's arena holds after the render (amvpt_release_device_memory) */
+    uint64_t primary_record_bytes; /* view-record bytes k_mv_primary wrote (4 per view all-diffuse, else 32) */
+    uint64_t splat_record_bytes;   /* view-record bytes the splat read (only the views it visits / that splat) */
 } amvpt_counters;
 
 /* kernels of the pipeline, for amvpt_counters.kernel_ms */

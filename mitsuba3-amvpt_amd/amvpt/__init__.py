@@ -78,7 +78,8 @@ class Counters(ctypes.Structure):
                 ("shadow_rays", u64), ("kernel_ms", f64 * 12), ("kernel_launches", u64 * 12),
                 ("record_bytes", u64), ("nonfinite_samples", u64), ("negative_samples", u64),
                 ("pushed_paths", u64), ("film_overflow", u64), ("film_range_drops", u64),
-                ("chunk_lanes", u64), ("buffer_sets", u64), ("arena_bytes", u64)]
+                ("chunk_lanes", u64), ("buffer_sets", u64), ("arena_bytes", u64),
+                ("primary_record_bytes", u64), ("splat_record_bytes", u64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

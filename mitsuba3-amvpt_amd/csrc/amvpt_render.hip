@@ -1515,7 +1515,9 @@ AD unsigned long long wave_sum(unsigned long long v) {
 }
 /* lane counters: stats[s * kStatShards + shard], one shard per block residue (summed on
  * the host), so the per-wave adds never pile onto one word */
-constexpr uint32_t kStatShards = 256, kStats = 10;   /* [8]: paths pushed into the suffix, [9]: deterministic-film range drops */
+/* [8]: paths pushed into the suffix, [9]: deterministic-film range drops, [10] / [11]: view-record bytes k_mv_primary
+ * writes / the splat reads (the byte model's record terms, ABI 10) */
+constexpr uint32_t kStatShards = 256, kStats = 12;
 static_assert(kStatShards == 256, "film_add shards its range-drop count by blockIdx % 256");
 AD void stat_add(unsigned long long *stats, uint32_t which, unsigned long long v) {
     v = wave_sum(v);
@@ -2547,6 +2549,13 @@ template <int NW> AD bool mget(const WMask<NW> &m, int k) {
     for (int q = 0; q < NW; ++q) x = (k >> 6) == q ? m.w[q] : x;
     return (x >> (k & 63)) & 1ull;
 }
+AD uint32_t mpopc(uint32_t m) { return (uint32_t) __popc(m & 0xffffu); }   /* G <= 16: bits 16+ are other fields */
+template <int NW> AD uint32_t mpopc(const WMask<NW> &m) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) c += (uint32_t) __popcll(m.w[q]);
+    return c;
+}
 AD void mset(uint32_t &m, int k, bool b) { m |= b ? 1u << k : 0u; }
 template <int NW> AD void mset(WMask<NW> &m, int k, bool b) {
 #pragma unroll
@@ -3321,6 +3330,7 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
         stat_add(B.stats, 2, st_vis);
         stat_add(B.stats, 0, (ok && P.max_depth != 0) ? 1ull : 0ull);
         stat_add(B.stats, 8, push ? 1ull : 0ull);
+        stat_add(B.stats, 10, ok ? (unsigned long long) ((kDiff ? 4 : 32) * Gn) : 0ull);
     }
 }
 #undef VSF
@@ -3459,6 +3469,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     const float *const vw = kDiff ? reinterpret_cast<const float *>(B.vrec) : vrec_compact(B, Gn, n);
     const float4 *const vR = B.vrec, *const vB = B.vrec + (size_t) Gn * n;
     uint32_t splats = 0, fallback = 0, nonfinite = 0, negative = 0;   /* per lane, <= G each */
+    uint32_t views_read = 0;   /* views the loop reads records of (wave-uniform) */
 #pragma unroll 1
     for (int k = 0; k < Gn; ++k) {
         /* a view no lane of the wave splats into: no reprojection, no put (the lane record carries the
@@ -3469,6 +3480,7 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
             const bool any = kRow ? wave_any(ok && mget(vmask, k)) : __syncthreads_or(ok && mget(vmask, k));
             if (!any) continue;
         }
+        ++views_read;
         const size_t o = (size_t) k * n + slot;
         float weight = 0.f;
         bool valid = false;
@@ -3543,6 +3555,11 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
     if (B.stats) {
         stat_add(B.stats, 3, splats); stat_add(B.stats, 4, fallback);
         stat_add(B.stats, 6, nonfinite); stat_add(B.stats, 7, negative);
+        /* view-record bytes read: a weight per visited view (all-diffuse records), else (result, weight) per
+         * valid view (every visited view when recording) and the BSDF value per indirect view */
+        const uint32_t vb = !ok ? 0u : kd ? 4u * views_read
+                                          : 16u * ((rec_ ? views_read : mpopc(vmask)) + (mis ? mpopc(imask) : 0u));
+        stat_add(B.stats, 11, vb);
     }
 }
 
@@ -4818,6 +4835,8 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         c.pushed_paths = hs[8];
         c.film_overflow = overflow_added;   /* this render's cells (renders append to the list) */
         c.film_range_drops = hs[9];
+        c.primary_record_bytes = hs[10];
+        c.splat_record_bytes = hs[11];
         c.chunk_lanes = chunk;
         c.buffer_sets = (uint64_t) n_sets;
         c.arena_bytes = A.bytes + A.abytes + A.fxbytes + A.cbytes;

@@ -47,7 +47,10 @@ def main():
         write = sw * 1024 / max(nw, 1)
         res[k] = {"launches": max(nf, nw), "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
                   "hbm_bytes_per_launch": fetch + write}
-    json.dump({"source": [fd, wd], "config": config, "source_revision": revision(),
+    # frames the profiled bench rendered: tools/gpu_run.sh runs `bench.py --steps 1 --warmup 0` (the timed frame and
+    # the instrumented frame), so the per-frame traffic is the launches' sum / 2 (bench.py frame_pmc)
+    frames = int(sys.argv[5]) if len(sys.argv) > 5 else 2
+    json.dump({"source": [fd, wd], "config": config, "source_revision": revision(), "frames_profiled": frames,
                "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 wide-read), WRITE_SIZE KiB x1024",
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in res.items():

@@ -28,7 +28,9 @@ def main():
             continue
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         ids[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
-    res = {"source": d, "config": config, "source_revision": revision(), "peak_valu_ginst_s": 1228.8, "kernels": {}}
+    frames = int(sys.argv[4]) if len(sys.argv) > 4 else 2   # bench.py --steps 1 --warmup 0: timed + instrumented frame
+    res = {"source": d, "config": config, "source_revision": revision(), "peak_valu_ginst_s": 1228.8,
+           "frames_profiled": frames, "kernels": {}}
     for k, c in acc.items():
         n = max(1, len(ids[k]))
         res["kernels"][k] = {"launches": n, "waves_per_launch": c["SQ_WAVES"] / n,
