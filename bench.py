@@ -590,8 +590,11 @@ def cpu_baseline(sd, vd, p, target_seconds):
     thread per usable host core."""
     from oracle import oracle as O
     threads, machine = host_cores()
+    n_prims = sum(sd[0].shapes[i].face_count if sd[0].shapes[i].type == 1 else 1 for i in range(sd[0].shape_count))
+    bvh = n_prims > 64   # BVH scenes: the oracle's own BVH (oracle_set_bvh; same hits), not a brute-force scan
     try:
         O.build()
+        O.set_bvh(bvh)
         n = 1 << 16
         while True:
             _, _, st = O.render(sd, vd, p, lane_begin=0, lane_end=n, threads=threads)
@@ -604,9 +607,13 @@ def cpu_baseline(sd, vd, p, target_seconds):
                 "host_cpus": machine, "cores_note": "threads = the CPUs this process may use (affinity set, "
                 "cgroup CPU quota); host_cpus = os.cpu_count() of the machine", "kind": "port",
                 "sample": "lanes [0, %d) of pass 0 of the same workload (%.1f s); CPU restatement of mvpath "
-                          "(oracle/, brute-force intersection), not Dr.Jit llvm_rgb" % (n, st["seconds"])}
+                          "(oracle/, %s), not Dr.Jit llvm_rgb" % (
+                              n, st["seconds"], "its median-split BVH over %d primitives (oracle_set_bvh)" % n_prims
+                              if bvh else "brute-force intersection over %d primitives" % n_prims)}
     except Exception as e:  # the baseline is reported, never the product path
         return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "port", "sample": "failed: %s" % e}
+    finally:
+        O.set_bvh(False)
 
 
 if __name__ == "__main__":

@@ -392,6 +392,8 @@ enum {
                                        * (no k_bin_sort); results are identical */
     AMVPT_OPT_NO_BOX_SCREEN = 64u,    /* ABI 9: the brute-force walks of small scenes test every triangle of a box
                                        * mesh (no per-lane face screening); results are identical */
+    AMVPT_OPT_THREADED_BVH = 128u,    /* ABI 10: the per-lane suffix walks of large BVHs take the threaded (skip-link)
+                                       * tree instead of the two-box one; results are identical */
     AMVPT_OPT_DETERMINISTIC = 16u     /* bitwise-reproducible film: splats summed as 32.32 fixed point with
                                        * integer atomics (order-independent), added to the film once at the
                                        * end; each footprint-cell add is rounded to a multiple of 2^-32 and
@@ -438,6 +440,13 @@ amvpt_status amvpt_film_accumulate(float *quilt, uint32_t quilt_width, uint32_t 
  * render allocates again.
  */
 amvpt_status amvpt_release_device_memory(int device);
+
+/*
+ * ABI 10: the two-box BVH of a scene (dscene.h DNode2) its per-lane suffix walks take: node count (0: the scene
+ * keeps the threaded walks -- a BVH small enough for the wave-uniform or LDS-staged walks, or one deeper than the
+ * walks' 16-entry stack) and the tree's depth in inner nodes (also when not built).
+ */
+amvpt_status amvpt_scene_bvh2(const amvpt_scene *scene, uint32_t *n_nodes2, uint32_t *depth);
 
 #ifdef __cplusplus
 }

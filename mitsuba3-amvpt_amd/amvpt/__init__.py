@@ -119,6 +119,7 @@ class RenderOpts(ctypes.Structure):
 OPT_GENERIC_KERNELS, OPT_WAVEFRONT_SUFFIX, OPT_SPLIT_NEE, OPT_ONE_STREAM, OPT_DETERMINISTIC = 1, 2, 4, 8, 16
 OPT_NO_BINNING = 32
 OPT_NO_BOX_SCREEN = 64
+OPT_THREADED_BVH = 128
 
 
 def wrap_run_exchange(fn):
@@ -481,6 +482,13 @@ class DeviceScene:
         n, p = u32(), u32()
         _check(self._lib.amvpt_scene_stats(self.h, n, p), self._lib)
         return n.value, p.value
+
+    def bvh2(self):
+        """(two-box BVH nodes, tree depth in inner nodes) -- amvpt_scene_bvh2 (0 nodes: threaded walks)"""
+        n, d = u32(), u32()
+        self._lib.amvpt_scene_bvh2.argtypes = [ctypes.c_void_p, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+        _check(self._lib.amvpt_scene_bvh2(self.h, n, d), self._lib)
+        return n.value, d.value
 
     def render(self, views_ptr, params, film_ptr, lane_begin=0, lane_end=2 ** 64 - 1, stream=None,
                counters=None):

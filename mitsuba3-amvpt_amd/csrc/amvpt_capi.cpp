@@ -90,6 +90,11 @@ static float g_bvh_trav_cost = 0.f;
 #endif
 /* direction-octant node orderings for the per-lane closest-hit walks of large BVHs (A/B builds:
  * EXTRA=-DAMVPT_OCT_BVH=0 keeps one copy); a build-time choice, never a process-global knob */
+/* the two-box BVH (dscene.h DNode2) for the per-lane suffix walks of large BVHs (A/B builds: EXTRA=-DAMVPT_BVH2=0
+ * keeps the threaded walks) */
+#ifndef AMVPT_BVH2
+#define AMVPT_BVH2 1
+#endif
 #ifndef AMVPT_OCT_BVH
 #define AMVPT_OCT_BVH 1
 #endif
@@ -196,6 +201,26 @@ struct Builder {
             flatten(bn.left_or_first + (near ^ 1u), out, oct, base, pos);
         }
         out[at].skip_count = (((uint32_t) out.size() - base) & kNodeSkipMask) | (bn.count << kNodeCountShift);
+    }
+    /* the two-box BVH (dscene.h DNode2) of the subtree under inner node ni, depth-first (a node, then its first
+     * child's subtree, then its second's); returns ni's index in out; depth: inner nodes on the path to ni */
+    uint32_t flatten2(uint32_t ni, std::vector<DNode2> &out, uint32_t depth, uint32_t &max_depth) const {
+        const uint32_t at = (uint32_t) out.size();
+        out.push_back(DNode2{});
+        max_depth = std::max(max_depth, depth);
+        uint32_t refs[2];
+        for (int c = 0; c < 2; ++c) {
+            const BNode &ch = nodes[nodes[ni].left_or_first + c];
+            refs[c] = ch.count ? (kRef2Leaf | (ch.count << kRef2CountShift) | ch.left_or_first)
+                               : flatten2(nodes[ni].left_or_first + c, out, depth + 1, max_depth);
+            for (int k = 0; k < 3; ++k) {
+                out[at].b[6 * c + k] = ch.box.lo[k];
+                out[at].b[6 * c + 3 + k] = ch.box.hi[k];
+            }
+        }
+        out[at].ref[0] = refs[0];
+        out[at].ref[1] = refs[1];
+        return at;
     }
     /* the treelet of one ordering: the nodes of depth < depth_cut in the same depth-first order, skip links
      * local to the treelet; an inner node at depth depth_cut - 1 is a portal to its subtree in the global
@@ -689,6 +714,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
         else outer_idx.clear();
     }
     std::vector<DNode> nodes, tnodes, onodes;
+    std::vector<DNode2> nodes2;   /* the two-box BVH (empty: none) */
+    uint32_t bvh2_depth = 0;
     std::vector<DPrim> prims;
     uint32_t oct_stride = 0;   /* nodes per octant copy (0: one copy) */
     uint32_t t_stride = 0;     /* nodes of the first ordering's treelet (0: none) */
@@ -737,6 +764,27 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
                 b.flatten_top(0, onodes, o, 0, g_oct_treelet_depth, gpos[o], o * n0, base);
                 if (o == 0) o_stride = (uint32_t) onodes.size();
             }
+        }
+        /* the two-box BVH of the per-lane suffix walks (BVHs read from device memory, leaves addressable in a
+         * reference, at most kStack2 inner nodes deep) */
+        if (AMVPT_BVH2 && n0 > kUniformNodeLimit && lds_b > kLdsSceneBytes && bprims.size() <= kRef2FirstMask) {
+            uint32_t depth = 0;
+            if (b.nodes[0].count) {
+                /* a root leaf: one node with the leaf and an empty second child */
+                DNode2 r{};
+                for (int k = 0; k < 3; ++k) {
+                    r.b[k] = b.nodes[0].box.lo[k]; r.b[3 + k] = b.nodes[0].box.hi[k];
+                    r.b[6 + k] = 1.f; r.b[9 + k] = -1.f;
+                }
+                r.ref[0] = kRef2Leaf | (b.nodes[0].count << kRef2CountShift) | b.nodes[0].left_or_first;
+                r.ref[1] = r.ref[0];
+                nodes2.push_back(r);
+                depth = 1;
+            } else {
+                b.flatten2(0, nodes2, 1, depth);
+            }
+            bvh2_depth = depth;
+            if (depth > kStack2) nodes2.clear();
         }
         prims.resize(bprims.size());
         for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
@@ -828,8 +876,10 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (box_prims.empty()) box_prims.resize(1);
     if (loose_prims.empty()) loose_prims.resize(1);
     void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes, *p_sph;
-    void *p_boxes, *p_box_prims, *p_loose, *p_outer;
+    void *p_boxes, *p_box_prims, *p_loose, *p_outer, *p_nodes2;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
+    const uint32_t n_nodes2 = (uint32_t) nodes2.size();
+    if (nodes2.empty()) nodes2.resize(1);
     if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
 #define UP(vec, ptr)                                                                      \
@@ -840,6 +890,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
     UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
     UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose) UP(outer, p_outer)
+    UP(nodes2, p_nodes2)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -874,6 +925,10 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     sc->n_boxes = n_boxes;
     D.outer = (const DPrim *) p_outer;
     D.n_outer = n_outer;
+    D.nodes2 = (const DNode2 *) p_nodes2;
+    D.n_nodes2 = n_nodes2;
+    sc->n_nodes2 = n_nodes2;
+    sc->bvh2_depth = bvh2_depth;
     sc->n_outer = n_outer;
     for (int a = 0; a < 3; ++a) {
         sc->root_lo[a] = bprims.empty() ? nodes[0].lo[a] : scene_lo[a];
@@ -938,6 +993,13 @@ amvpt_status amvpt_scene_destroy(amvpt_scene *scene) {
     if (!scene) return AMVPT_OK;
     for (void *p : scene->allocations) (void) hipFree(p);
     delete scene;
+    return AMVPT_OK;
+}
+
+amvpt_status amvpt_scene_bvh2(const amvpt_scene *scene, uint32_t *n_nodes2, uint32_t *depth) {
+    if (!scene || !n_nodes2 || !depth) { set_error("amvpt_scene_bvh2: null argument"); return AMVPT_ERR_INVALID; }
+    *n_nodes2 = scene->n_nodes2;
+    *depth = scene->bvh2_depth;
     return AMVPT_OK;
 }
 

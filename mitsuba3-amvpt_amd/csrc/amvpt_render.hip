@@ -79,17 +79,29 @@ template <int kWalk> constexpr int walk_sph() { return kWalk == WALK_LANE_TRI ? 
 #ifndef AMVPT_LANE_NS
 #define AMVPT_LANE_NS 1   /* sphere-free scenes take the WALK_LANE_NS suffix walks (0: WALK_LANE, A/B) */
 #endif
+/* the per-lane walks take the two-box BVH when the kernel gave the thread a stack (sc.stk: k_extend / k_shadow with
+ * KParams::bvh2), else the threaded one */
 template <int kWalk> AD Hit walk_closest(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_closest<kWalk == WALK_BRUTE>(sc, r);
+    if (kWalk != WALK_UNI && sc.stk) {
+        Hit best{kInf, 0.f, 0.f, -1};
+        uint32_t best_orig = 0xffffffffu;
+        outer_closest(sc, r, best, best_orig);
+        return trace_closest2<walk_sph<kWalk>()>(sc, r, best, best_orig);
+    }
     return trace_closest<kWalk == WALK_UNI, AMVPT_WALK_WW, walk_sph<kWalk>()>(sc, r);
 }
 template <int kWalk> AD bool walk_any(const SceneRef &sc, const Ray &r) {
     if (kWalk == WALK_BRUTE || kWalk == WALK_BRUTE_NS) return brute_any<kWalk == WALK_BRUTE>(sc, r);
+    if (kWalk != WALK_UNI && sc.stk) return trace_any2<walk_sph<kWalk>()>(sc, r, outer_any(sc, r, false));
     return trace_any<kWalk == WALK_UNI, AMVPT_WALK_WW, walk_sph<kWalk>()>(sc, r);
 }
 
 struct KParams {
     uint32_t W, H, C;
+    /* the per-lane suffix walks on the two-box BVH (DScene::nodes2): their LDS stack's byte offset in the dynamic
+     * LDS of k_extend / k_shadow (0 / 0 with bvh2 = 0: the threaded walks) */
+    uint32_t bvh2, stk_off_ext, stk_off_any;
     uint32_t spp_pp, log_spp, pow2;
     uint32_t max_depth, rr_depth;
     uint32_t sa_mis, fast_mis, debug, n_adapt;
@@ -274,6 +286,8 @@ AD SceneRef stage_scene(DScene &S, char *lds, uint32_t mode, const DView **V = n
     sc.onodes = nullptr;
     sc.o_n = 0;
     sc.lds_bvh = false;
+    sc.nodes2 = S.n_nodes2 ? S.nodes2 : nullptr;
+    sc.stk = nullptr;   /* the two-box walks' stack: set by the kernels that run them (k_extend / k_shadow) */
     sc.n_nodes = S.n_nodes;
     sc.gnodes = S.nodes;
     sc.gprims = S.prims;
@@ -1988,6 +2002,7 @@ k_extend(KParams P, const DScene *Sp, Bufs B) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false, true, false, (AMVPT_TREELETS & 2) != 0>(S, lds, P.trav_mode, nullptr, 0, P.box_screen != 0);
+    if (P.bvh2) sc.stk = reinterpret_cast<uint32_t *>(lds + P.stk_off_ext) + threadIdx.x;
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_in[part * kCntStride], pbase = part * B.qcap;
     /* the counters k_bounce fills are zeroed here (the previous k_bounce / k_shadow are done) */
@@ -2037,6 +2052,7 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
     extern __shared__ __attribute__((aligned(16))) char lds[];
     DScene S = *Sp;
     SceneRef sc = stage_scene<false, true, (AMVPT_TREELETS & 1) != 0>(S, lds, P.trav_mode, nullptr, 0, P.box_screen != 0);
+    if (P.bvh2) sc.stk = reinterpret_cast<uint32_t *>(lds + P.stk_off_any) + threadIdx.x;
     const uint32_t part = blockIdx.x % kQParts, pstride = gridDim.x / kQParts * blockDim.x;
     const uint32_t count = B.cnt_nee[part * kCntStride], pbase = part * B.qcap;
     /* the visible-light write of a record (the path's result becomes fma(throughput, contribution, result),
@@ -4538,9 +4554,17 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     /* k_suffix_fused: the box triangles staged for box_walk (AMVPT_BOX_LDS) */
     const size_t box_lds = (AMVPT_BOX_LDS && P.box_screen) ? (size_t) scene->n_boxes * 12u * sizeof(DPrim) : 0u;
     const size_t lds_ext = scene_lds_bytes(scene->dev, trav);                                       /* BVH walks */
-    const size_t lds_any = lds_ext + ((AMVPT_TREELETS & 1) ? tree_lds_bytes(scene->dev, trav) : 0u);     /* k_shadow: + any-hit treelet */
+    const size_t lds_any0 = lds_ext + ((AMVPT_TREELETS & 1) ? tree_lds_bytes(scene->dev, trav) : 0u);    /* k_shadow: + any-hit treelet */
     const size_t lds_vis = lds_ext + ((AMVPT_TREELETS & 4) ? tree_lds_bytes(scene->dev, trav) : 0u);     /* k_vis */
-    const size_t lds_close = lds_ext + ((AMVPT_TREELETS & 2) ? oct_tree_lds_bytes(scene->dev, trav) : 0u); /* k_extend: + octant treelets */
+    const size_t lds_close0 = lds_ext + ((AMVPT_TREELETS & 2) ? oct_tree_lds_bytes(scene->dev, trav) : 0u); /* k_extend: + octant treelets */
+    /* the two-box BVH walks (DScene::nodes2) for the per-lane suffix walks of BVHs read from device memory: a stack
+     * of kStack2 u32 entries per thread after the kernels' other LDS (AMVPT_OPT_THREADED_BVH keeps the threaded walks) */
+    P.bvh2 = (scene->n_nodes2 && lane_walk && !(AMVPT_TREELETS & 3) && !(opts.flags & AMVPT_OPT_THREADED_BVH)) ? 1u : 0u;
+    const size_t stk_bytes = P.bvh2 ? (size_t) kStack2 * kStk2Stride * 4u : 0u;
+    P.stk_off_ext = (uint32_t) ((lds_close0 + 15u) & ~(size_t) 15u);
+    P.stk_off_any = (uint32_t) ((lds_any0 + 15u) & ~(size_t) 15u);
+    const size_t lds_close = P.bvh2 ? P.stk_off_ext + stk_bytes : lds_close0;
+    const size_t lds_any = P.bvh2 ? P.stk_off_any + stk_bytes : lds_any0;
     const size_t lds_prim = tab_p ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;        /* primary shading */
     KTimer T;
     T.init(counters != nullptr);

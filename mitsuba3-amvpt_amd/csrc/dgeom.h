@@ -49,7 +49,12 @@ struct SceneRef {
     /* BVH scenes: rectangles kept out of the BVH (DScene::outer), tested by every walk before its BVH */
     const DPrim *outer;
     uint32_t n_outer;
+    /* the two-box BVH (DScene::nodes2) and this thread's LDS stack for its walks (trace_closest2 / trace_any2):
+     * entry k at stk[k * kStk2Stride]; null: none */
+    const DNode2 *nodes2;
+    uint32_t *stk;
 };
+constexpr uint32_t kStk2Stride = 256;   /* the suffix walks' block size: entry k of every thread's stack in one row */
 
 
 struct Hit { float t, u, v; int32_t prim; };
@@ -885,6 +890,120 @@ template <bool kUni, int kWW = 0, int kSph = 1> AD bool trace_any(const SceneRef
         return false;
     };
     return sc.lds_bvh ? walk(std::true_type{}) : walk(std::false_type{});
+}
+
+/*
+ * Walks of the two-box BVH (dscene.h DNode2; round 6), per lane, for the suffix rays of large
+ * BVHs.  A node holds both children's boxes, so the walk loads a node only when it enters it -- one dependent load
+ * per inner node entered, where the threaded walk loads every node it TESTS (both children of each node entered)
+ * -- and orders the children by the ray's own entry distances, nearer first, the farther one on a per-lane stack of
+ * kStack2 entries in LDS (entry k of thread t at stk[k * kStk2Stride + t]: the lanes of a wave hit distinct banks
+ * whatever their stack depths).  The host builds the tree only when it is at most kStack2 inner nodes deep, so
+ * the stack never overflows (a walk pushes at most one entry per inner node on its path).  Leaves are references
+ * in their parent; a leaf reached is held and tested in the speculative while-while rounds of the threaded walks
+ * (the wave tests its lanes' leaves together; a lane holding one keeps stepping until it meets a second).  The
+ * boxes are the threaded tree's padded ones, tested with box_hit's operations; the primitives, their tests and
+ * the (t, scene-order index) rule are the same, so the hits and verdicts are the same bits.
+ */
+AD bool box2_hit(const float *b, const BoxRay &br, float tmax, float &tmin_out) {
+    const float tx0 = fmaf(b[0], br.inv.x, -br.oinv.x), tx1 = fmaf(b[3], br.inv.x, -br.oinv.x);
+    const float ty0 = fmaf(b[1], br.inv.y, -br.oinv.y), ty1 = fmaf(b[4], br.inv.y, -br.oinv.y);
+    const float tz0 = fmaf(b[2], br.inv.z, -br.oinv.z), tz1 = fmaf(b[5], br.inv.z, -br.oinv.z);
+    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+    const float tm = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tmin_out = tmin;
+    return tmin <= tm;
+}
+AD uint32_t stk_load(const uint32_t *stk, uint32_t k) {
+    typedef __attribute__((address_space(3))) const uint32_t lu32;
+    return ((lu32 *) (uint32_t) (uintptr_t) stk)[k * kStk2Stride];
+}
+AD void stk_store(uint32_t *stk, uint32_t k, uint32_t v) {
+    typedef __attribute__((address_space(3))) uint32_t lu32;
+    ((lu32 *) (uint32_t) (uintptr_t) stk)[k * kStk2Stride] = v;
+}
+constexpr uint32_t kRef2End = 0x7fffffffu;   /* no node (an inner index never reaches it) */
+/* one step of a two-box walk at inner node `cur`: enter the nearer hit child, stack the farther one */
+AD uint32_t node2_step(const SceneRef &sc, uint32_t cur, const BoxRay &br, float tmax, uint32_t &sp) {
+    const DNode2 n = load_global(sc.nodes2, cur);
+    float t0, t1;
+    const bool h0 = box2_hit(n.b, br, tmax, t0), h1 = box2_hit(n.b + 6, br, tmax, t1);
+    const bool sw = h1 && (!h0 || t1 < t0);
+    const uint32_t a = sw ? n.ref[1] : n.ref[0], b = sw ? n.ref[0] : n.ref[1];
+    if (h0 && h1) stk_store(sc.stk, sp++, b);
+    if (h0 || h1) return a;
+    return sp ? stk_load(sc.stk, --sp) : kRef2End;
+}
+template <int kSph> AD Hit trace_closest2(const SceneRef &sc, const Ray &ray, Hit best, uint32_t best_orig) {
+    const BoxRay br = box_ray(ray);
+    float tmax_box = fminf(ray.maxt, best.t);
+    uint32_t cur = 0, sp = 0;
+    for (;;) {
+        uint32_t lf = 0, lc = 0;
+        bool stop = false;
+        for (;;) {
+            if (!wave_any(lc == 0u && cur != kRef2End)) break;
+            if (cur != kRef2End && !stop) {
+                if (cur & kRef2Leaf) {
+                    /* a leaf: held for this round's tests, or (a second one) kept for the next round */
+                    stop = lc != 0u;
+                    if (!stop) {
+                        lf = cur & kRef2FirstMask;
+                        lc = (cur >> kRef2CountShift) & 15u;
+                        cur = sp ? stk_load(sc.stk, --sp) : kRef2End;
+                    }
+                } else {
+                    cur = node2_step(sc, cur, br, tmax_box, sp);
+                }
+            }
+        }
+        if (!wave_any(lc != 0u)) break;
+        for (uint32_t i = 0; i < lc; ++i) {
+            const uint32_t pi = lf + i;
+            const DPrim p = load_global(sc.gprims, pi);
+            float t, u, v;
+            if (prim_hit_l<kSph>(p, ray, t, u, v)) {
+                if (t < best.t || (t == best.t && p.pad < best_orig)) {
+                    best.t = t; best.u = u; best.v = v; best.prim = (int32_t) pi;
+                    best_orig = p.pad;
+                    tmax_box = t;
+                }
+            }
+        }
+    }
+    return best;
+}
+template <int kSph> AD bool trace_any2(const SceneRef &sc, const Ray &ray, bool found) {
+    const BoxRay br = box_ray(ray);
+    uint32_t cur = found ? kRef2End : 0u, sp = 0;
+    for (;;) {
+        uint32_t lf = 0, lc = 0;
+        bool stop = false;
+        for (;;) {
+            if (!wave_any(lc == 0u && cur != kRef2End)) break;
+            if (cur != kRef2End && !stop) {
+                if (cur & kRef2Leaf) {
+                    stop = lc != 0u;
+                    if (!stop) {
+                        lf = cur & kRef2FirstMask;
+                        lc = (cur >> kRef2CountShift) & 15u;
+                        cur = sp ? stk_load(sc.stk, --sp) : kRef2End;
+                    }
+                } else {
+                    cur = node2_step(sc, cur, br, ray.maxt, sp);
+                }
+            }
+        }
+        if (!wave_any(lc != 0u)) break;
+        bool f = false;
+        for (uint32_t i = 0; i < lc && !f; ++i) {
+            const DPrim p = load_global(sc.gprims, lf + i);
+            float t, u, v;
+            f = prim_hit_l<kSph>(p, ray, t, u, v);
+        }
+        if (f) { found = true; cur = kRef2End; }
+    }
+    return found;
 }
 
 /*

@@ -32,6 +32,23 @@ struct alignas(16) DNode {
     uint32_t skip_count;     /* bits 0..27: skip node index; bits 28..31: prim count (0 = inner node) */
 };
 constexpr uint32_t kNodeSkipMask = 0x0fffffffu, kNodeCountShift = 28, kMaxLeafPrims = 15;
+/*
+ * Two-box BVH node (round 6) for the per-lane suffix walks of large BVHs: an inner node of the same binary SAH
+ * tree holding BOTH children's (padded) boxes and their references, so a walk loads a node only when it enters it
+ * -- one dependent load per inner node entered instead of one per node tested -- and orders the two children by
+ * the ray's own entry distances (near first) with the far one on a short per-lane LDS stack.  A reference is an
+ * inner node's index in nodes2[], or kRef2Leaf | count << 27 | first for a leaf of prims[first, first + count)
+ * (the threaded BVH's leaves, the same BVH-order prims[]).  4 x 16 B: (lo0.xyz, hi0.x), (hi0.yz, lo1.xy),
+ * (lo1.z, hi1.xyz), (ref0, ref1, -, -).
+ */
+struct alignas(16) DNode2 {
+    float b[12];             /* lo0[3], hi0[3], lo1[3], hi1[3] */
+    uint32_t ref[2];
+    uint32_t pad[2];
+};
+constexpr uint32_t kRef2Leaf = 0x80000000u, kRef2FirstMask = 0x07ffffffu, kRef2CountShift = 27;
+constexpr uint32_t kStack2 = 16;   /* per-lane stack entries of the two-box walks: a tree deeper than this keeps the
+                                    * threaded walks (a walk pushes at most one entry per inner node on its path) */
 /* BVHs up to this many nodes are traversed wave-uniformly; per-lane walks stage nodes + prims
  * in LDS up to kLdsSceneBytes. */
 constexpr uint32_t kUniformNodeLimit = 255, kLdsSceneBytes = 48 * 1024;
@@ -149,6 +166,10 @@ struct DScene {
      * `type` | its index in prims[] << 8 (they follow the BVH's primitives there); n_outer = 0: none */
     const DPrim *outer;
     uint32_t n_outer;
+    /* the two-box BVH of the per-lane suffix walks (DNode2; nodes2[0] is the root); n_nodes2 = 0: none (small or
+     * LDS-staged BVHs, a tree deeper than kStack2, or AMVPT_BVH2 off) */
+    const DNode2 *nodes2;
+    uint32_t n_nodes2;
 };
 constexpr uint32_t kOuterMax = 8;
 constexpr uint32_t kPortal = 0x80000000u;

@@ -18,6 +18,8 @@ struct amvpt_scene {
     uint32_t n_outer = 0;       /* rectangles kept out of the BVH (DScene::outer) */
     bool bvh_tri_only = false;  /* every BVH primitive is a triangle (the WALK_LANE_TRI suffix walks) */
     uint32_t n_boxes = 0;       /* box meshes the brute-force walks screen (DScene::boxes) */
+    uint32_t n_nodes2 = 0;      /* two-box BVH nodes (DScene::nodes2; 0: the per-lane walks stay threaded) */
+    uint32_t bvh2_depth = 0;    /* its depth in inner nodes (<= kStack2 when built) */
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   /* the BVH root box (ray binning's grid) */
     bool has_spheres = false;   /* the brute-force suffix walks take their sphere-free instances otherwise */
     bool all_diffuse = false;   /* every BSDF is plain `diffuse`: kernels take their kDiff instances */

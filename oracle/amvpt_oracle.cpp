@@ -52,6 +52,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <functional>
+#include <array>
 
 using namespace orc;
 
@@ -179,6 +181,11 @@ struct Scene {
     int environment = -1;         /* the constant emitter (Scene::m_environment), or -1 */
     V3 bs_center{0, 0, 0};        /* ConstantBackgroundEmitter::m_bsphere after set_scene */
     float bs_radius = 0.f;
+    /* optional acceleration (oracle_set_bvh, the CPU-baseline timing only; the parity tests keep the brute-force
+     * scans): a binary median-split BVH over padded primitive boxes, leaves of <= 4 primitive indices */
+    struct BNode { double lo[3], hi[3]; uint32_t first, count, right, axis; };
+    std::vector<BNode> bvh;
+    std::vector<uint32_t> bvh_idx;
 };
 
 /* PreliminaryIntersection */
@@ -249,8 +256,137 @@ static inline bool sphere_hit(const Shape &s, const Ray &ray, float &t_out) {
     return active;
 }
 
-/* closest hit: minimum (t, prim index) over all primitives (brute force). */
+static inline bool prim_hit_any_type(const Scene &sc, size_t i, const Ray &ray, float &t, float &u, float &v) {
+    const Prim &pr = sc.prims[i];
+    const Shape &s = sc.shapes[pr.shape];
+    u = v = 0.f;
+    if (pr.type == AMVPT_SHAPE_RECTANGLE) return rect_hit(s, ray, t, u, v);
+    if (pr.type == AMVPT_SHAPE_MESH) return tri_hit(s, pr.face, ray, t, u, v);
+    return sphere_hit(s, ray, t);
+}
+/* slab test of a padded box in double (conservative for every hit the float tests report) */
+static inline bool bvh_box_hit(const Scene::BNode &n, const Ray &ray, float tmax) {
+    double t0 = 0.0, t1 = (double) tmax;
+    const double o[3] = {ray.o.x, ray.o.y, ray.o.z}, d[3] = {ray.d.x, ray.d.y, ray.d.z};
+    for (int a = 0; a < 3; ++a) {
+        if (d[a] == 0.0) {
+            if (o[a] < n.lo[a] || o[a] > n.hi[a]) return false;
+            continue;
+        }
+        const double inv = 1.0 / d[a];
+        double ta = (n.lo[a] - o[a]) * inv, tb = (n.hi[a] - o[a]) * inv;
+        if (ta > tb) std::swap(ta, tb);
+        t0 = std::max(t0, ta);
+        t1 = std::min(t1, tb);
+        if (t0 > t1) return false;
+    }
+    return true;
+}
+/* the BVH walk: every primitive whose box the ray crosses, closest by the (t, index) rule (= the brute-force scan's
+ * lowest-index-first tie break), or any hit */
+template <bool kAny> static PI bvh_walk(const Scene &sc, const Ray &ray) {
+    PI best;
+    uint32_t stack[128], sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const Scene::BNode &n = sc.bvh[stack[--sp]];
+        /* closest hit: boxes beyond the best hit so far are skipped (inclusive: a tie may still win on the index) */
+        if (!bvh_box_hit(n, ray, kAny ? ray.maxt : std::min(ray.maxt, best.t))) continue;
+        if (n.count) {
+            for (uint32_t k = 0; k < n.count; ++k) {
+                const uint32_t i = sc.bvh_idx[n.first + k];
+                float t, u, v;
+                if (prim_hit_any_type(sc, i, ray, t, u, v) && (t < best.t || (t == best.t && (int) i < best.prim))) {
+                    best.t = t; best.u = u; best.v = v; best.prim = (int) i;
+                    if (kAny) return best;
+                }
+            }
+        } else if (sp + 2 <= 128) {
+            /* the child on the ray's side of the split first (popped first) */
+            const uint32_t left = (uint32_t) (&n - sc.bvh.data()) + 1u;
+            const float da = n.axis == 0 ? ray.d.x : n.axis == 1 ? ray.d.y : ray.d.z;
+            stack[sp++] = da < 0.f ? left : n.right;
+            stack[sp++] = da < 0.f ? n.right : left;
+        } else {
+            /* (never at these depths) the rest by brute force */
+            for (size_t i = 0; i < sc.prims.size(); ++i) {
+                float t, u, v;
+                if (prim_hit_any_type(sc, i, ray, t, u, v) && (t < best.t || (t == best.t && (int) i < best.prim))) {
+                    best.t = t; best.u = u; best.v = v; best.prim = (int) i;
+                }
+            }
+            return best;
+        }
+    }
+    return best;
+}
+static void build_bvh(Scene &sc) {
+    const size_t n = sc.prims.size();
+    std::vector<std::array<double, 6>> box(n);
+    std::vector<std::array<double, 3>> cen(n);
+    for (size_t i = 0; i < n; ++i) {
+        const Prim &pr = sc.prims[i];
+        const Shape &s = sc.shapes[pr.shape];
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        auto grow = [&](V3 p) {
+            const double q[3] = {p.x, p.y, p.z};
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], q[a]); hi[a] = std::max(hi[a], q[a]); }
+        };
+        if (pr.type == AMVPT_SHAPE_RECTANGLE) {
+            for (int c = 0; c < 4; ++c) grow(xform_point_affine(s.to_world, v3((c & 1) ? 1.f : -1.f, (c & 2) ? 1.f : -1.f, 0.f)));
+        } else if (pr.type == AMVPT_SHAPE_MESH) {
+            for (int k = 0; k < 3; ++k) grow(vtx(s, s.faces[3 * pr.face + k]));
+        } else {
+            grow(v3(s.center[0] - s.radius, s.center[1] - s.radius, s.center[2] - s.radius));
+            grow(v3(s.center[0] + s.radius, s.center[1] + s.radius, s.center[2] + s.radius));
+        }
+        double m = 0.0;
+        for (int a = 0; a < 3; ++a) m = std::max(m, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+        const double e = 1e-4 * (1.0 + m);
+        for (int a = 0; a < 3; ++a) {
+            box[i][a] = lo[a] - e; box[i][3 + a] = hi[a] + e;
+            cen[i][a] = .5 * (lo[a] + hi[a]);
+        }
+    }
+    sc.bvh_idx.resize(n);
+    for (size_t i = 0; i < n; ++i) sc.bvh_idx[i] = (uint32_t) i;
+    sc.bvh.clear();
+    std::function<uint32_t(uint32_t, uint32_t)> build = [&](uint32_t b, uint32_t e) -> uint32_t {
+        const uint32_t at = (uint32_t) sc.bvh.size();
+        sc.bvh.push_back({});
+        Scene::BNode nd{};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int a = 0; a < 3; ++a) { nd.lo[a] = INFINITY; nd.hi[a] = -INFINITY; }
+        for (uint32_t k = b; k < e; ++k) {
+            const uint32_t i = sc.bvh_idx[k];
+            for (int a = 0; a < 3; ++a) {
+                nd.lo[a] = std::min(nd.lo[a], box[i][a]); nd.hi[a] = std::max(nd.hi[a], box[i][3 + a]);
+                clo[a] = std::min(clo[a], cen[i][a]); chi[a] = std::max(chi[a], cen[i][a]);
+            }
+        }
+        if (e - b <= 4) {
+            nd.first = b; nd.count = e - b;
+        } else {
+            int ax = 0;
+            for (int a = 1; a < 3; ++a) if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
+            const uint32_t mid = (b + e) / 2;
+            std::nth_element(sc.bvh_idx.begin() + b, sc.bvh_idx.begin() + mid, sc.bvh_idx.begin() + e,
+                             [&](uint32_t x, uint32_t y) { return cen[x][ax] < cen[y][ax]; });
+            build(b, mid);                  /* left child: at + 1 */
+            nd.right = build(mid, e);
+            nd.count = 0;
+            nd.axis = (uint32_t) ax;
+        }
+        sc.bvh[at] = nd;
+        return at;
+    };
+    if (n) build(0, (uint32_t) n);
+}
+static bool g_use_bvh = false;   /* oracle_set_bvh */
+
+/* closest hit: minimum (t, prim index) over all primitives (brute force; or the BVH walk, oracle_set_bvh). */
 static PI intersect_pi(const Scene &sc, const Ray &ray) {
+    if (!sc.bvh.empty()) return bvh_walk<false>(sc, ray);
     PI best;
     for (size_t i = 0; i < sc.prims.size(); ++i) {
         const Prim &pr = sc.prims[i];
@@ -266,6 +402,7 @@ static PI intersect_pi(const Scene &sc, const Ray &ray) {
 }
 
 static bool ray_test(const Scene &sc, const Ray &ray) {
+    if (!sc.bvh.empty()) return bvh_walk<true>(sc, ray).prim >= 0;
     for (size_t i = 0; i < sc.prims.size(); ++i) {
         const Prim &pr = sc.prims[i];
         const Shape &s = sc.shapes[pr.shape];
@@ -1584,6 +1721,7 @@ bool build_scene(const amvpt_scene_desc *d, Scene &sc) {
         }
         sc.shapes.push_back(std::move(sh));
     }
+    if (g_use_bvh && sc.prims.size() > 64) build_bvh(sc);
     if (sc.environment >= 0) {
         /* ConstantBackgroundEmitter::set_scene (constant.cpp:73-88): the bounding sphere of the scene's
          * bounding box (union of Shape::bbox: rectangle corners rectangle.cpp bbox(), mesh vertices,
@@ -1686,6 +1824,9 @@ struct oracle_stats { uint64_t lanes, vertices, reuse_lanes, visibility_rays, ad
  * into the f32 film once at the end (k_fixed_resolve); 0: the f32 film of ImageBlock::put */
 static bool g_fixed_film = false;
 void oracle_set_fixed_film(int on) { g_fixed_film = on != 0; }
+/* closest-hit / any-hit queries through a BVH instead of the brute-force scans (scenes of more than 64 primitives):
+ * the same hits by the (t, index) rule -- bench.py's CPU baseline on the mesh config; the parity tests keep it off */
+void oracle_set_bvh(int on) { g_use_bvh = on != 0; }
 
 /*
  * Render [lane_begin, lane_end) of every pass into `film` (host memory, H*W*C

@@ -43,6 +43,7 @@ def lib():
         L.oracle_set_exchange.argtypes = [ExchangeFn, ctypes.c_void_p]
         L.oracle_set_run_exchange.argtypes = [RunExchangeFn, ctypes.c_void_p]
         L.oracle_set_fixed_film.argtypes = [ctypes.c_int]
+        L.oracle_set_bvh.argtypes = [ctypes.c_int]
         L.oracle_primary_hits.restype = ctypes.c_int
         L.oracle_primary_hits.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_render_rect.restype = ctypes.c_int
@@ -155,6 +156,12 @@ def render_rect(scene_desc_ptr, views_ptr, params, rect, threads=0, film=None):
     if rc != 0:
         raise RuntimeError("oracle_render_rect failed (status %d)" % rc)
     return film, st.as_dict()
+
+
+def set_bvh(on):
+    """Closest-hit / any-hit queries through a BVH (scenes of > 64 primitives) instead of brute force: the same hits
+    (the (t, index) rule); bench.py's CPU baseline uses it, the parity tests do not."""
+    lib().oracle_set_bvh(1 if on else 0)
 
 
 def render(scene_desc_ptr, views_ptr, params, lane_begin=0, lane_end=2 ** 64 - 1, threads=0,

@@ -507,6 +507,23 @@ def test_file_meshes_per_lane_bvh(gpu_ready, amvpt_mod, oracle):
     _check(amvpt_mod, oracle, s)
 
 
+@pytest.mark.parametrize("kw", [dict(res=16, spp=16), dict(res=24, spp=16, gx=4, gy=2, reuse=8)], ids=["path_g1", "g8"])
+def test_two_box_bvh_keeps_records(gpu_ready, amvpt_mod, oracle, kw):
+    """The per-lane suffix walks of the 3.6 k-triangle mesh on the two-box BVH (dscene.h DNode2: both child boxes in
+    a node, near-first by the ray's entry distances, a 16-entry LDS stack; dgeom.h trace_closest2 / trace_any2):
+    records bit-identical to the oracle, binned and unbinned, and to the threaded walks (AMVPT_OPT_THREADED_BVH)."""
+    s = amvpt_mod.load_file(MESH, **kw)
+    sd, vd, p = s.describe(0, 0, 0)
+    n2, depth = amvpt_mod.DeviceScene(sd).bvh2()
+    print("two-box BVH: %d nodes, depth %d" % (n2, depth))
+    assert n2 > 0 and 0 < depth <= 16
+    _check(amvpt_mod, oracle, s)
+    _check(amvpt_mod, oracle, s, flags=amvpt_mod.OPT_NO_BINNING)
+    a = _records(amvpt_mod, oracle, sd, vd, p, 0)
+    b = _records(amvpt_mod, oracle, sd, vd, p, amvpt_mod.OPT_THREADED_BVH)
+    assert _bit_equal(a, b).all()
+
+
 @pytest.mark.parametrize("kw", [dict(res=16, spp=16), dict(res=16, spp=16, gx=4, gy=2, reuse=8)], ids=["path_g1", "g8"])
 def test_ray_binning_keeps_records(gpu_ready, amvpt_mod, oracle, kw):
     """Ray binning (k_bin_sort): the per-lane suffix walks of the 3.6 k-triangle mesh take each partition's

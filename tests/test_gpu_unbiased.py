@@ -25,9 +25,10 @@ drop-in host path (Integrator::render -> C-ABI -> HIP) on the GPU, K independent
    case tests that explanation: with a one-pixel footprint the rejections must shrink to the 3 x 3
    neighbourhood of the discontinuities themselves.  Tile-edge pixels mix two views' content in the
    borderless quilt.
-2. Per-view energy: the mean over each view's interior pixels, two-sample z over the K frames,
-   |z| < 4.5 for every view -- a systematic bias (MIS weights that do not sum to one, a lost or
-   doubled strategy) moves these means while edge effects of either sign average out.
+2. Per-view energy: the mean over each view's interior pixels off the edge mask, two-sample z over the
+   K frames, |z| < 4.5 for every view -- a systematic bias (MIS weights that do not sum to one, a lost or
+   doubled strategy) moves these means.  (Round 5 took every interior pixel, assuming the edge effects of
+   either sign average out; with a wide baseline -- the cone grid -- they do not, see the case list.)
 3. Power: the same AMVPT frames scaled by 1.3 fail gate 1.
 """
 import os
@@ -138,10 +139,10 @@ def _z_gate(test, ref, significance=0.01):
     return float((p > alpha).mean()), float(p.min()), alpha
 
 
-def _view_means(frames, res):
-    """(K, n_views) mean over each view tile's interior"""
+def _view_means(frames, res, mask=None):
+    """(K, n_views) mean over each view tile's interior (and `mask`)"""
     Kf, H, W, _ = frames.shape
-    inner = _interior((H, W), res)
+    inner = _interior((H, W), res) if mask is None else mask
     out = []
     for ty in range(H // res):
         for tx in range(W // res):
@@ -191,12 +192,20 @@ def test_amvpt_views_unbiased_against_single_view(gpu_ready, amvpt_mod, name, pa
     gate = interior & ~edges
     frac, pmin, alpha = _z_gate(test[:, gate], ref[:, gate])
     full, _, _ = _z_gate(test[:, interior], ref[:, interior])
-    vt, vr = _view_means(test, res), _view_means(ref, res)
+    # per-view energy over the same off-mask pixels as the Z-test (round 6): the discontinuity pixels carry the
+    # self-normalised film's footprint-straddle bias, which does not cancel within a view once the group's
+    # baseline is wide -- tools/cone_control.py (profiles/r06d_cone_control.*): on the 12-degree cone grid and on a
+    # plain cam_dir line through the same camera positions the central views' interior means read +0.14..0.19 %
+    # (|z| up to 11 at 256 spp, growing with spp), all of it in the masked pixels; off the mask every view is
+    # within 0.03 % (|z| < 2.1), with either filter
+    vt, vr = _view_means(test, res, gate), _view_means(ref, res, gate)
     zv = np.abs(vt.mean(0) - vr.mean(0)) / np.sqrt(vt.var(0, ddof=1) / K + vr.var(0, ddof=1) / K)
+    at, ar = _view_means(test, res), _view_means(ref, res)
+    za = np.abs(at.mean(0) - ar.mean(0)) / np.sqrt(at.var(0, ddof=1) / K + ar.var(0, ddof=1) / K)
     print("%s: off-edge gate %.5f of %d channels (%.1f %% of the interior; p > %.3g, min p %.3g); all interior %.5f; "
-          "per-view |z| max %.2f, mean ratio %s" % (
+          "per-view off-mask |z| max %.2f, mean ratio %s; all-interior |z| max %.2f, mean ratio %s" % (
               name, frac, int(gate.sum()) * 3, 100.0 * gate.sum() / interior.sum(), alpha, pmin, full, zv.max(),
-              np.round(vt.mean(0) / vr.mean(0), 4).tolist()))
+              np.round(vt.mean(0) / vr.mean(0), 4).tolist(), za.max(), np.round(at.mean(0) / ar.mean(0), 4).tolist()))
     assert frac >= 0.9975, "Z-test rejects: only %.4f of off-edge pixel channels pass" % frac
     assert zv.max() < 4.5, "per-view mean differs: |z| = %s" % np.round(zv, 2).tolist()
 

@@ -315,3 +315,23 @@ def test_fixed_point_film_matches_float_film(oracle, amvpt_mod):
     assert np.abs(x1 - f).max() <= 1e-5 * np.abs(f).max()
     g, _, _ = oracle.render(sd, vd, p, threads=4)   # the mode does not stick
     assert np.abs(g - f).max() <= 1e-5 * np.abs(f).max()
+
+
+def test_oracle_bvh_mode_matches_brute_force(amvpt_mod, oracle):
+    """The oracle's optional BVH (oracle_set_bvh: bench.py's CPU baseline on BVH scenes) gives the brute-force scan's
+    records bit for bit on the 3.6 k-triangle mesh scene (path and G = 8)."""
+    import os
+    import numpy as np
+    from conftest import SCENES
+    for kw in (dict(res=8, spp=16), dict(res=8, spp=16, gx=4, gy=2, reuse=8)):
+        s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_mesh.xml"), **kw)
+        sd, vd, p = s.describe(0, 0, 0)
+        f0, r0, _ = oracle.render(sd, vd, p, threads=8, record_pass=0)
+        oracle.set_bvh(True)
+        try:
+            f1, r1, _ = oracle.render(sd, vd, p, threads=8, record_pass=0)
+        finally:
+            oracle.set_bvh(False)
+        same = (r0 == r1) | (np.isnan(r0) & np.isnan(r1))
+        assert same.all(), "%d record floats differ" % (~same).sum()
+        assert np.array_equal(f0, f1)
