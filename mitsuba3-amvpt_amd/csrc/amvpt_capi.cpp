@@ -42,6 +42,27 @@ static inline void hcross(const float *a, const float *b, float *o) {
     o[1] = std::fmaf(a[2], b[0], -(a[0] * b[2]));
     o[2] = std::fmaf(a[0], b[1], -(a[1] * b[0]));
 }
+/* x as an IEEE float16 bit pattern rounded toward -inf (up = false) or +inf (up = true); magnitudes past the
+ * float16 range go to -+inf / the largest finite value on the conservative side */
+static uint16_t half_dir(double x, bool up) {
+    auto to_d = [](uint16_t h) -> double {
+        const int e = (h >> 10) & 31, m = h & 1023;
+        const double v = e == 0 ? std::ldexp((double) m, -24) : e == 31 ? INFINITY : std::ldexp((double) (1024 + m), e - 25);
+        return (h & 0x8000) ? -v : v;
+    };
+    /* the nearest representable by bisection over the ordered bit patterns (monotone in value) */
+    auto key = [](uint16_t h) -> int { return (h & 0x8000) ? -(int) (h & 0x7fff) : (int) (h & 0x7fff); };
+    auto from_key = [](int k) -> uint16_t { return k < 0 ? (uint16_t) (0x8000 | (-k)) : (uint16_t) k; };
+    int lo = key(0xfc00), hi = key(0x7c00);   /* -inf .. +inf */
+    /* largest pattern with value <= x (down), or smallest with value >= x (up) */
+    if (!up) {
+        while (hi - lo > 1) { const int mid = lo + (hi - lo) / 2; if (to_d(from_key(mid)) <= x) lo = mid; else hi = mid; }
+        return from_key(to_d(from_key(hi)) <= x ? hi : lo);
+    }
+    while (hi - lo > 1) { const int mid = lo + (hi - lo) / 2; if (to_d(from_key(mid)) >= x) hi = mid; else lo = mid; }
+    return from_key(to_d(from_key(lo)) >= x ? lo : hi);
+}
+
 /* .5 * dr::norm(dr::cross(p1 - p0, p2 - p0)) (mesh.cpp:470) */
 static inline float tri_area(const float *p0, const float *p1, const float *p2) {
     const float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
@@ -715,6 +736,8 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     }
     std::vector<DNode> nodes, tnodes, onodes;
     std::vector<DNode2> nodes2;   /* the two-box BVH (empty: none) */
+    std::vector<DNode2h> nodes2h; /* its float16 form */
+    float n2_center[3] = {0.f, 0.f, 0.f}, n2_scale = 1.f;
     uint32_t bvh2_depth = 0;
     std::vector<DPrim> prims;
     uint32_t oct_stride = 0;   /* nodes per octant copy (0: one copy) */
@@ -785,6 +808,29 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
             }
             bvh2_depth = depth;
             if (depth > kStack2) nodes2.clear();
+            /* the float16 form (dscene.h DNode2h): the root box's centre and half extent set the frame */
+            const Box &rb = b.nodes[0].box;
+            double hmax = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                n2_center[k] = (float) (.5 * ((double) rb.lo[k] + (double) rb.hi[k]));
+                hmax = std::max(hmax, .5 * ((double) rb.hi[k] - (double) rb.lo[k]));
+            }
+            n2_scale = hmax > 0.0 ? (float) (1.0 / hmax) : 1.f;
+            for (const DNode2 &n : nodes2) {
+                DNode2h q{};
+                uint16_t hv[12];
+                for (int c = 0; c < 2; ++c)
+                    for (int k = 0; k < 3; ++k) {
+                        const double lo = ((double) n.b[6 * c + k] - (double) n2_center[k]) * (double) n2_scale;
+                        const double hi = ((double) n.b[6 * c + 3 + k] - (double) n2_center[k]) * (double) n2_scale;
+                        hv[6 * c + k] = half_dir(lo, false);
+                        hv[6 * c + 3 + k] = half_dir(hi, true);
+                    }
+                for (int w = 0; w < 6; ++w) q.h[w] = (uint32_t) hv[2 * w] | ((uint32_t) hv[2 * w + 1] << 16);
+                q.ref[0] = n.ref[0];
+                q.ref[1] = n.ref[1];
+                nodes2h.push_back(q);
+            }
         }
         prims.resize(bprims.size());
         for (size_t i = 0; i < bprims.size(); ++i) prims[i] = scene_prims[bprims[i].idx];
@@ -876,10 +922,11 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     if (box_prims.empty()) box_prims.resize(1);
     if (loose_prims.empty()) loose_prims.resize(1);
     void *p_nodes, *p_prims, *p_shapes, *p_bsdfs, *p_emit, *p_vpos, *p_vnrm, *p_vuv, *p_faces, *p_farea, *p_tnodes, *p_onodes, *p_sph;
-    void *p_boxes, *p_box_prims, *p_loose, *p_outer, *p_nodes2;
+    void *p_boxes, *p_box_prims, *p_loose, *p_outer, *p_nodes2, *p_nodes2h;
     if (tnodes.empty()) tnodes.resize(1);   /* keep a valid pointer */
     const uint32_t n_nodes2 = (uint32_t) nodes2.size();
     if (nodes2.empty()) nodes2.resize(1);
+    if (nodes2h.empty()) nodes2h.resize(1);
     if (onodes.empty()) onodes.resize(1);
     amvpt_status st;
 #define UP(vec, ptr)                                                                      \
@@ -890,7 +937,7 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     UP(nodes, p_nodes) UP(prims, p_prims) UP(shapes, p_shapes) UP(bsdfs, p_bsdfs) UP(emitters, p_emit)
     UP(vpos, p_vpos) UP(vnrm, p_vnrm) UP(vuv, p_vuv) UP(faces, p_faces) UP(face_area, p_farea) UP(tnodes, p_tnodes) UP(onodes, p_onodes)
     UP(sph_prims, p_sph) UP(boxes, p_boxes) UP(box_prims, p_box_prims) UP(loose_prims, p_loose) UP(outer, p_outer)
-    UP(nodes2, p_nodes2)
+    UP(nodes2, p_nodes2) UP(nodes2h, p_nodes2h)
 #undef UP
     DScene &D = sc->dev;
     D.nodes = (const DNode *) p_nodes;
@@ -927,6 +974,9 @@ amvpt_status amvpt_scene_create(const amvpt_scene_desc *d, amvpt_scene **out) {
     D.n_outer = n_outer;
     D.nodes2 = (const DNode2 *) p_nodes2;
     D.n_nodes2 = n_nodes2;
+    D.nodes2h = (const DNode2h *) p_nodes2h;
+    for (int k = 0; k < 3; ++k) D.n2_center[k] = n2_center[k];
+    D.n2_scale = n2_scale;
     sc->n_nodes2 = n_nodes2;
     sc->bvh2_depth = bvh2_depth;
     sc->n_outer = n_outer;

@@ -923,19 +923,48 @@ AD void stk_store(uint32_t *stk, uint32_t k, uint32_t v) {
     ((lu32 *) (uint32_t) (uintptr_t) stk)[k * kStk2Stride] = v;
 }
 constexpr uint32_t kRef2End = 0x7fffffffu;   /* no node (an inner index never reaches it) */
+/* the 32-B float16 nodes (dscene.h DNode2h) instead of the 64-B float ones: half the bytes per node step (A/B) */
+#ifndef AMVPT_BVH2_HALF
+#define AMVPT_BVH2_HALF 1
+#endif
+AD void half2_unpack(uint32_t w, float &a, float &b) {
+    a = (float) __builtin_bit_cast(_Float16, (uint16_t) (w & 0xffffu));
+    b = (float) __builtin_bit_cast(_Float16, (uint16_t) (w >> 16));
+}
+/* the walk's ray: in the float16 nodes' normalized frame (same t: origin and direction scale together) */
+AD BoxRay box2_ray(const SceneRef &sc, const Ray &r) {
+    if (!AMVPT_BVH2_HALF) return box_ray(r);
+    const DScene &S = *sc.g;
+    const float s = S.n2_scale;
+    const Ray q{mk((r.o.x - S.n2_center[0]) * s, (r.o.y - S.n2_center[1]) * s, (r.o.z - S.n2_center[2]) * s),
+                mk(r.d.x * s, r.d.y * s, r.d.z * s), r.maxt};
+    return box_ray(q);
+}
 /* one step of a two-box walk at inner node `cur`: enter the nearer hit child, stack the farther one */
 AD uint32_t node2_step(const SceneRef &sc, uint32_t cur, const BoxRay &br, float tmax, uint32_t &sp) {
-    const DNode2 n = load_global(sc.nodes2, cur);
+    float bx[12];
+    uint32_t r0, r1;
+    if (AMVPT_BVH2_HALF) {
+        const DNode2h n = load_global(sc.g->nodes2h, cur);
+#pragma unroll
+        for (int w = 0; w < 6; ++w) half2_unpack(n.h[w], bx[2 * w], bx[2 * w + 1]);
+        r0 = n.ref[0]; r1 = n.ref[1];
+    } else {
+        const DNode2 n = load_global(sc.nodes2, cur);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) bx[k] = n.b[k];
+        r0 = n.ref[0]; r1 = n.ref[1];
+    }
     float t0, t1;
-    const bool h0 = box2_hit(n.b, br, tmax, t0), h1 = box2_hit(n.b + 6, br, tmax, t1);
+    const bool h0 = box2_hit(bx, br, tmax, t0), h1 = box2_hit(bx + 6, br, tmax, t1);
     const bool sw = h1 && (!h0 || t1 < t0);
-    const uint32_t a = sw ? n.ref[1] : n.ref[0], b = sw ? n.ref[0] : n.ref[1];
+    const uint32_t a = sw ? r1 : r0, b = sw ? r0 : r1;
     if (h0 && h1) stk_store(sc.stk, sp++, b);
     if (h0 || h1) return a;
     return sp ? stk_load(sc.stk, --sp) : kRef2End;
 }
 template <int kSph> AD Hit trace_closest2(const SceneRef &sc, const Ray &ray, Hit best, uint32_t best_orig) {
-    const BoxRay br = box_ray(ray);
+    const BoxRay br = box2_ray(sc, ray);
     float tmax_box = fminf(ray.maxt, best.t);
     uint32_t cur = 0, sp = 0;
     for (;;) {
@@ -974,7 +1003,7 @@ template <int kSph> AD Hit trace_closest2(const SceneRef &sc, const Ray &ray, Hi
     return best;
 }
 template <int kSph> AD bool trace_any2(const SceneRef &sc, const Ray &ray, bool found) {
-    const BoxRay br = box_ray(ray);
+    const BoxRay br = box2_ray(sc, ray);
     uint32_t cur = found ? kRef2End : 0u, sp = 0;
     for (;;) {
         uint32_t lf = 0, lc = 0;

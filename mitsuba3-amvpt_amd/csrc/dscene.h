@@ -47,6 +47,17 @@ struct alignas(16) DNode2 {
     uint32_t pad[2];
 };
 constexpr uint32_t kRef2Leaf = 0x80000000u, kRef2FirstMask = 0x07ffffffu, kRef2CountShift = 27;
+/*
+ * The same node in 32 B (AMVPT_BVH2_HALF): the two child boxes as float16 in the scene's normalized frame
+ * (x' = (x - n2_center) * n2_scale, the BVH root box mapped into [-1, 1]^3), each plane rounded outward (lo down, hi
+ * up) from the padded float box, so every box contains its float box: a cull test only, never a hit, so the walk
+ * finds the same hits.  h[0..5] = (lo0.xy), (lo0.z, hi0.x), (hi0.yz), (lo1.xy), (lo1.z, hi1.x), (hi1.yz), two halves
+ * per word, low half first; then the two references.
+ */
+struct alignas(16) DNode2h {
+    uint32_t h[6];
+    uint32_t ref[2];
+};
 constexpr uint32_t kStack2 = 16;   /* per-lane stack entries of the two-box walks: a tree deeper than this keeps the
                                     * threaded walks (a walk pushes at most one entry per inner node on its path) */
 /* BVHs up to this many nodes are traversed wave-uniformly; per-lane walks stage nodes + prims
@@ -170,6 +181,8 @@ struct DScene {
      * LDS-staged BVHs, a tree deeper than kStack2, or AMVPT_BVH2 off) */
     const DNode2 *nodes2;
     uint32_t n_nodes2;
+    const DNode2h *nodes2h;       /* the float16 form of nodes2 (AMVPT_BVH2_HALF), in the normalized frame: */
+    float n2_center[3], n2_scale; /*   x' = (x - n2_center) * n2_scale */
 };
 constexpr uint32_t kOuterMax = 8;
 constexpr uint32_t kPortal = 0x80000000u;

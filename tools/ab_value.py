@@ -57,6 +57,8 @@ def child(steps=3, kernels=False):
     dt = time.perf_counter() - t0
     out = {"variant": os.environ.get("AB_VARIANT", "lib"), "msamples_s": round(lanes * steps / dt / 1e6, 2),
            "ms_per_frame": round(dt * 1e3 / steps, 2)}
+    if hasattr(dev._lib, "amvpt_scene_bvh2"):
+        out["bvh2"] = dev.bvh2()   # (two-box BVH nodes, depth): 0 nodes = the threaded walks
     if kernels:
         # one instrumented frame with every chunk on one stream (per-kernel event times do not overlap)
         c = amvpt.Counters()
