@@ -924,6 +924,9 @@ AD void stk_store(uint32_t *stk, uint32_t k, uint32_t v) {
 }
 constexpr uint32_t kRef2End = 0x7fffffffu;   /* no node (an inner index never reaches it) */
 /* the 32-B float16 nodes (dscene.h DNode2h) instead of the 64-B float ones: half the bytes per node step (A/B) */
+#ifndef AMVPT_TRI_LOAD48
+#define AMVPT_TRI_LOAD48 1   /* the two-box walks of triangle-only BVHs load 48 / 52 B of a leaf triangle (0: 64, A/B) */
+#endif
 #ifndef AMVPT_BVH2_HALF
 #define AMVPT_BVH2_HALF 1
 #endif
@@ -963,6 +966,26 @@ AD uint32_t node2_step(const SceneRef &sc, uint32_t cur, const BoxRay &br, float
     if (h0 || h1) return a;
     return sp ? stk_load(sc.stk, --sp) : kRef2End;
 }
+/* a leaf primitive of the two-box walks: a triangle-only BVH (kSph < 0) reads the record's three vertex vectors and
+ * (closest hit: kPad) the scene-order index only -- 48 / 52 of its 64 B (the walks are bound by the bytes their
+ * divergent gathers return, see above); other BVHs read the whole record */
+template <int kSph, bool kPad> AD DPrim leaf_prim(const SceneRef &sc, uint32_t i) {
+    if constexpr (kSph < 0 && AMVPT_TRI_LOAD48) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const v4f gv4f;
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        const gv4f *q = (const gv4f *) (uintptr_t) (sc.gprims + i);
+        DPrim p;
+        const v4f a = q[0], b = q[1], c = q[2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { p.a[k] = a[k]; p.b[k] = b[k]; p.c[k] = c[k]; }
+        p.type = PRIM_TRI; p.shape = 0; p.face = 0;
+        p.pad = kPad ? ((gu32 *) (uintptr_t) (sc.gprims + i))[15] : 0u;
+        return p;
+    } else {
+        return load_global(sc.gprims, i);
+    }
+}
 template <int kSph> AD Hit trace_closest2(const SceneRef &sc, const Ray &ray, Hit best, uint32_t best_orig) {
     const BoxRay br = box2_ray(sc, ray);
     float tmax_box = fminf(ray.maxt, best.t);
@@ -989,7 +1012,7 @@ template <int kSph> AD Hit trace_closest2(const SceneRef &sc, const Ray &ray, Hi
         if (!wave_any(lc != 0u)) break;
         for (uint32_t i = 0; i < lc; ++i) {
             const uint32_t pi = lf + i;
-            const DPrim p = load_global(sc.gprims, pi);
+            const DPrim p = leaf_prim<kSph, true>(sc, pi);
             float t, u, v;
             if (prim_hit_l<kSph>(p, ray, t, u, v)) {
                 if (t < best.t || (t == best.t && p.pad < best_orig)) {
@@ -1026,7 +1049,7 @@ template <int kSph> AD bool trace_any2(const SceneRef &sc, const Ray &ray, bool 
         if (!wave_any(lc != 0u)) break;
         bool f = false;
         for (uint32_t i = 0; i < lc && !f; ++i) {
-            const DPrim p = load_global(sc.gprims, lf + i);
+            const DPrim p = leaf_prim<kSph, false>(sc, lf + i);
             float t, u, v;
             f = prim_hit_l<kSph>(p, ray, t, u, v);
         }
