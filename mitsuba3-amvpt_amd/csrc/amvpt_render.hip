@@ -2893,6 +2893,20 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * (uniform dynamic index) measured slower, 444 ms (r03h) */
 #define AMVPT_PAIR_REGS 1
 #endif
+#ifndef AMVPT_PDF_REGS
+/* 1: with the pair registers, the views' F_PDF lives in registers only (written under a uniform view index in
+ * camera_selection, read the same way in mis_weights), so the generic instance's per-view LDS state drops from 6
+ * to 5 fields: 29.4 -> 25.3 KB per 128-thread block at C3, 6 blocks (12 waves, its VGPR limit) per CU instead of
+ * 5 (0: A/B) */
+#define AMVPT_PDF_REGS 1
+#endif
+/* the generic compile-time groups keep F_PDF out of LDS (see AMVPT_PDF_REGS) */
+template <int G, bool kDiff> __host__ __device__ constexpr bool pdf_in_regs() {
+    return AMVPT_PAIR_REGS && AMVPT_PDF_REGS && !kDiff && G >= 2 && G <= 8;
+}
+template <int G, bool kDiff> __host__ __device__ constexpr int vs_fields() {
+    return kDiff ? kVsFieldsDiff : VS_FIELDS - (pdf_in_regs<G, kDiff>() ? 1 : 0);
+}
 #ifndef AMVPT_FUSED_TWO_STREAMS
 #define AMVPT_FUSED_TWO_STREAMS 0   /* 1: fused-suffix scenes alternate chunks over two streams too (A/B) */
 #endif
@@ -2943,7 +2957,9 @@ template <int G, bool kTab, bool kDiff, bool kGenRec>
 AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, const DView *V, const Bufs &B,
                         float *const vs, const uint32_t vs_stride, const uint32_t slot, const uint32_t i, const bool ok) {
     const int Gn = group_size<G>(P);
-#define VSF(f, k) vs[((f) * Gn + (k)) * vs_stride]
+    constexpr bool kPdfRegs = pdf_in_regs<G, kDiff>();
+    /* field f of view slot k (kPdfRegs: F_PDF is not stored, the other fields move down one) */
+#define VSF(f, k) vs[(((f) - (kPdfRegs ? 1 : 0)) * Gn + (k)) * vs_stride]
     PathState ps;
     bool push = false;
     unsigned long long st_reuse = 0, st_vis = 0;
@@ -3035,7 +3051,8 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                 /* ---- camera_selection (mvpath_multi.h:371-464) ---- */
                 Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
-                VSF(F_PDF, 0) = pdf0; VSF(F_JP, 0) = Jp0;
+                if (!kPdfRegs) VSF(F_PDF, 0) = pdf0;
+                VSF(F_JP, 0) = Jp0;
                 mset(vmask, 0, p_hit);
                 mset(imask, 0, p_hit);
                 const f3 wo_r0 = reflect_l(si.wi);
@@ -3056,6 +3073,12 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                     return P.fast_mis ? tv_pdf_fast(wo_r0, wik, pdfM, bd, active)
                                       : tv_pdf(S.bsdfs, wo_r0, wik, pdfM, bd, active);
                 };
+                /* kPdfRegs: the views' F_PDF (slots 1..G-1) */
+                float rPdf[kPdfRegs ? G : 1];
+                if constexpr (kPdfRegs) {
+#pragma unroll
+                    for (int j = 0; j < G; ++j) rPdf[j] = 0.f;
+                }
                 float n_direct = 1.f, n_indir = 2.f;
                 int rep_k = 0;   /* AMVPT_DEFER_SAMPLE: the view whose BSDF sample replaces the primary's */
                 (void) rep_k;
@@ -3084,7 +3107,13 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                     float pdf_Sel = pdf_Mat * pdf_J;
                     valid = valid && (rng.next_1d() < pdf_Sel);
                     VSF(F_JP, k) = r.Jp;
-                    VSF(F_PDF, k) = valid ? r.pdf : 0.f;
+                    if constexpr (kPdfRegs) {
+                        const float pk = valid ? r.pdf : 0.f;
+#pragma unroll
+                        for (int j = 1; j < G; ++j) rPdf[j] = j == k ? pk : rPdf[j];
+                    } else {
+                        VSF(F_PDF, k) = valid ? r.pdf : 0.f;
+                    }
                     bool indirect = valid, direct = valid;
                     bool replace = n_indir * rng.next_1d() < 1.f;
                     C3 bvk;
@@ -3154,7 +3183,9 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                 if constexpr (kPR > 1) {
 #pragma unroll
                     for (int j = 1; j < kPR; ++j) {
-                        pJp[j] = VSF(F_JP, j); pPdf[j] = VSF(F_PDF, j);
+                        pJp[j] = VSF(F_JP, j);
+                        if constexpr (kPdfRegs) pPdf[j] = rPdf[j < G ? j : 0];
+                        else pPdf[j] = VSF(F_PDF, j);
                         pWx[j] = VSF(F_WX, j); pWy[j] = VSF(F_WY, j); pWz[j] = VSF(F_WZ, j);
                     }
                 }
@@ -3172,7 +3203,16 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                         pdf_lk = vk ? pdf0 * J * ((kDiff ? 1.f : mat_pdf(wik, pdfMk, true)) * pdf_J) : 0.f;
                     }
                     float pdfSum = pdf_lk;
-                    if (k > 0) pdfSum += VSF(F_PDF, k);
+                    if (k > 0) {
+                        if constexpr (kPdfRegs) {
+                            float pk = 0.f;
+#pragma unroll
+                            for (int j = 1; j < G; ++j) pk = j == k ? pPdf[j] : pk;
+                            pdfSum += pk;
+                        } else {
+                            pdfSum += VSF(F_PDF, k);
+                        }
+                    }
                     bool cond = k > 0 ? vk : bd.reuse;
                     float acc = 0.f;
                     if (!kDiff && cond && !bd.diffuse) {
@@ -3722,7 +3762,7 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
                            const DScene *S, const DView *V, const Bufs &B, bool tab, bool uni, bool diff, KTimer &T) {
     constexpr int kPB = prim_block<G>(), kVW = vis_waves<G>();
     const dim3 g256((cn + 255) / 256), g64((cn + 63) / 64), gp((cn + kPB - 1) / kPB);
-    const size_t lds_view = B.vstate ? 0u : (size_t) (diff ? kVsFieldsDiff : VS_FIELDS) * group_size_host<G>(P) * kPB * sizeof(float);
+    const size_t lds_view = B.vstate ? 0u : (size_t) (diff ? vs_fields<G, true>() : vs_fields<G, false>()) * group_size_host<G>(P) * kPB * sizeof(float);
     if (uni && ab_knobs().fuse_prim) {
         T.begin(AMVPT_K_PRIM_HIT, st);
         /* sphere-free scenes: the instances without float64 sphere code (the Cornell and mesh benches); scenes of
