@@ -96,6 +96,9 @@ struct BNode { Box box; uint32_t left_or_first, count, axis = 0; };
 /* SAH shape: leaves of up to g_bvh_max_leaf primitives are kept when the split is
  * not cheaper; a split costs g_bvh_trav_cost primitive tests per unit of area on top
  * of the children's tests (amvpt_set_bvh_build). */
+#ifndef AMVPT_SAH_BINS
+#define AMVPT_SAH_BINS 16   /* centroid bins per axis of the binned SAH build */
+#endif
 static uint32_t g_bvh_max_leaf = 4;
 static float g_bvh_trav_cost = 0.f;
 /* depth of the LDS treelets (dscene.h DScene::tnodes), 0: none (A/B builds: EXTRA=-DAMVPT_TREELET_DEPTH=n);
@@ -144,7 +147,7 @@ struct Builder {
         set(ni, b);
         uint32_t n = end - begin;
         if (n <= 2) { nodes[ni].left_or_first = begin; nodes[ni].count = n; return; }
-        const int NB = 16;
+        const int NB = AMVPT_SAH_BINS;
         float best_cost = INFINITY;
         int best_axis = -1, best_split = -1;
         for (int ax = 0; ax < 3; ++ax) {
