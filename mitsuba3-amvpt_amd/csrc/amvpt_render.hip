@@ -199,7 +199,9 @@ struct Bufs {
     uint4 *lmask_w[24];   /* groups > 16 views: valid, indirect, wi.z > 0 masks per slot (mask_planes<G>() each) */
     float *vstate;        /* runtime groups whose per-view state exceeds LDS: VS_FIELDS x G x vs_stride floats */
     float4 *sray[2];      /* ray binning (k_bin_sort): a partition's rays in bin order, 32-B records [2 j], [2 j + 1]:
-                           * (o, d.x | dest), (d.yz | target, entry); sray[1] unused */
+                           * extension rays (o, d.x), (d.yz, entry, -); NEE rays (AMVPT_NEE_CARRY) (o, dest),
+                           * (target, result r) with sgb[j] = result g, b; sray[1] unused */
+    float2 *sgb;          /* ray binning of NEE rays: the visible result's green and blue channels in bin order */
     uint16_t *key_out, *key_in, *key_nee;   /* ray binning: bin keys of the pushed paths / NEE records (null: off) */
 };
 
@@ -1845,11 +1847,20 @@ AMVPT_TU_LOCAL __global__ void __launch_bounds__(256) k_raygen_adapt(KParams P, 
 #ifndef AMVPT_BIN
 #define AMVPT_BIN 3   /* bit 0: bin the extension rays (k_extend), bit 1: the NEE rays (k_shadow); 0: off (A/B) */
 #endif
+#ifndef AMVPT_NEE_CARRY
+/* 1: a binned NEE record carries the visible result itself (red in the record's last word, green and blue in a
+ * bin-order plane, sgb) instead of the entry it came from: k_shadow's visible write then reads it with the sorted
+ * record (coalesced) instead of two scattered loads from the unsorted records (nee[1][entry].w, nee_gb[entry]) --
+ * the mesh frame's k_shadow fetched 270 GB from HBM for ~50 GB of sorted records (r06y_traffic_mesh.json); 0: A/B */
+#define AMVPT_NEE_CARRY 1
+#endif
 #ifndef AMVPT_BIN_UNI
 #define AMVPT_BIN_UNI 0   /* 1: binned waves take the wave-uniform walk (scalar node loads) instead of the per-lane one */
 #endif
 template <bool kNee, bool kFromRays = false>
 __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
+    /* NEE records carry their visible result (AMVPT_NEE_CARRY): k_shadow then reads it in bin order */
+    constexpr bool nee_carry = kNee && AMVPT_NEE_CARRY;
     __shared__ uint32_t h[kBins];
     __shared__ uint32_t wsum[kBinBlock / 64];
     const uint32_t part = blockIdx.x;
@@ -1909,13 +1920,15 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
         /* one 32-B record per ray (a whole memory sector per scattered write, not two 16-B halves in two planes) */
         const uint32_t j = pbase + atomicAdd(&h[key], 1u);
         B.sray[0][2 * (size_t) j] = a;
-        B.sray[0][2 * (size_t) j + 1] = kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
+        B.sray[0][2 * (size_t) j + 1] = nee_carry ? b : kNee ? make_float4(b.x, b.y, b.z, bitsf(i)) : make_float4(b.x, b.y, bitsf(i), 0.f);
+        if (nee_carry) B.sgb[j] = B.nee_gb[i];
     };
 #if AMVPT_BIN_STAGE
     /* staged scatter: batches of kStage entries are counting-sorted in LDS first, so the global writes go out
      * as runs of consecutive records of one bin (consecutive threads, consecutive addresses) */
     constexpr uint32_t kStage = 2 * kBinBlock;
     __shared__ float4 stg[2 * kStage];
+    __shared__ float2 sgb[kNee && AMVPT_NEE_CARRY ? kStage : 1];
     __shared__ uint16_t skey[kStage];
     __shared__ uint32_t lh[kBins], lbase[kBins];
     for (uint32_t b0 = 0; b0 < count; b0 += kStage) {
@@ -1966,7 +1979,8 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
             if (e < count) {
                 const uint32_t sp = lh[k[u]] + r[u], i = pbase + e;
                 stg[2 * sp] = a[u];
-                stg[2 * sp + 1] = kNee ? make_float4(b[u].x, b[u].y, b[u].z, bitsf(i)) : make_float4(b[u].x, b[u].y, bitsf(i), 0.f);
+                stg[2 * sp + 1] = nee_carry ? b[u] : kNee ? make_float4(b[u].x, b[u].y, b[u].z, bitsf(i)) : make_float4(b[u].x, b[u].y, bitsf(i), 0.f);
+                if (nee_carry) sgb[sp] = B.nee_gb[i];
                 skey[sp] = (uint16_t) k[u];
             }
         }
@@ -1975,6 +1989,7 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
             const uint32_t q = skey[sp], j = pbase + lbase[q] + (sp - lh[q]);
             B.sray[0][2 * (size_t) j] = stg[2 * sp];
             B.sray[0][2 * (size_t) j + 1] = stg[2 * sp + 1];
+            if (nee_carry) B.sgb[j] = sgb[sp];
         }
         __syncthreads();
     }
@@ -2083,8 +2098,18 @@ __global__ void __launch_bounds__(256, AMVPT_SHADOW_WAVES) k_shadow(KParams P, c
                 const Ray r = nee_ray(a, b);
                 const bool occ = AMVPT_BIN_UNI ? trace_any<true, 0, kWalk != WALK_LANE_NS>(sc, r) : walk_any<kWalk>(sc, r);
                 if (!occ) {
-                    const uint32_t i = fbits(b.w);
-                    visible(i, a, make_float4(0.f, 0.f, 0.f, B.nee[1][i].w));
+                    if (AMVPT_NEE_CARRY) {
+                        /* the record's own result: red in b.w, green and blue in sgb[j] */
+                        const float2 gb = B.sgb[j];
+                        const uint32_t dest = fbits(a.w);
+                        float *const dp = (float *) ((dest & 0x80000000u) ? &B.lane_out[dest & 0x7fffffffu] : &B.q_out[4][dest]);
+                        dp[0] = b.w;
+                        dp[1] = gb.x;
+                        dp[2] = gb.y;
+                    } else {
+                        const uint32_t i = fbits(b.w);
+                        visible(i, a, make_float4(0.f, 0.f, 0.f, B.nee[1][i].w));
+                    }
                 }
             }
         }
@@ -4351,7 +4376,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
     const size_t lds_tab_views = (AMVPT_PRIM_TAB && tables_staged(scene->dev, Pp.n_views))
                                      ? scene->dev.tab_bytes + views_lds_bytes(Pp.n_views) : 0u;
     const bool vs_global = wide && lds_tab_views + (size_t) VS_FIELDS * G * 64 * sizeof(float) > 65536;
-    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + 32 + 6 /* binned rays and their keys */ +
+    const size_t per_lane = 2 * kQPlanes * 16 + 32 + 52 + 48 + 64 + 32 + 8 + 6 /* binned rays, binned NEE results, keys */ +
                             (size_t) (diff_rec ? 4 : (AMVPT_WAVE_DIFF ? 36 : 32)) * G + (G + 7) / 8 +
                             (wide ? (size_t) 4 * 16 * mplanes : 0) + (vs_global ? (size_t) VS_FIELDS * 4 * G : 0);
     uint64_t chunk_max = opts.chunk_lanes ? std::max<uint64_t>(256, opts.chunk_lanes) : 0;
@@ -4573,6 +4598,7 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         cs.ka = cs.kb = nullptr;
         B.key_out = B.key_in = B.key_nee = nullptr;
         if (bin_ext || bin_nee) { B.sray[0] = (float4 *) carve(32 * qlen); B.sray[1] = nullptr; }
+        B.sgb = (bin_nee && AMVPT_NEE_CARRY) ? (float2 *) carve(8 * qlen) : nullptr;
         if (bin_ext) { cs.ka = (uint16_t *) carve(2 * qlen); cs.kb = (uint16_t *) carve(2 * qlen); }
         if (bin_nee) B.key_nee = (uint16_t *) carve(2 * qlen);
         if (wide) {
