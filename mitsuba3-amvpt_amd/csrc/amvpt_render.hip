@@ -2925,12 +2925,24 @@ AD f3 reflect_l(f3 w) { return mk(-w.x, -w.y, w.z); }
  * 5 (0: A/B) */
 #define AMVPT_PDF_REGS 1
 #endif
+#ifndef AMVPT_DIFF_REGS
+/* 1: the all-diffuse body (kDiff: the all-diffuse scenes' k_mv_primary and the mixed scenes' all-diffuse waves) of
+ * the compile-time groups up to 8 views keeps both per-view fields, F_PDF and F_JP, in registers (written and read
+ * under a uniform view index, the MIS pair sums unrolled over register operands), so it has no per-view LDS state
+ * and no LDS read per pair term.  Measured slower (r06ad: config-M k_mv_primary 40.0 -> 41.7 ms, C3 and mesh neutral --
+ * the uniform-index select chains cost more issue than the LDS reads they replace), so 0: the two LDS fields */
+#define AMVPT_DIFF_REGS 0
+#endif
+/* the all-diffuse body keeps F_PDF and F_JP in registers (see AMVPT_DIFF_REGS) */
+template <int G, bool kDiff> __host__ __device__ constexpr bool diff_regs() {
+    return AMVPT_DIFF_REGS && AMVPT_PAIR_REGS && kDiff && G >= 2 && G <= 8;
+}
 /* the generic compile-time groups keep F_PDF out of LDS (see AMVPT_PDF_REGS) */
 template <int G, bool kDiff> __host__ __device__ constexpr bool pdf_in_regs() {
-    return AMVPT_PAIR_REGS && AMVPT_PDF_REGS && !kDiff && G >= 2 && G <= 8;
+    return (AMVPT_PAIR_REGS && AMVPT_PDF_REGS && !kDiff && G >= 2 && G <= 8) || diff_regs<G, kDiff>();
 }
 template <int G, bool kDiff> __host__ __device__ constexpr int vs_fields() {
-    return kDiff ? kVsFieldsDiff : VS_FIELDS - (pdf_in_regs<G, kDiff>() ? 1 : 0);
+    return kDiff ? (diff_regs<G, kDiff>() ? 0 : kVsFieldsDiff) : VS_FIELDS - (pdf_in_regs<G, kDiff>() ? 1 : 0);
 }
 #ifndef AMVPT_FUSED_TWO_STREAMS
 #define AMVPT_FUSED_TWO_STREAMS 0   /* 1: fused-suffix scenes alternate chunks over two streams too (A/B) */
@@ -2983,6 +2995,7 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                         float *const vs, const uint32_t vs_stride, const uint32_t slot, const uint32_t i, const bool ok) {
     const int Gn = group_size<G>(P);
     constexpr bool kPdfRegs = pdf_in_regs<G, kDiff>();
+    constexpr bool kJpRegs = diff_regs<G, kDiff>();   /* F_JP in registers as well: no per-view LDS state */
     /* field f of view slot k (kPdfRegs: F_PDF is not stored, the other fields move down one) */
 #define VSF(f, k) vs[(((f) - (kPdfRegs ? 1 : 0)) * Gn + (k)) * vs_stride]
     PathState ps;
@@ -3077,7 +3090,15 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                 Surf p0 = camera_sample_surface(V[view_of(0)], si, p_hit, apx, apy);
                 const float pdf0 = p0.pdf, Jp0 = p0.Jp, iJp0 = p_hit ? rcp(p0.Jp) : 0.f;
                 if (!kPdfRegs) VSF(F_PDF, 0) = pdf0;
-                VSF(F_JP, 0) = Jp0;
+                /* kJpRegs: the views' F_JP (slot 0 and slots 1..G-1) */
+                float rJp[kJpRegs ? G : 1];
+                if constexpr (kJpRegs) {
+                    rJp[0] = Jp0;
+#pragma unroll
+                    for (int j = 1; j < G; ++j) rJp[j] = 0.f;
+                } else {
+                    VSF(F_JP, 0) = Jp0;
+                }
                 mset(vmask, 0, p_hit);
                 mset(imask, 0, p_hit);
                 const f3 wo_r0 = reflect_l(si.wi);
@@ -3131,7 +3152,12 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                     float pdf_J = J > 1.f ? rcp(J) : J;
                     float pdf_Sel = pdf_Mat * pdf_J;
                     valid = valid && (rng.next_1d() < pdf_Sel);
-                    VSF(F_JP, k) = r.Jp;
+                    if constexpr (kJpRegs) {
+#pragma unroll
+                        for (int j = 1; j < G; ++j) rJp[j] = j == k ? r.Jp : rJp[j];
+                    } else {
+                        VSF(F_JP, k) = r.Jp;
+                    }
                     if constexpr (kPdfRegs) {
                         const float pk = valid ? r.pdf : 0.f;
 #pragma unroll
@@ -3203,21 +3229,30 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                 float n_ind = 0.f, pdf = 0.f;
                 /* the pair sums' operands of views j >= 1 (same for every k): registers for the
                  * compile-time groups up to 8 views, LDS otherwise */
-                constexpr int kPR = (AMVPT_PAIR_REGS && !kDiff && G >= 2 && G <= 8) ? G : 1;
-                float pJp[kPR], pPdf[kPR], pWx[kPR], pWy[kPR], pWz[kPR];
+                constexpr int kPR = (AMVPT_PAIR_REGS && (!kDiff || kJpRegs) && G >= 2 && G <= 8) ? G : 1;
+                constexpr int kPW = kDiff ? 1 : kPR;   /* the all-diffuse body reads no wi_j */
+                float pJp[kPR], pPdf[kPR], pWx[kPW], pWy[kPW], pWz[kPW];
                 if constexpr (kPR > 1) {
 #pragma unroll
                     for (int j = 1; j < kPR; ++j) {
-                        pJp[j] = VSF(F_JP, j);
+                        if constexpr (kJpRegs) pJp[j] = rJp[j < G ? j : 0];
+                        else pJp[j] = VSF(F_JP, j);
                         if constexpr (kPdfRegs) pPdf[j] = rPdf[j < G ? j : 0];
                         else pPdf[j] = VSF(F_PDF, j);
-                        pWx[j] = VSF(F_WX, j); pWy[j] = VSF(F_WY, j); pWz[j] = VSF(F_WZ, j);
+                        if constexpr (!kDiff) { pWx[j] = VSF(F_WX, j); pWy[j] = VSF(F_WY, j); pWz[j] = VSF(F_WZ, j); }
                     }
                 }
 #pragma unroll 1
                 for (int k = 0; k < Gn; ++k) {
                     const bool vk = mget(vmask, k);
-                    const float Jpk = VSF(F_JP, k);
+                    float Jpk;
+                    if constexpr (kJpRegs) {
+                        Jpk = rJp[0];
+#pragma unroll
+                        for (int j = 1; j < G; ++j) Jpk = j == k ? rJp[j] : Jpk;
+                    } else {
+                        Jpk = VSF(F_JP, k);
+                    }
                     const float iJpk = k == 0 ? iJp0 : (vk ? rcp(Jpk) : 0.f);
                     const f3 wik = wi_of(k);
                     const float pdfMk = kDiff ? 1.f : VSF(F_PDFM, k);
@@ -3249,7 +3284,8 @@ AD void mv_primary_lane(const KParams &P, const DScene &S, const SceneRef &sc, c
                             for (int j = 1; j < kPR; ++j) {
                                 if (j == k) continue;
                                 const float pdf_J = vmin(sqr(pJp[j] * iJpk), 1.f);
-                                const f3 worj = reflect_l(mk(pWx[j], pWy[j], pWz[j]));
+                                const int jw = kDiff ? 0 : j;   /* (the all-diffuse body never runs this branch) */
+                                const f3 worj = reflect_l(mk(pWx[jw], pWy[jw], pWz[jw]));
                                 const bool vj = mget(vmask, j);
 #if AMVPT_PDF_ROW
                                 const float pdf_Mat = P.fast_mis ? tv_pdf_fast(worj, wik, pdfMk, bd, vj)
@@ -3826,7 +3862,7 @@ void launch_primary(uint32_t cn, size_t lds_tab, size_t lds_bvh, hipStream_t st,
     else {
         if (AMVPT_WAVE_DIFF) {
             /* the all-diffuse waves first, with the all-diffuse body's smaller per-view LDS state */
-            const size_t lds_dw = B.vstate ? 0u : (size_t) kVsFieldsDiff * group_size_host<G>(P) * kPB * sizeof(float);
+            const size_t lds_dw = B.vstate ? 0u : (size_t) vs_fields<G, true>() * group_size_host<G>(P) * kPB * sizeof(float);
             if (tab) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, true, false, true>), gp, dim3(kPB), lds_tab + lds_dw, st, P, S, V, B);
             else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mv_primary<G, false, false, true>), gp, dim3(kPB), lds_tab + lds_dw, st, P, S, V, B);
         }
