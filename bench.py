@@ -112,11 +112,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AMVPT_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing the visible devices
+    # (rank -> device local % count; collectives staged through the host, amvpt.dist.comm_device): a check
+    # of the partitions and exchanges on real renders, not a measurement -- the metric runs over RCCL
+    backend = os.environ.get("AMVPT_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     hip = amvpt.hip_lib()
     hip.amvpt_set_device(local)
+    cdev = adist.comm_device("cuda")   # where this process group's collectives run
 
     scene = amvpt.load_file(os.path.join(REPO, "scenes", scene_file), **cfg)
     sd, vd, p = scene.describe(0, 0, 0)
@@ -191,7 +197,7 @@ def main():
             dev.render_ex(vd, p, film.data_ptr(), lanes=amvpt.LaneSet(band[0], band[1], 0, 0, 0, 0), stream=stream,
                           counters=cb, exchange=exchange)
             own_ms = sum(cb.as_dict()["kernel_ms"].values())
-            t = torch.tensor([own_ms], dtype=torch.float64, device="cuda")
+            t = torch.tensor([own_ms], dtype=torch.float64, device=cdev)
             ts = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(ts, t)
             shard_ms = [float(x.item()) for x in ts]
@@ -216,7 +222,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -286,7 +292,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": world if backend != "gloo" else torch.cuda.device_count(),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -295,6 +301,10 @@ def main():
             "chunk_streams": 1 if args.one_stream else "auto (up to 4 for the per-depth wavefront suffix of BVH scenes)",
             "rmse_vs_oracle": rmse,
             "vs_baseline": None,
+            **({"ranks": world, "dist_backend": backend,
+                "note": "rehearsal: %d ranks share %d device(s) over gloo (host-staged collectives); a check of the "
+                        "multi-rank path, not a measurement" % (world, torch.cuda.device_count())}
+               if backend == "gloo" and world > 1 else {}),
             "dtype": "f32",
             "data": "synthetic (%s on a %dx%d grid sensor; no external assets)" % (
                 {"veach_grid.xml": "Veach-MIS-class scene: 4 GGX rough-conductor plates, 4 sphere lights",

@@ -25,6 +25,16 @@ Three partitions are provided:
 """
 
 
+def comm_device(device=None):
+    """The device collectives run on: `device` under RCCL ("nccl"), the CPU under gloo.  gloo moves host
+    buffers only, so a gloo process group over GPU renders (several ranks rehearsing the multi-GPU path on
+    one device: bench.py's AMVPT_DIST_BACKEND=gloo) stages every collective's tensors through the host."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+        return "cpu"
+    return device
+
+
 def pass_shard(params, rank, world, plan):
     """Params for `rank`'s share of a world * spp frame. `plan` = amvpt.plan(params)."""
     spp, spp_pp, n_passes, _ = plan
@@ -86,7 +96,7 @@ def count_exchange(device=None):
     def fn(local):
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return 0, local
-        t = torch.tensor([local], dtype=torch.int64, device=device)
+        t = torch.tensor([local], dtype=torch.int64, device=comm_device(device))
         out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
         dist.all_gather(out, t)
         counts = [int(o.item()) for o in out]
@@ -95,10 +105,17 @@ def count_exchange(device=None):
 
 
 def reduce_film(film, dst=0):
-    """Sum the ranks' RGBW ImageBlocks on `dst` (RCCL over xGMI on GPUs, gloo on CPU)."""
+    """Sum the ranks' RGBW ImageBlocks on `dst` (RCCL over xGMI on GPUs, gloo on CPU; a GPU film under
+    gloo goes through the host, comm_device)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(film, dst=dst)
+        if film.is_cuda and comm_device(film.device) == "cpu":
+            t = film.cpu()
+            dist.reduce(t, dst=dst)
+            if dist.get_rank() == dst:
+                film.copy_(t)
+        else:
+            dist.reduce(film, dst=dst)
     return film
 
 
@@ -195,7 +212,8 @@ def run_exchange(device=None):
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return exclusive_prefix(begins, counts, begins)
         world = dist.get_world_size()
-        n = torch.tensor([len(begins)], dtype=torch.int64, device=device)
+        dev = comm_device(device)
+        n = torch.tensor([len(begins)], dtype=torch.int64, device=dev)
         ns = [torch.zeros_like(n) for _ in range(world)]
         dist.all_gather(ns, n)
         m = max(1, max(int(x.item()) for x in ns))
@@ -204,7 +222,7 @@ def run_exchange(device=None):
         if begins:
             buf[:len(begins), 0] = torch.tensor(begins, dtype=torch.int64)
             buf[:len(begins), 1] = torch.tensor(counts, dtype=torch.int64)
-        buf = buf.to(device) if device else buf
+        buf = buf.to(dev) if dev else buf
         outs = [torch.zeros_like(buf) for _ in range(world)]
         dist.all_gather(outs, buf)
         allr = torch.cat(outs).cpu().numpy()
@@ -236,18 +254,19 @@ def gather_windows(window_film, window, overflow, quilt, windows, dst=0):
     rank = dist.get_rank() if multi else 0
     world = dist.get_world_size() if multi else 1
     idx, val = overflow_entries(overflow)
+    dev = comm_device(window_film.device) if multi else window_film.device   # gloo: through the host
     if multi:
-        n = torch.tensor([idx.numel()], dtype=torch.int64, device=window_film.device)
+        n = torch.tensor([idx.numel()], dtype=torch.int64, device=dev)
         ns = [torch.zeros_like(n) for _ in range(world)]
         dist.all_gather(ns, n)
         counts = [int(x.item()) for x in ns]
     else:
         counts = [idx.numel()]
     if rank != dst:
-        ops = [dist.P2POp(dist.isend, window_film.contiguous(), dst)]
+        ops = [dist.P2POp(dist.isend, window_film.contiguous().to(dev), dst)]
         if counts[rank]:
-            ops.append(dist.P2POp(dist.isend, idx.contiguous(), dst))
-            ops.append(dist.P2POp(dist.isend, val.contiguous(), dst))
+            ops.append(dist.P2POp(dist.isend, idx.contiguous().to(dev), dst))
+            ops.append(dist.P2POp(dist.isend, val.contiguous().to(dev), dst))
         for w in dist.batch_isend_irecv(ops):
             w.wait()
         return None
@@ -259,12 +278,12 @@ def gather_windows(window_film, window, overflow, quilt, windows, dst=0):
         if r == rank:
             continue
         x0, y0, w, h = windows[r]
-        t = torch.empty((h, w, C), dtype=quilt.dtype, device=quilt.device)
+        t = torch.empty((h, w, C), dtype=quilt.dtype, device=dev)
         recv[r] = [t]
         ops.append(dist.P2POp(dist.irecv, t, r))
         if counts[r]:
-            ti = torch.empty(counts[r], dtype=torch.int64, device=quilt.device)
-            tv = torch.empty(counts[r], dtype=torch.float32, device=quilt.device)
+            ti = torch.empty(counts[r], dtype=torch.int64, device=dev)
+            tv = torch.empty(counts[r], dtype=torch.float32, device=dev)
             recv[r] += [ti, tv]
             ops += [dist.P2POp(dist.irecv, ti, r), dist.P2POp(dist.irecv, tv, r)]
     if ops:
@@ -278,7 +297,7 @@ def gather_windows(window_film, window, overflow, quilt, windows, dst=0):
             if idx.numel():
                 flat.index_add_(0, idx.to(quilt.device), val.to(quilt.device))
         else:
-            quilt[y0:y0 + h, x0:x0 + w] += recv[r][0]
+            quilt[y0:y0 + h, x0:x0 + w] += recv[r][0].to(quilt.device)
             if counts[r]:
-                flat.index_add_(0, recv[r][1], recv[r][2])
+                flat.index_add_(0, recv[r][1].to(quilt.device), recv[r][2].to(quilt.device))
     return quilt
