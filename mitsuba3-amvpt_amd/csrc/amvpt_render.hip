@@ -1604,6 +1604,13 @@ constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCe
 #define AMVPT_BIN_UNROLL 4   /* entries per thread in flight in k_bin_sort's passes (one 1024-thread block per partition) */
 #endif
 constexpr uint32_t kBinUnroll = AMVPT_BIN_UNROLL;
+#ifndef AMVPT_BIN_PREFETCH
+/* 1: k_bin_sort's staged scatter loads the next batch during this one's run writes.  Neutral (r06af: k_bin 50.4 ms
+ * either way on the mesh), so 0.  What did pay in that change is the entries as named structs instead of arrays
+ * indexed by an unrolled loop, which the compiler had promoted to 32 KB of LDS (each load then waited for its LDS
+ * copy): k_bin 57.7 -> 50.4 ms per mesh frame (r06ad vs r06af) */
+#define AMVPT_BIN_PREFETCH 0
+#endif
 #ifndef AMVPT_BIN_STAGE
 #define AMVPT_BIN_STAGE 1   /* k_bin_sort stages each batch in LDS and writes runs of one bin: sort 54.0 -> 50.3 ms,
                                      * mesh 857 -> 876 Msamples/s (r05h); 0: one scattered write per entry (A/B) */
@@ -1931,19 +1938,32 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
     __shared__ float2 sgb[kNee && AMVPT_NEE_CARRY ? kStage : 1];
     __shared__ uint16_t skey[kStage];
     __shared__ uint32_t lh[kBins], lbase[kBins];
+    /* the batch's global loads (rays, producer keys, carried green / blue): with AMVPT_BIN_PREFETCH the next batch's
+     * are issued before this batch's run writes, so their latency overlaps them (one block per CU leaves nothing
+     * else to hide it).  Two entries per thread as named structs, not arrays: an array indexed by the unrolled
+     * entry loop is promoted to LDS before the loop is unrolled, and the load then waits for its LDS copy. */
+    struct Ent { float4 a, b; uint32_t k, r; float2 g; };
+    auto load = [&](uint32_t e, Ent &x) {
+        const uint32_t i = pbase + min(e, count - 1u);
+        x.a = src[0][i]; x.b = src[1][i];
+        if (!kFromRays) x.k = keys[i];
+        if (nee_carry) x.g = B.nee_gb[i];
+    };
+    Ent x0, x1, n0, n1;
+    x0.k = x1.k = n0.k = n1.k = 0u;
+    x0.g = x1.g = n0.g = n1.g = make_float2(0.f, 0.f);
+    if (AMVPT_BIN_PREFETCH && count > 0) { load(threadIdx.x, x0); load(threadIdx.x + kBinBlock, x1); }
     for (uint32_t b0 = 0; b0 < count; b0 += kStage) {
         const uint32_t n = min(kStage, count - b0);
-        for (uint32_t k = threadIdx.x; k < kBins; k += kBinBlock) lh[k] = 0u;
+        for (uint32_t q = threadIdx.x; q < kBins; q += kBinBlock) lh[q] = 0u;
         __syncthreads();
-        float4 a[2], b[2];
-        uint32_t k[2], r[2];
-#pragma unroll
-        for (uint32_t u = 0; u < 2; ++u) {
-            const uint32_t e = b0 + threadIdx.x + u * kBinBlock, i = pbase + min(e, count - 1u);
-            a[u] = src[0][i]; b[u] = src[1][i];
-            k[u] = kFromRays ? bin_key(P, mk(a[u].x, a[u].y, a[u].z), mk(a[u].w, b[u].x, b[u].y)) : keys[i];
-            r[u] = e < count ? atomicAdd(&lh[k[u]], 1u) : 0u;
-        }
+        if (!AMVPT_BIN_PREFETCH) { load(b0 + threadIdx.x, x0); load(b0 + threadIdx.x + kBinBlock, x1); }
+        auto rank = [&](Ent &x, uint32_t e) {
+            if (kFromRays) x.k = bin_key(P, mk(x.a.x, x.a.y, x.a.z), mk(x.a.w, x.b.x, x.b.y));
+            x.r = e < count ? atomicAdd(&lh[x.k], 1u) : 0u;
+        };
+        rank(x0, b0 + threadIdx.x);
+        rank(x1, b0 + threadIdx.x + kBinBlock);
         __syncthreads();
         /* the batch's run of each bin: its position in the batch (a scan of lh) and in the partition */
         for (uint32_t q = threadIdx.x; q < kBins; q += kBinBlock) {
@@ -1973,17 +1993,20 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
             run2 += vv[q];
         }
         __syncthreads();
-#pragma unroll
-        for (uint32_t u = 0; u < 2; ++u) {
-            const uint32_t e = b0 + threadIdx.x + u * kBinBlock;
+        auto stage = [&](const Ent &x, uint32_t e) {
             if (e < count) {
-                const uint32_t sp = lh[k[u]] + r[u], i = pbase + e;
-                stg[2 * sp] = a[u];
-                stg[2 * sp + 1] = nee_carry ? b[u] : kNee ? make_float4(b[u].x, b[u].y, b[u].z, bitsf(i)) : make_float4(b[u].x, b[u].y, bitsf(i), 0.f);
-                if (nee_carry) sgb[sp] = B.nee_gb[i];
-                skey[sp] = (uint16_t) k[u];
+                const uint32_t sp = lh[x.k] + x.r, i = pbase + e;
+                stg[2 * sp] = x.a;
+                stg[2 * sp + 1] = nee_carry ? x.b : kNee ? make_float4(x.b.x, x.b.y, x.b.z, bitsf(i)) : make_float4(x.b.x, x.b.y, bitsf(i), 0.f);
+                if (nee_carry) sgb[sp] = x.g;
+                skey[sp] = (uint16_t) x.k;
             }
-        }
+        };
+        stage(x0, b0 + threadIdx.x);
+        stage(x1, b0 + threadIdx.x + kBinBlock);
+        /* the next batch's loads (registers of their own, live across the run writes) */
+        const bool more = AMVPT_BIN_PREFETCH && b0 + kStage < count;
+        if (more) { load(b0 + kStage + threadIdx.x, n0); load(b0 + kStage + threadIdx.x + kBinBlock, n1); }
         __syncthreads();
         for (uint32_t sp = threadIdx.x; sp < n; sp += kBinBlock) {
             const uint32_t q = skey[sp], j = pbase + lbase[q] + (sp - lh[q]);
@@ -1991,6 +2014,7 @@ __global__ void __launch_bounds__(kBinBlock) k_bin_sort(KParams P, Bufs B) {
             B.sray[0][2 * (size_t) j + 1] = stg[2 * sp + 1];
             if (nee_carry) B.sgb[j] = sgb[sp];
         }
+        if (more) { x0 = n0; x1 = n1; }
         __syncthreads();
     }
 #else
