@@ -1192,6 +1192,16 @@ AD float union_weight(const FilterCoeffs &F, float r, int x0, int cell, int lo, 
     const float w = gaussian_eval(F, r + (float) (cell - x0));
     return (cell >= lo && cell < hi) ? w : 0.f;
 }
+#ifndef AMVPT_SPLAT_PKW
+/* 1: the row splat evaluates its union weights two at a time with packed-f32 operations (gaussian_eval2: the same
+ * bits); 0: one gaussian_eval per weight (A/B) */
+#define AMVPT_SPLAT_PKW 1
+#endif
+/* union_weight of cells a and b (packed evaluation) */
+AD f2v_t union_weight2(const FilterCoeffs &F, float r, int x0, int a, int b, int lo, int hi) {
+    const f2v_t w = gaussian_eval2(F, f2v_t{r + (float) (a - x0), r + (float) (b - x0)});
+    return f2v_t{(a >= lo && a < hi) ? w.x : 0.f, (b >= lo && b < hi) ? w.y : 0.f};
+}
 /* The row splat runs for the default Gaussian only (rfilter stddev 0.5, the reference's default,
  * gaussian.cpp): its coefficients -- exactly what gaussian_coeffs(0.5) computes on the host, checked
  * there bit for bit before the row splat is chosen -- are compile-time literals, so every Estrin step is
@@ -1260,19 +1270,34 @@ AD void row_put_win(const KParams &P, float *film, WinT *const wbase, const Win 
          * straight-line code, not a branch per evaluation */
         const FilterCoeffs F = default_filter();
         float wx[6];
+#if AMVPT_SPLAT_PKW
+#pragma unroll
+        for (int c = 0; c < 6; c += 2) {
+            const f2v_t w = union_weight2(F, f.rx, f.x0, ux0 + c, ux0 + c + 1, x0c, x1);
+            wx[c] = w.x;
+            wx[c + 1] = w.y;
+        }
+        if (u5) wx[5] = 0.f;
+#else
 #pragma unroll
         for (int c = 0; c < 5; ++c) wx[c] = union_weight(F, f.rx, f.x0, ux0 + c, x0c, x1);
         wx[5] = 0.f;
         if (!u5) wx[5] = union_weight(F, f.rx, f.x0, ux0 + 5, x0c, x1);
+#endif
         WinT *const wch = wbase + ch * wn.plane;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
             /* row position r + 3 h holds union row r + 3 (h ^ b2); the quad shares b2 */
             float Ky[2], B1y[2], B2y[2], B3y[2];
             /* union rows r and r + 3 (lane-uniform), row 5 skipped when every fast row of the wave fits 5 */
+#if AMVPT_SPLAT_PKW
+            const f2v_t wyAB = union_weight2(F, f.ry, f.y0, uy0 + r, uy0 + r + 3, y0c, y1);
+            const float wyA = wyAB.x, wyB = (r < 2 || !u5r) ? wyAB.y : 0.f;
+#else
             const float wyA = union_weight(F, f.ry, f.y0, uy0 + r, y0c, y1);
             float wyB = 0.f;
             if (r < 2 || !u5r) wyB = union_weight(F, f.ry, f.y0, uy0 + r + 3, y0c, y1);
+#endif
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const float wy = (h ^ b2) ? wyB : wyA;
@@ -1606,9 +1631,9 @@ constexpr uint32_t kBinCellBits = AMVPT_BIN_CELL_BITS, kBins = 8u << (3 * kBinCe
 constexpr uint32_t kBinUnroll = AMVPT_BIN_UNROLL;
 #ifndef AMVPT_BIN_PREFETCH
 /* 1: k_bin_sort's staged scatter loads the next batch during this one's run writes.  Neutral (r06af: k_bin 50.4 ms
- * either way on the mesh), so 0.  What did pay in that change is the entries as named structs instead of arrays
- * indexed by an unrolled loop, which the compiler had promoted to 32 KB of LDS (each load then waited for its LDS
- * copy): k_bin 57.7 -> 50.4 ms per mesh frame (r06ad vs r06af) */
+ * either way on one box), so 0.  The same change holds the entries in named structs instead of arrays indexed by an
+ * unrolled loop, which the compiler had promoted to 32 KB of LDS (each load then waited for its LDS copy): k_bin
+ * 57.8 -> 56.9 ms per mesh frame on one box (r06ah; k_bin differs by up to 7 ms between boxes) */
 #define AMVPT_BIN_PREFETCH 0
 #endif
 #ifndef AMVPT_BIN_STAGE
