@@ -294,6 +294,24 @@ AD float gaussian_eval(const FilterCoeffs &f, float x) {
     float x16 = x8 * x8;
     return vmax(fmadd(x16, w1, w0), 0.f);
 }
+/* gaussian_eval at two arguments as packed-f32 operations (v_pk_mul_f32 / v_pk_fma_f32 are per-element IEEE, so
+ * each element is gaussian_eval's value bit for bit): the row splat's filter weights, two per instruction */
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+AD f2v_t gaussian_eval2(const FilterCoeffs &f, f2v_t x) {
+    const f2v_t x2 = x * x;
+    const float *c = f.c;
+    auto pf = [](f2v_t a, f2v_t b, f2v_t d) { return __builtin_elementwise_fma(a, b, d); };
+    const f2v_t r0 = pf(x2, (f2v_t) c[1], (f2v_t) c[0]), r1 = pf(x2, (f2v_t) c[3], (f2v_t) c[2]),
+                r2 = pf(x2, (f2v_t) c[5], (f2v_t) c[4]), r3 = pf(x2, (f2v_t) c[7], (f2v_t) c[6]),
+                r4 = pf(x2, (f2v_t) c[9], (f2v_t) c[8]);
+    const f2v_t x4 = x2 * x2;
+    const f2v_t q0 = pf(x4, r1, r0), q1 = pf(x4, r3, r2), q2 = r4;
+    const f2v_t x8 = x4 * x4;
+    const f2v_t w0 = pf(x8, q1, q0), w1 = q2;
+    const f2v_t x16 = x8 * x8;
+    const f2v_t v = pf(x16, w1, w0);
+    return f2v_t{vmax(v.x, 0.f), vmax(v.y, 0.f)};
+}
 
 /* Warps (warp.h) */
 AD void disk_concentric(float u, float v, float &ox, float &oy) {
