@@ -1194,8 +1194,9 @@ AD float union_weight(const FilterCoeffs &F, float r, int x0, int cell, int lo, 
 }
 #ifndef AMVPT_SPLAT_PKW
 /* 1: the row splat evaluates its union weights two at a time with packed-f32 operations (gaussian_eval2: the same
- * bits); 0: one gaussian_eval per weight (A/B) */
-#define AMVPT_SPLAT_PKW 1
+ * bits).  Slower (r06ai: splat 78.3 -> 81.7 ms at M, 320 -> 338 ms at C3 -- the scalar form folds every coefficient
+ * into v_fmamk / v_fmaak literals, the packed one moves them through registers), so 0: one gaussian_eval per weight */
+#define AMVPT_SPLAT_PKW 0
 #endif
 /* union_weight of cells a and b (packed evaluation) */
 AD f2v_t union_weight2(const FilterCoeffs &F, float r, int x0, int a, int b, int lo, int hi) {
