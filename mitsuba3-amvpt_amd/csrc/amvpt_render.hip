@@ -3566,6 +3566,9 @@ __global__ void __launch_bounds__(prim_block<G>(), AMVPT_PRIM_WAVES) k_mv_primar
 #ifndef AMVPT_SPLAT_SKIP
 #define AMVPT_SPLAT_SKIP 1   /* skip views without a valid splat in the wave (0: off, A/B) */
 #endif
+#ifndef AMVPT_SPLAT_BVW
+#define AMVPT_SPLAT_BVW 1   /* all-diffuse waves form Bv * pdfW inside the view loop (0: hoisted by the compiler, A/B) */
+#endif
 #ifndef AMVPT_SPLAT_WAVES
 #define AMVPT_SPLAT_WAVES 5
 #endif
@@ -3678,7 +3681,18 @@ __global__ void __launch_bounds__(kSplatBlock, AMVPT_SPLAT_WAVES) k_splat_multi(
                     asm volatile("" : "+v"(lf));
                     const C3 Dn = {(lf & 0x100u) ? qnan : 0.f, (lf & 0x200u) ? qnan : 0.f, (lf & 0x400u) ? qnan : 0.f};
                     result = k == 0 ? R0 : csel(direct && valid, csel(mget(smask, k), Dp, Dn), c3(0.f));
-                    if (mget(imask, k)) result = cfma(Bv * pdfW, indirect, result);
+                    if (mget(imask, k)) {
+#if AMVPT_SPLAT_BVW
+                        /* Bv * pdfW formed here, per view: hoisted out of the view loop, the generic instance kept the
+                         * three products in registers it did not have and spilled two of them (a scratch reload and
+                         * wait per indirect view of every all-diffuse wave) */
+                        float pw = pdfW;
+                        asm volatile("" : "+v"(pw));
+                        result = cfma(Bv * pw, indirect, result);
+#else
+                        result = cfma(Bv * pdfW, indirect, result);
+#endif
+                    }
                 } else {
                     result = res0;
                 }
