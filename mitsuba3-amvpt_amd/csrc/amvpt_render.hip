@@ -137,6 +137,9 @@ struct KParams {
     uint32_t record;      /* write per-lane splat records */
     uint32_t row_splat;   /* row-reduced splat (row_put): lanes in pixel-major order, see slot_lane */
     uint32_t tile_w;      /* != 0: row-splat slots run over 4 x 4 pixel tiles of a tile_w-pixel-wide quilt */
+    /* host-computed reciprocals of the kernel-uniform divisors the path-fetch code divides by (udiv_r; 0 when the
+     * divisor is 0): tile_w / 4, run_len, n_adapt */
+    double rcp_tpr, rcp_run_len, rcp_n_adapt;
     uint32_t adapt_pass;  /* the suffix runs paths of the adaptive wavefront (path_seq) */
     uint32_t valid_ray0;  /* !hide_emitters && environment: escaped camera rays count as valid
                            * (mvpath_multi.h:140, mvpath_single.h:98, path.cpp:114) */
@@ -1481,23 +1484,45 @@ AD void block_put(const KParams &P, float *film, SplatLds<C> &L, int buf, float 
  * use the identity map.  The map is a bijection on [0, chunk_n).
  */
 constexpr int kSplatSplit = kSplatSuper / kSplatBlock;
+constexpr uint32_t kSplatSuperLog = __builtin_ctz(kSplatSuper), kSplatSplitLog = __builtin_ctz(kSplatSplit);
+static_assert((1 << kSplatSuperLog) == kSplatSuper && (1 << kSplatSplitLog) == kSplatSplit, "powers of two");
+#ifndef AMVPT_UDIV_RCP
+/* 1: the path fetch of the suffix kernels (path_seq: slot -> lane -> TEA seed) divides by its kernel-uniform runtime
+ * divisors through host-computed f64 reciprocals (udiv_r<true>) -- the generic expansion computes each divisor's
+ * reciprocal in VGPRs up front, and the fused suffix spilled three of them (a scratch reload and wait at every path
+ * fetch).  Elsewhere (k_mv_primary's slot order, the splat) the plain division stays: there the f64 form cost more
+ * than it saved (r06am: config-M k_mv_primary 39.7 -> 41.6 ms).  The path-fetch form measured neutral (r06an: M, mesh
+ * and C5 within noise, the reloads hide behind the other waves), so 0: plain division everywhere */
+#define AMVPT_UDIV_RCP 0
+#endif
+/* n / d for a kernel-uniform d > 0, exactly: the f64 product n * fl(1/d) lies within 2^-20 of n / d (n, d < 2^32),
+ * so its truncation is the quotient or one off, and one step each way corrects it */
+template <bool kRcp = true> AD uint32_t udiv_r(uint32_t n, uint32_t d, double rcp) {
+    if (!(AMVPT_UDIV_RCP && kRcp)) return n / d;
+    uint32_t q = (uint32_t) ((double) n * rcp);
+    q -= ((uint64_t) q * d > (uint64_t) n) ? 1u : 0u;
+    q += ((uint64_t) (q + 1u) * d <= (uint64_t) n) ? 1u : 0u;
+    return q;
+}
+/* host side of udiv_r */
+inline double host_rcp(uint32_t d) { return d ? 1.0 / (double) d : 0.0; }
 /*
  * Tiled slot order (KParams::tile_w, 16 samples per pixel and pass): slot block b of 256 = the 4 x 4
  * pixel tile b of the chunk's rows (tile rows of tile_w / 4 tiles), a wave = one pixel row of the
  * tile (64 consecutive lanes), a DPP row = one pixel.  A splat block's footprints then cover ~8 x 8
  * cells instead of 20 x 5, so a block-wide window flushes fewer film cells per sample.
  */
-AD uint32_t tile_slot_lane(const KParams &P, uint32_t slot) {
+template <bool kRcp = false> AD uint32_t tile_slot_lane(const KParams &P, uint32_t slot) {
     const uint32_t b = slot >> 8, t = slot & 255u, tpr = P.tile_w >> 2;
-    const uint32_t trow = b / tpr, tcol = b - trow * tpr, pt = t >> 4;
+    const uint32_t trow = udiv_r<kRcp>(b, tpr, P.rcp_tpr), tcol = b - trow * tpr, pt = t >> 4;
     return ((trow * 4u + (pt >> 2)) * P.tile_w + tcol * 4u + (pt & 3u)) * 16u + (t & 15u);
 }
 AD uint32_t tile_lane_slot(const KParams &P, uint32_t lane) {
     const uint32_t pix = lane >> 4, y = pix / P.tile_w, x = pix - y * P.tile_w, tpr = P.tile_w >> 2;
     return (((y >> 2) * tpr + (x >> 2)) << 8) | ((((y & 3u) << 2) | (x & 3u)) << 4) | (lane & 15u);
 }
-AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
-    if (P.tile_w) return tile_slot_lane(P, slot);
+template <bool kRcp = false> AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
+    if (P.tile_w) return tile_slot_lane<kRcp>(P, slot);
     if (P.row_splat) return slot;   /* pixel-major: a 16-lane row = 16 samples of one pixel (row_put) */
     const uint32_t super = slot / (uint32_t) kSplatSuper, within = slot % (uint32_t) kSplatSuper;
     const uint32_t base = super * kSplatSuper;
@@ -1505,8 +1530,8 @@ AD uint32_t slot_lane(const KParams &P, uint32_t slot) {
     const uint32_t S = P.spp_pp;
     if (remain >= (uint32_t) kSplatSuper && P.pow2 && S >= (uint32_t) kSplatSplit && S <= (uint32_t) kSplatBlock) {
         const uint32_t h = within / (uint32_t) kSplatBlock, t = within % (uint32_t) kSplatBlock;
-        const uint32_t ppb = (uint32_t) kSplatSuper >> P.log_spp;
-        return base + (t % ppb) * S + h * (S / kSplatSplit) + t / ppb;
+        const uint32_t ppb = (uint32_t) kSplatSuper >> P.log_spp;   /* a power of two: mask and shift, not a division */
+        return base + (t & (ppb - 1u)) * S + h * (S / kSplatSplit) + (t >> (kSplatSuperLog - P.log_spp));
     }
     return slot;
 }
@@ -1521,7 +1546,7 @@ AD uint32_t lane_slot(const KParams &P, uint32_t lane) {
     if (remain >= (uint32_t) kSplatSuper && P.pow2 && S >= (uint32_t) kSplatSplit && S <= (uint32_t) kSplatBlock) {
         const uint32_t half = S / kSplatSplit, ppb = (uint32_t) kSplatSuper >> P.log_spp;
         const uint32_t p = off >> P.log_spp, smp = off & (S - 1u);
-        return base + (smp / half) * (uint32_t) kSplatBlock + (smp % half) * ppb + p;
+        return base + (smp >> (P.log_spp - kSplatSplitLog)) * (uint32_t) kSplatBlock + (smp & (half - 1u)) * ppb + p;
     }
     return lane;
 }
@@ -1699,17 +1724,17 @@ AD PathState load_state(float4 *const *q, uint32_t slot) {
 
 /* global lane (mvpath.cpp:173-190 wavefront index) of virtual index v of the render's lane set:
  * a contiguous range, or rect_h runs of run_len lanes (one per pixel row of the rectangle) */
-AD uint32_t lane_of(const KParams &P, uint64_t v) {
+template <bool kRcp = false> AD uint32_t lane_of(const KParams &P, uint64_t v) {
     if (!P.rect) return (uint32_t) (P.range_begin + v);
-    const uint32_t vv = (uint32_t) v, r = vv / P.run_len, o = vv - r * P.run_len;
+    const uint32_t vv = (uint32_t) v, r = udiv_r<kRcp>(vv, P.run_len, P.rcp_run_len), o = vv - r * P.run_len;
     return ((P.rect_y0 + r) * P.W + P.rect_x0) * P.spp_pp + o;
 }
 /* the adaptive fill (mvpath_multi.h:79-115: dr::compress, dr::repeat): index in the PASS's
  * repeated wavefront of entry j of this render's part -- entry e = j / n_adapt of the render's
  * compressed list sits at e + run_delta[run of its lane] of the pass's compressed array */
-AD uint32_t adapt_index(const KParams &P, const Bufs &B, uint32_t j) {
-    const uint32_t e = j / P.n_adapt, rep = j - e * P.n_adapt;
-    const uint32_t run = P.rect ? B.asel[e] / P.run_len : 0u;
+template <bool kRcp = false> AD uint32_t adapt_index(const KParams &P, const Bufs &B, uint32_t j) {
+    const uint32_t e = udiv_r<kRcp>(j, P.n_adapt, P.rcp_n_adapt), rep = j - e * P.n_adapt;
+    const uint32_t run = P.rect ? udiv_r<kRcp>(B.asel[e], P.run_len, P.rcp_run_len) : 0u;
     return (e + B.run_delta[run]) * P.n_adapt + rep;
 }
 
@@ -1718,8 +1743,8 @@ AD uint32_t adapt_index(const KParams &P, const Bufs &B, uint32_t j) {
  * the adaptive pass wavefront entry chunk_begin + slot with adapt_seed (k_raygen_adapt) */
 AD uint32_t path_seq(const KParams &P, const Bufs &B, uint32_t slot) {
     uint32_t v0, v1;
-    if (P.adapt_pass) tea4(P.adapt_seed, adapt_index(P, B, (uint32_t) (P.chunk_begin + slot)), v0, v1);
-    else tea4(P.seed_value, lane_of(P, P.chunk_begin + slot_lane(P, slot)), v0, v1);
+    if (P.adapt_pass) tea4(P.adapt_seed, adapt_index<true>(P, B, (uint32_t) (P.chunk_begin + slot)), v0, v1);
+    else tea4(P.seed_value, lane_of<true>(P, P.chunk_begin + slot_lane<true>(P, slot)), v0, v1);
     return v1;
 }
 
@@ -4597,6 +4622,9 @@ amvpt_status render_impl(amvpt_scene *scene, const amvpt_view_desc *views, const
         (void) hipGetLastError();
     }
     if (P.tile_w && chunk % (4ull * QW * 16ull) != 0) P.tile_w = 0;   /* chunks must hold whole tile bands */
+    P.rcp_tpr = host_rcp(P.tile_w >> 2);   /* udiv_r's reciprocals of the final divisors */
+    P.rcp_run_len = host_rcp(P.run_len);
+    P.rcp_n_adapt = host_rcp(P.n_adapt);
     P.vs_stride = (uint32_t) chunk;
     const uint32_t qcap = qcap_of(chunk);
     const uint64_t qlen = (uint64_t) qcap * kQParts;
