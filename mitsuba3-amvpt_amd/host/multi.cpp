@@ -19,6 +19,11 @@
  * streams and film buffers are cached on the host scene, keyed by the device list, and reused by the
  * next frame (amvpt_host_multi_stats counts scene creations and communicator initialisations).
  *
+ * A device list naming ONE device several times is a shared-device rehearsal of the same code (a box with one GPU):
+ * every rank renders its share on that device through its own scene copy, stream and film, and devices[0]'s thread
+ * sums the others' films / windows and overflow cells with amvpt_film_accumulate instead of RCCL (renders on one
+ * device serialise on its lane arena, so the adaptive fill's cross-rank count exchange is refused there).
+ *
  * Failure handling: the device threads meet at in-process barriers after setup and after the render;
  * the collectives run only when every device reached them healthy, so a failing device (bad id, OOM,
  * a failed render) never leaves a peer blocked inside RCCL, and a failed render aborts the count
@@ -223,6 +228,21 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
                                              " is not visible (" + std::to_string(visible) + " devices)");
         }
 
+        /* one device named n > 1 times: the shared-device rehearsal (header comment); other repeats are refused */
+        bool shared = false;
+        if (n > 1) {
+            std::vector<int> u(devices, devices + n);
+            std::sort(u.begin(), u.end());
+            const size_t distinct = (size_t) (std::unique(u.begin(), u.end()) - u.begin());
+            if (distinct == 1) shared = true;
+            else if (distinct < (size_t) n)
+                throw std::runtime_error("amvpt_host_render_multi: a device list repeats a device (only a list of one "
+                                         "device repeated is a shared-device rehearsal)");
+            if (shared && p.adaptive > 0 && p.sa_reuse)
+                throw std::runtime_error("amvpt_host_render_multi: a shared-device rehearsal cannot run the adaptive "
+                                         "fill's count exchange (renders on one device serialise on its lane arena)");
+        }
+
         /* ---- the cache: communicators, per-device scenes, streams and buffers for this device list ---- */
         std::shared_ptr<amvpt_multi_cache> &slot = amvpt_host_multi_slot(s);
         if (!slot) slot = std::make_shared<amvpt_multi_cache>();
@@ -235,7 +255,7 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
             cache->dev.resize((size_t) n);
             for (int r = 0; r < n; ++r) cache->dev[(size_t) r].device = devs[(size_t) r];
         }
-        if (cache->comms.empty() && n > 1) {
+        if (cache->comms.empty() && n > 1 && !shared) {
             cache->comms.assign((size_t) n, nullptr);
             if (ncclCommInitAll(cache->comms.data(), n, devices) != ncclSuccess) {
                 cache->comms.clear();
@@ -312,13 +332,32 @@ int amvpt_host_render_multi(amvpt_host_scene *s, uint32_t si, uint32_t seed, uin
                 return "";
             }
             case amvpt_ranks::PREPARE:   /* devices[0]: room for the peers' overflow cells */
-                if (groups && r == 0)
+                /* shared device: devices[0]'s thread reads every rank's film in COMBINE, so each one's is complete */
+                if (shared && hipStreamSynchronize(D.st) != hipSuccess) return "hipStreamSynchronize failed";
+                if (groups && r == 0 && !shared)
                     for (int q = 1; q < n; ++q)
                         if (!grow(D.recv_ov[(size_t) q], D.recv_ov_bytes[(size_t) q], 16 * std::max<uint64_t>(1, ov_count[(size_t) q])))
                             return "hipMalloc(overflow receive) failed";
                 return "";
             case amvpt_ranks::COMBINE: {   /* every device is healthy here, so every collective completes */
-                if (groups) {
+                if (shared) {
+                    /* one device: devices[0]'s thread sums the others' films (lane bands) or assembles the quilt from
+                     * every rank's window and overflow cells (view groups), as the RCCL forms below do */
+                    if (r == 0) {
+                        if (groups && hipMemsetAsync(D.quilt, 0, nfloat * sizeof(float), D.st) != hipSuccess)
+                            return "hipMemset(quilt) failed";
+                        for (int q = groups ? 0 : 1; q < n; ++q) {
+                            const DevState &E = cache->dev[(size_t) q];
+                            const auto &w = wins[(size_t) q];
+                            const amvpt_status st = groups
+                                ? amvpt_film_accumulate(D.quilt, p.film_width, p.film_height, C, E.film, w[0], w[1], w[2],
+                                                        w[3], E.ovf + 4, ov_count[(size_t) q], D.st)
+                                : amvpt_film_accumulate(D.film, p.film_width, p.film_height, C, E.film, 0, 0, p.film_width,
+                                                        p.film_height, nullptr, 0, D.st);
+                            if (st != AMVPT_OK) return amvpt_last_error();
+                        }
+                    }
+                } else if (groups) {
                     ncclComm_t comm = cache->comms[(size_t) r];
                     bool ok = ncclGroupStart() == ncclSuccess;
                     if (r == 0) {

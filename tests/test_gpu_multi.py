@@ -112,3 +112,32 @@ def test_concurrent_renders_with_different_exchanges(gpu_ready, amvpt_mod):
     for r in (0, 1):
         assert np.abs(together[r] - alone[r]).max() <= 1e-5 * np.abs(ref).max()
     assert np.abs(together[0] + together[1] - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("defines", [
+    dict(res=32, spp=32, gx=4, gy=2, reuse=8),     # one group of 8 views: lane bands
+    dict(res=32, spp=16, gx=8, gy=4, reuse=4),     # eight groups of 4: view groups, windows + overflow cells
+], ids=["lane_bands", "view_groups"])
+def test_render_multi_shared_device_rehearsal(gpu_ready, amvpt_mod, defines):
+    """VERDICT r05 "multi-device execution has never happened": a device list naming the box's one GPU several times
+    runs amvpt_host_render_multi's partitions for real -- a thread, scene copy, stream and film per rank, lane bands or
+    view-group windows with their overflow cells, the sum onto devices[0] (amvpt_film_accumulate standing in for RCCL)
+    -- and must equal render() up to the film's float-atomic summation order, with the same lane counts."""
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), **defines)
+    c1 = amvpt_mod.Counters()
+    ref = amvpt_mod.render(s, raw=True, counters=c1)
+    for devs in ([0, 0], [0, 0, 0, 0]):
+        c2 = amvpt_mod.Counters()
+        out = amvpt_mod.render_multi(s, devs, raw=True, counters=c2)
+        assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max(), devs
+        assert c1.lanes == c2.lanes and c1.view_splats == c2.view_splats and c1.vertices == c2.vertices, devs
+    img, dev = amvpt_mod.render(s), amvpt_mod.render_multi(s, [0, 0])
+    assert np.abs(dev - img).max() <= 1e-4 * max(1.0, np.abs(img).max())
+
+
+def test_render_multi_shared_device_refuses_the_adaptive_exchange(gpu_ready, amvpt_mod):
+    """The adaptive fill's count exchange needs every rank's render in flight at once, which one device's lane arena
+    does not allow: the rehearsal refuses it with a message instead of blocking."""
+    s = amvpt_mod.load_file(os.path.join(SCENES, "cbox_grid.xml"), res=32, spp=16, reuse=4, adaptive=2)
+    with pytest.raises(Exception, match="shared-device rehearsal"):
+        amvpt_mod.render_multi(s, [0, 0], raw=True)
