@@ -72,7 +72,9 @@ int amvpt_host_render_stats(amvpt_host_scene *scene, uint64_t *scene_creates, ui
  * devices[0].  The adaptive fill's per-run count exchange runs between the threads (per-call option).
  * Communicators, per-device scenes and films are cached on the scene for the next frame.  The image
  * equals amvpt_host_render's up to float summation order.  Counters: lane statistics summed, times of
- * the slowest device.
+ * the slowest device.  A list naming ONE device several times is a shared-device rehearsal (one rank per
+ * entry on that device, the films summed on it with amvpt_film_accumulate instead of RCCL; adaptive renders
+ * are refused there, their count exchange needs concurrent renders); other repeated devices are an error.
  */
 int amvpt_host_render_multi(amvpt_host_scene *scene, uint32_t sensor_index, uint32_t seed, uint32_t spp,
                             int raw, const int *devices, int n_devices, float *out_host,
